@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training samples/s (whole node) of DALL-E d_model=1024, 24 layers,
+256 text + 32x32 image tokens, bf16 data-parallel on 1/2/4/8 MI355X (BASELINE.json config 2).
+
+One process per GPU (torchrun), RCCL over xGMI. Every timed step is a full training step:
+forward + backward (fused HIP kernels), gradient all-reduce across ranks (bucketed, RCCL),
+global grad-norm clip and a LAMB optimizer update on every parameter -- i.e. the collaborative
+optimizer with ``target_batch_size`` equal to the global batch, so each step is a global step.
+
+Data: synthetic LAION-shaped pairs (256 caption ids padded with 1, 1024 VQGAN codes), random-init
+weights. ``python bench.py --gpus N --steps K --warmup W``; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from dalle_amd.config import get_config  # noqa: E402
+from dalle_amd.data.synthetic import synthetic_batch  # noqa: E402
+from dalle_amd.models.dalle import DALLE  # noqa: E402
+from dalle_amd.optim import FlatArena, LAMB8bit  # noqa: E402
+from dalle_amd.parallel.dp import GradSync  # noqa: E402
+
+BASELINE_VALUE = None  # the reference publishes no throughput numbers
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 16)), help="per-GPU micro-batch")
+    ap.add_argument("--model", default="bench24")
+    ap.add_argument("--optim-bits", type=int, default=32, choices=[8, 32])
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    cfg = get_config(args.model)
+    torch.manual_seed(1234)
+    model = DALLE(cfg).to(device)
+    arena = FlatArena(model.parameters(), device=device)
+    if world > 1:  # identical init on every rank
+        dist.broadcast(arena.data, 0)
+    no_decay = ["bias", "LayerNorm.weight"]  # task.py:138-150 (only biases match dalle-pytorch names)
+    named = list(model.named_parameters())
+    groups = [
+        {"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": 0.045},
+        {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0},
+    ]
+    opt = LAMB8bit(groups, lr=0.0025, betas=(0.9, 0.96), eps=1e-6, weight_decay=0.045, clamp_value=10000.0,
+                   max_grad_norm=4.0, reuse_grad_buffers=True, optim_bits=args.optim_bits, arena=arena)
+    sync = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype)
+
+    gen = torch.Generator().manual_seed(1000 + rank)
+    batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
+                               cfg.num_image_tokens, gen, device=device) for _ in range(4)]
+
+    def step(i):
+        b = batches[i % len(batches)]
+        arena.zero_grad()
+        loss = model(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
+        loss.backward()
+        sync.all_reduce()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    samples = args.batch * world * args.steps
+    value = samples / elapsed
+    ms = elapsed / args.steps * 1000
+    if rank == 0:
+        tflops = cfg.train_flops_per_sample() * value / world / 1e12
+        print(json.dumps({
+            "metric": "training samples/sec (whole node), DALL-E d_model=1024 at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
+            "dtype": "bf16",
+            "data": "synthetic LAION-shaped pairs (256 caption ids + 32x32 VQGAN codes), random-init weights",
+            "config": {"model": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
+                       "preset": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "seq_len": cfg.seq_len, "parallelism": f"dp{world}",
+                       "optimizer": f"LAMB ({args.optim_bits}-bit moments) + global clip 4.0",
+                       "grad_allreduce_dtype": args.grad_dtype},
+            "model_tflops_per_gpu": round(tflops, 1),
+            "loss": round(final_loss, 4),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

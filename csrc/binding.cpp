@@ -1,0 +1,279 @@
+// PyTorch bindings for the dalle_amd HIP kernels (module dalle_amd._C).
+// Every op checks device, dtype, contiguity and the shapes its kernel's grid assumes BEFORE launching
+// (a mis-sized launch of a hand-written kernel can fault the GPU).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels/geom.h"
+
+namespace dalle {
+
+void attn_fwd(const void*, const void*, const void*, void*, float*, const AttnGeom&, int, hipStream_t);
+void attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*, void*, void*,
+              void*, const AttnGeom&, int, hipStream_t);
+void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
+void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
+bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t);
+bool ln_shift_bwd(const float*, const float*, const void*, const float*, const float*, float*, float*, float*, const ShiftGeom&,
+                  int, int, hipStream_t);
+void geglu_fwd(const void*, void*, long, int, hipStream_t);
+void geglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
+void scale_residual(float*, const void*, const float*, long, int, hipStream_t);
+void scale_residual_bwd(const float*, const void*, const float*, void*, float*, long, int, hipStream_t);
+void nonfinite(const float*, long, int*, hipStream_t);
+void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
+void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
+void lamb_step(const float*, float*, const float*, float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*,
+               const float*, const int*, const long*, const long*, const int*, const float*, const float*, const float*,
+               float*, float*, float*, float*, int, long, float, float, float, float, int, hipStream_t);
+}  // namespace dalle
+
+using torch::Tensor;
+
+static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " has wrong dtype")
+#define CHECK_IN(x, dt) CHECK_CUDA(x); CHECK_CONTIG(x); CHECK_DT(x, dt)
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  TORCH_CHECK((1 << l) == v, "image side must be a power of two");
+  return l;
+}
+
+static dalle::AttnGeom make_attn_geom(int T, int S, int n, int K, int H, int pattern) {
+  dalle::AttnGeom g;
+  g.T = T;
+  g.Tp = (T + 31) / 32 * 32;
+  g.S = S;
+  g.logS = ilog2(S);
+  g.I = S * S;
+  g.Np = g.Tp + g.I;
+  g.n = n;
+  g.K = K;
+  g.H = H;
+  g.pattern = pattern;
+  TORCH_CHECK(g.I % 32 == 0, "image grid must be a multiple of 32 tokens");
+  TORCH_CHECK(n == T + g.I - 1, "sequence length must be text_len + image_seq_len - 1");
+  return g;
+}
+
+// ---------------------------------------------------------------------------------------------
+std::vector<Tensor> ln_shift_fwd(Tensor x, Tensor w, Tensor b, int64_t T, int64_t S, bool shift, double eps) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(b, torch::kFloat32);
+  TORCH_CHECK(x.dim() == 3, "x must be (B, n, D)");
+  const int B = x.size(0), n = x.size(1), D = x.size(2);
+  TORCH_CHECK(w.numel() == D && b.numel() == D);
+  if (shift) TORCH_CHECK(n >= T && n - T <= S * S && D % 4 == 0, "token shift geometry mismatch");
+  auto y = torch::empty({B, n, D}, x.options().dtype(torch::kBFloat16));
+  auto mean = torch::empty({B * n}, x.options());
+  auto rstd = torch::empty({B * n}, x.options());
+  dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
+  bool ok = dalle::ln_shift_fwd(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+                                mean.data_ptr<float>(), rstd.data_ptr<float>(), g, B * n, D, (float)eps, cur_stream());
+  TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
+  return {y, mean, rstd};
+}
+
+std::vector<Tensor> ln_shift_bwd(Tensor x, Tensor w, Tensor dy, Tensor mean, Tensor rstd, int64_t T, int64_t S, bool shift) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(dy, torch::kBFloat16);
+  CHECK_IN(mean, torch::kFloat32); CHECK_IN(rstd, torch::kFloat32);
+  const int B = x.size(0), n = x.size(1), D = x.size(2);
+  TORCH_CHECK(dy.sizes() == x.sizes() && mean.numel() == B * n && rstd.numel() == B * n);
+  auto dx = torch::empty_like(x);
+  auto dw = torch::zeros({D}, x.options());
+  auto db = torch::zeros({D}, x.options());
+  dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
+  bool ok = dalle::ln_shift_bwd(x.data_ptr<float>(), w.data_ptr<float>(), dy.data_ptr(), mean.data_ptr<float>(),
+                                rstd.data_ptr<float>(), dx.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(), g,
+                                B * n, D, cur_stream());
+  TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
+  return {dx, dw, db};
+}
+
+// ---------------------------------------------------------------------------------------------
+static dalle::RopeGeom make_rope_geom(int T, int S, int n, int H, bool col_major) {
+  dalle::RopeGeom g;
+  g.T = T;
+  g.Tp = (T + 31) / 32 * 32;
+  g.S = S;
+  g.logS = ilog2(S);
+  g.n = n;
+  g.Np = g.Tp + S * S;
+  g.H = H;
+  g.col_major = col_major ? 1 : 0;
+  TORCH_CHECK(n == T + S * S - 1, "rope: sequence length mismatch");
+  return g;
+}
+
+std::vector<Tensor> rope_fwd(Tensor qkv, Tensor cosT, Tensor sinT, int64_t T, int64_t S, int64_t H, bool col_major, double qscale) {
+  CHECK_IN(qkv, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  const int B = qkv.size(0), n = qkv.size(1);
+  TORCH_CHECK(qkv.size(2) == 3 * H * 64, "rope: dim_head must be 64");
+  TORCH_CHECK(cosT.size(0) >= n && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes());
+  auto g = make_rope_geom(T, S, n, H, col_major);
+  auto opts = qkv.options();
+  auto q = torch::empty({B * H, g.Np, 64}, opts);
+  auto k = torch::empty({B * H, g.Np, 64}, opts);
+  auto v = torch::empty({B * H, g.Np, 64}, opts);
+  dalle::rope_fwd(qkv.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(), q.data_ptr(), k.data_ptr(), v.data_ptr(), g,
+                  B * H, (float)qscale, cur_stream());
+  return {q, k, v};
+}
+
+Tensor rope_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cosT, Tensor sinT, int64_t B, int64_t T, int64_t S, int64_t H, int64_t n,
+                bool col_major, double qscale) {
+  CHECK_IN(dq, torch::kBFloat16); CHECK_IN(dk, torch::kBFloat16); CHECK_IN(dv, torch::kBFloat16);
+  CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  auto g = make_rope_geom(T, S, n, H, col_major);
+  TORCH_CHECK(dq.size(0) == B * H && dq.size(1) == g.Np && dq.size(2) == 64);
+  TORCH_CHECK(dk.sizes() == dq.sizes() && dv.sizes() == dq.sizes());
+  auto dqkv = torch::empty({B, n, 3 * H * 64}, dq.options());
+  dalle::rope_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(),
+                  g, B, (float)qscale, cur_stream());
+  return dqkv;
+}
+
+// ---------------------------------------------------------------------------------------------
+std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, int64_t B, int64_t T, int64_t S, int64_t n, int64_t K, int64_t H,
+                             int64_t pattern) {
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(k, torch::kBFloat16); CHECK_IN(v, torch::kBFloat16);
+  auto g = make_attn_geom(T, S, n, K, H, pattern);
+  TORCH_CHECK(q.size(0) == B * H && q.size(1) == g.Np && q.size(2) == 64, "attn: q must be (B*H, Np, 64)");
+  TORCH_CHECK(k.sizes() == q.sizes() && v.sizes() == q.sizes());
+  TORCH_CHECK(pattern >= 0 && pattern <= 3);
+  auto out = torch::empty({B, n, H * 64}, q.options());
+  auto lse = torch::empty({B * H, g.Np}, q.options().dtype(torch::kFloat32));
+  dalle::attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), g, B * H, cur_stream());
+  return {out, lse};
+}
+
+std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, int64_t B, int64_t T, int64_t S,
+                             int64_t n, int64_t K, int64_t H, int64_t pattern) {
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(k, torch::kBFloat16); CHECK_IN(v, torch::kBFloat16);
+  CHECK_IN(out, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16); CHECK_IN(lse, torch::kFloat32);
+  auto g = make_attn_geom(T, S, n, K, H, pattern);
+  TORCH_CHECK(q.size(0) == B * H && q.size(1) == g.Np && q.size(2) == 64);
+  TORCH_CHECK(k.sizes() == q.sizes() && v.sizes() == q.sizes());
+  TORCH_CHECK(out.size(0) == B && out.size(1) == n && out.size(2) == H * 64 && dout.sizes() == out.sizes());
+  TORCH_CHECK(lse.numel() == B * H * g.Np);
+  auto do_st = torch::empty_like(q);
+  auto delta = torch::empty({B * H, g.Np}, lse.options());
+  auto dq = torch::empty_like(q);
+  auto dk = torch::empty_like(q);
+  auto dv = torch::empty_like(q);
+  dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                  do_st.data_ptr(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), g, B * H,
+                  cur_stream());
+  return {dq, dk, dv};
+}
+
+// ---------------------------------------------------------------------------------------------
+Tensor geglu_fwd(Tensor h) {
+  CHECK_IN(h, torch::kBFloat16);
+  const long F2 = h.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "geglu: hidden must be a multiple of 16");
+  const long M = h.numel() / F2;
+  auto sizes = h.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto out = torch::empty(sizes, h.options());
+  dalle::geglu_fwd(h.data_ptr(), out.data_ptr(), M, F2 / 2, cur_stream());
+  return out;
+}
+
+Tensor geglu_bwd(Tensor h, Tensor dout) {
+  CHECK_IN(h, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16);
+  const long F2 = h.size(-1);
+  const long M = h.numel() / F2;
+  TORCH_CHECK(dout.numel() == M * F2 / 2);
+  auto dh = torch::empty_like(h);
+  dalle::geglu_bwd(h.data_ptr(), dout.data_ptr(), dh.data_ptr(), M, F2 / 2, cur_stream());
+  return dh;
+}
+
+void scale_residual_(Tensor x, Tensor y, Tensor scale) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
+  const long D = x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && y.numel() == x.numel() && scale.numel() == D);
+  dalle::scale_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), x.numel() / D, D, cur_stream());
+}
+
+std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale) {
+  CHECK_IN(g, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
+  const long D = g.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 2048 && y.numel() == g.numel() && scale.numel() == D);
+  auto dy = torch::empty(g.sizes(), y.options());
+  auto dscale = torch::zeros({D}, g.options());
+  dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), dscale.data_ptr<float>(),
+                            g.numel() / D, D, cur_stream());
+  return {dy, dscale};
+}
+
+Tensor nonfinite(Tensor x) {
+  CHECK_IN(x, torch::kFloat32);
+  auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
+  dalle::nonfinite(x.data_ptr<float>(), x.numel(), flag.data_ptr<int>(), cur_stream());
+  return flag;
+}
+
+Tensor xent_fwd_bwd_(Tensor logits, Tensor labels, double gscale) {
+  CHECK_IN(logits, torch::kBFloat16); CHECK_IN(labels, torch::kInt64);
+  TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0));
+  auto loss = torch::empty({logits.size(0)}, logits.options().dtype(torch::kFloat32));
+  dalle::xent_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), logits.size(0), logits.size(1),
+                      (float)gscale, cur_stream());
+  return loss;
+}
+
+// ---------------------------------------------------------------------------------------------
+void lamb_grad_norm(Tensor g, Tensor partial, double max_norm, Tensor coef, Tensor norm) {
+  CHECK_IN(g, torch::kFloat32); CHECK_IN(partial, torch::kFloat32);
+  TORCH_CHECK(g.numel() % 4096 == 0 && partial.numel() >= g.numel() / 4096);
+  dalle::lamb_grad_norm(g.data_ptr<float>(), g.numel(), partial.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(),
+                        norm.data_ptr<float>(), cur_stream());
+}
+
+void lamb_step(Tensor p, Tensor g, Tensor delta, Tensor q1, Tensor q2, Tensor absmax1, Tensor absmax2, Tensor m32, Tensor v32,
+               Tensor code1, Tensor code2, Tensor block_tensor, Tensor tstart, Tensor tsize, Tensor tmode, Tensor twd, Tensor tlr,
+               Tensor coef, Tensor partial, Tensor trust, Tensor wnorm, Tensor snorm, double beta1, double beta2, double eps,
+               double clamp_value, bool use_clip) {
+  CHECK_IN(p, torch::kFloat32); CHECK_IN(g, torch::kFloat32); CHECK_IN(delta, torch::kFloat32);
+  CHECK_IN(q1, torch::kUInt8); CHECK_IN(q2, torch::kUInt8);
+  CHECK_IN(block_tensor, torch::kInt32); CHECK_IN(tstart, torch::kInt64); CHECK_IN(tsize, torch::kInt64);
+  const long n = p.numel();
+  TORCH_CHECK(n % 4096 == 0 && g.numel() == n && delta.numel() == n && q1.numel() == n && q2.numel() == n);
+  TORCH_CHECK(m32.numel() == n && v32.numel() == n && absmax1.numel() == n / 4096 && absmax2.numel() == n / 4096);
+  TORCH_CHECK(block_tensor.numel() == n / 4096 && partial.numel() >= 2 * (n / 4096));
+  TORCH_CHECK(code1.numel() == 256 && code2.numel() == 256);
+  const int nt = tstart.numel();
+  TORCH_CHECK(tsize.numel() == nt && tmode.numel() == nt && twd.numel() == nt && tlr.numel() == nt && trust.numel() == nt);
+  dalle::lamb_step(p.data_ptr<float>(), p.data_ptr<float>(), g.data_ptr<float>(), delta.data_ptr<float>(), q1.data_ptr<uint8_t>(),
+                   q2.data_ptr<uint8_t>(), absmax1.data_ptr<float>(), absmax2.data_ptr<float>(), m32.data_ptr<float>(),
+                   v32.data_ptr<float>(), code1.data_ptr<float>(), code2.data_ptr<float>(), block_tensor.data_ptr<int>(),
+                   (const long*)tstart.data_ptr<int64_t>(), (const long*)tsize.data_ptr<int64_t>(), tmode.data_ptr<int>(),
+                   twd.data_ptr<float>(), tlr.data_ptr<float>(), coef.data_ptr<float>(), partial.data_ptr<float>(),
+                   trust.data_ptr<float>(), wnorm.data_ptr<float>(), snorm.data_ptr<float>(), nt, n, (float)beta1, (float)beta2,
+                   (float)eps, (float)clamp_value, use_clip ? 1 : 0, cur_stream());
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "dalle_amd HIP/CDNA4 kernels (gfx950)";
+  m.def("ln_shift_fwd", &ln_shift_fwd);
+  m.def("ln_shift_bwd", &ln_shift_bwd);
+  m.def("rope_fwd", &rope_fwd);
+  m.def("rope_bwd", &rope_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("geglu_fwd", &geglu_fwd);
+  m.def("geglu_bwd", &geglu_bwd);
+  m.def("scale_residual_", &scale_residual_);
+  m.def("scale_residual_bwd", &scale_residual_bwd);
+  m.def("nonfinite", &nonfinite);
+  m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
+  m.def("lamb_grad_norm", &lamb_grad_norm);
+  m.def("lamb_step", &lamb_step);
+}

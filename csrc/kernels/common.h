@@ -1,0 +1,77 @@
+// Shared device helpers for the dalle_amd CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dalle {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef uint16_t bf16_raw;
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;
+
+__device__ __forceinline__ float bf2f(bf16_raw v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_raw f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_raw, b);
+}
+__device__ __forceinline__ float bfv2f(__bf16 v) { return (float)v; }
+
+// 8 bf16 <-> 8 floats
+__device__ __forceinline__ void unpack8(const s16x8& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f((bf16_raw)v[i]);
+}
+__device__ __forceinline__ s16x8 pack8(const float* f) {
+  s16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(f[i]);
+  return v;
+}
+__device__ __forceinline__ void unpack4(const s16x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) f[i] = bf2f((bf16_raw)v[i]);
+}
+__device__ __forceinline__ s16x4 pack4(const float* f) {
+  s16x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (short)f2bf(f[i]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == 256 (4 waves); `red` must hold >= 8 floats of LDS.
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0] + red[1] + red[2] + red[3];
+  return r;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+}  // namespace dalle

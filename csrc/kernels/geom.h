@@ -1,0 +1,25 @@
+// Launch geometry structs shared by the HIP kernels and the (host-compiled) bindings.
+#pragma once
+namespace dalle {
+struct AttnGeom {
+  int T;        // text positions incl. BOS (257)
+  int Tp;       // padded text rows (288)
+  int S;        // image side (32)
+  int logS;     // log2(S)
+  int I;        // S*S
+  int Np;       // Tp + I
+  int n;        // unpadded sequence length (1280)
+  int K;        // conv window
+  int H;        // heads
+  int pattern;  // 0 full, 1 axial_row, 2 axial_col, 3 conv_like
+};
+struct RopeGeom {
+  int T, Tp, S, logS, n, Np, H, col_major;
+};
+struct ShiftGeom {
+  int n;      // sequence length
+  int T;      // text_len (BOS + text)
+  int S;      // image side
+  int shift;  // 0 = plain LayerNorm
+};
+}  // namespace dalle

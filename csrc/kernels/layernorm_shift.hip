@@ -1,0 +1,179 @@
+// Fused PreNorm LayerNorm + PreShiftToken (SURVEY K3 + K4).
+//
+// Forward: x (rows = B*n, D) fp32 residual stream -> y bf16, where y is LN(x) after the token
+// shift: text positions take channels [0, D/2) from the previous position; image positions
+// (raster, S x S grid) take [0, D/4) from the token above and [D/4, D/2) from the token to the
+// left; missing sources are zeros. One wave per source row: it normalises its row once and scatters
+// each channel quarter to its destination row, and writes the zeros its own row is owed, so every
+// output element is written exactly once (no memset, no second pass).
+// Backward: one wave per source row gathers the shifted output grads back, then LN backward;
+// dweight / dbias are reduced per wave over a grid-stride loop and added with one fp32 atomic per
+// channel per wave.
+#include "common.h"
+#include "geom.h"
+
+namespace dalle {
+
+// destination position of channel group `grp` (0: [0,D/4), 1: [D/4,D/2), 2: [D/2,D)) of source p,
+// or -1 if dropped
+__device__ __forceinline__ int shift_dest(const ShiftGeom& g, int p, int grp) {
+  if (!g.shift || grp == 2) return p;
+  if (p < g.T) return (p + 1 < g.T) ? p + 1 : -1;
+  const int k = p - g.T;
+  if (grp == 0) return (p + g.S < g.n) ? p + g.S : -1;
+  const int col = k % g.S;
+  return (col < g.S - 1 && p + 1 < g.n) ? p + 1 : -1;
+}
+
+// source position for destination p (inverse map) or -1 (zero)
+__device__ __forceinline__ int shift_src(const ShiftGeom& g, int p, int grp) {
+  if (!g.shift || grp == 2) return p;
+  if (p < g.T) return p >= 1 ? p - 1 : -1;
+  const int k = p - g.T;
+  if (grp == 0) return (k >= g.S) ? p - g.S : -1;
+  return (k % g.S) ? p - 1 : -1;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, __bf16* __restrict__ y,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                           ShiftGeom g, int rows, float eps) {
+  constexpr int PER = D / 256;  // float4 per lane
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= rows) return;
+  const int row = wave;
+  const int b = row / g.n, p = row - b * g.n;
+  const float* xr = x + (size_t)row * D;
+  f32x4 v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = *reinterpret_cast<const f32x4*>(xr + 4 * (lane + 64 * j));
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const int grp = c < D / 4 ? 0 : (c < D / 2 ? 1 : 2);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[i] + bv[i];
+    const int gsh = (g.shift && p < g.T && grp == 1) ? 0 : grp;  // text: whole first half moves by one
+    const int dst = shift_dest(g, p, gsh);
+    if (dst >= 0) *reinterpret_cast<s16x4*>(y + ((size_t)b * g.n + dst) * D + c) = pack4(o);
+    if (gsh != 2 && g.shift && shift_src(g, p, gsh) < 0) {
+      const s16x4 z = {};
+      *reinterpret_cast<s16x4*>(y + (size_t)row * D + c) = z;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const __bf16* __restrict__ dy, const float* __restrict__ mean_in,
+                                                           const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                           float* __restrict__ dw, float* __restrict__ db, ShiftGeom g,
+                                                           int rows) {
+  constexpr int PER = D / 256;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int wave0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  float dwa[PER][4] = {}, dba[PER][4] = {};
+  for (int row = wave0; row < rows; row += nwaves) {
+    const int b = row / g.n, p = row - b * g.n;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[PER][4], gy[PER][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      const int grp = c < D / 4 ? 0 : (c < D / 2 ? 1 : 2);
+      const int gsh = (g.shift && p < g.T && grp == 1) ? 0 : grp;
+      const int dst = shift_dest(g, p, gsh);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)row * D + c);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+      float gv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (dst >= 0) unpack4(*reinterpret_cast<const s16x4*>(dy + ((size_t)b * g.n + dst) * D + c), gv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xh[j][i] = (xv[i] - mean) * rstd;
+        gy[j][i] = gv[i] * wv[i];
+        dwa[j][i] += gv[i] * xh[j][i];
+        dba[j][i] += gv[i];
+        s1 += gy[j][i];
+        s2 += gy[j][i] * xh[j][i];
+      }
+    }
+    s1 = wave_sum(s1) * (1.0f / D);
+    s2 = wave_sum(s2) * (1.0f / D);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      f32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = rstd * (gy[j][i] - s1 - xh[j][i] * s2);
+      *reinterpret_cast<f32x4*>(dx + (size_t)row * D + c) = o;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = 4 * (lane + 64 * j);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      atomicAdd(dw + c + i, dwa[j][i]);
+      atomicAdd(db + c + i, dba[j][i]);
+    }
+  }
+}
+
+// plain LayerNorm variants for the final norm (no shift): same kernels with shift = 0
+
+template <int D>
+static void launch_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g,
+                       int rows, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(ln_shift_fwd_kernel<D>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, (__bf16*)y, mean, rstd, g, rows, eps);
+}
+
+template <int D>
+static void launch_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, float* dx, float* dw,
+                       float* db, const ShiftGeom& g, int rows, hipStream_t st) {
+  int blocks = (rows + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, dx, dw, db, g, rows);
+}
+
+bool ln_shift_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g, int rows,
+                  int D, float eps, hipStream_t st) {
+  switch (D) {
+    case 256: launch_fwd<256>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
+    case 512: launch_fwd<512>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
+    case 1024: launch_fwd<1024>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
+    case 2048: launch_fwd<2048>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
+    default: return false;
+  }
+}
+
+bool ln_shift_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, float* dx, float* dw,
+                  float* db, const ShiftGeom& g, int rows, int D, hipStream_t st) {
+  switch (D) {
+    case 256: launch_bwd<256>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
+    case 512: launch_bwd<512>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
+    case 1024: launch_bwd<1024>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
+    case 2048: launch_bwd<2048>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
+    default: return false;
+  }
+}
+
+}  // namespace dalle

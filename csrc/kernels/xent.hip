@@ -1,0 +1,94 @@
+// Fused softmax cross-entropy with the gradient produced in the same pass.
+// logits (R, V) bf16 (one split of the text/image vocabulary), labels (R) int64 (already offset into
+// this split). Per row: loss = logsumexp(l) - l[label]; dlogits = (softmax(l) - onehot) * gscale
+// written IN PLACE over the logits (bf16), so the backward pass is two GEMMs with no extra
+// elementwise kernel. One 256-thread workgroup per row; online max/sum over 16-byte loads.
+#include "common.h"
+
+namespace dalle {
+
+__global__ __launch_bounds__(256) void xent_fwd_bwd_kernel(__bf16* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                           float* __restrict__ loss, int V, float gscale) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  __bf16* lrow = logits + row * (long)V;
+  const int tid = threadIdx.x;
+  // rows of an odd-length vocabulary are not 16-B aligned: scalar head, vector body, scalar tail
+  const int head = (int)((8 - ((row * (long)V) & 7)) & 7) < V ? (int)((8 - ((row * (long)V) & 7)) & 7) : V;
+  __bf16* lr = lrow + head;
+  const int Vb = V - head;
+  const int nvec = Vb / 8;
+  float m = NEG_BIG, s = 0.f;
+  if (tid < head) {
+    const float f = bf2f(reinterpret_cast<const bf16_raw*>(lrow)[tid]);
+    s = 1.0f;
+    m = f;
+  }
+  for (int i = tid; i < nvec; i += 256) {
+    float f[8];
+    unpack8(*reinterpret_cast<const s16x8*>(lr + 8 * i), f);
+    float mx = f[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) mx = fmaxf(mx, f[j]);
+    const float mn = fmaxf(m, mx);
+    float acc = s * __expf(m - mn);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += __expf(f[j] - mn);
+    m = mn;
+    s = acc;
+  }
+  for (int i = nvec * 8 + tid; i < Vb; i += 256) {
+    const float f = bf2f(reinterpret_cast<const bf16_raw*>(lr)[i]);
+    const float mn = fmaxf(m, f);
+    s = s * __expf(m - mn) + __expf(f - mn);
+    m = mn;
+  }
+  // block reduce (max, sum)
+  float wm = wave_max(m);
+  float ws = wave_sum(s * __expf(m - wm));
+  const int w = tid >> 6, l = tid & 63;
+  if (l == 0) { red[w] = wm; red[4 + w] = ws; }
+  __syncthreads();
+  float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float Ssum = red[4] * __expf(red[0] - M) + red[5] * __expf(red[1] - M) + red[6] * __expf(red[2] - M) +
+               red[7] * __expf(red[3] - M);
+  const float lse = M + __logf(Ssum);
+  const int64_t lab = labels[row];
+  __syncthreads();
+  if (tid == 0) {
+    const float xl = bf2f(reinterpret_cast<const bf16_raw*>(lrow)[lab]);
+    loss[row] = lse - xl;
+  }
+  __syncthreads();
+  if (tid < head) {
+    bf16_raw* p = reinterpret_cast<bf16_raw*>(lrow) + tid;
+    float g = __expf(bf2f(*p) - lse);
+    if (tid == lab) g -= 1.0f;
+    *p = f2bf(g * gscale);
+  }
+  const int64_t labb = lab - head;
+  for (int i = tid; i < nvec; i += 256) {
+    float f[8];
+    s16x8* p = reinterpret_cast<s16x8*>(lr + 8 * i);
+    unpack8(*p, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float g = __expf(f[j] - lse);
+      if (8 * i + j == labb) g -= 1.0f;
+      f[j] = g * gscale;
+    }
+    *p = pack8(f);
+  }
+  for (int i = nvec * 8 + tid; i < Vb; i += 256) {
+    bf16_raw* p = reinterpret_cast<bf16_raw*>(lr) + i;
+    float g = __expf(bf2f(*p) - lse);
+    if (i == labb) g -= 1.0f;
+    *p = f2bf(g * gscale);
+  }
+}
+
+void xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, long R, int V, float gscale, hipStream_t st) {
+  hipLaunchKernelGGL(xent_fwd_bwd_kernel, dim3(R), dim3(256), 0, st, (__bf16*)logits, labels, loss, V, gscale);
+}
+
+}  // namespace dalle

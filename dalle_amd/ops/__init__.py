@@ -1,0 +1,101 @@
+"""Op dispatch: hand-written HIP/CDNA4 kernels on MI355X, pure-PyTorch reference on CPU.
+
+Every op the model calls goes through this module. Backend selection per call:
+
+* CPU tensors                    -> ``reference`` (pure PyTorch, fp32)
+* CUDA(=HIP) tensors              -> ``hip`` (``dalle_amd._C`` kernels + hipBLASLt GEMMs), bf16 compute
+* ``DALLE_AMD_BACKEND=torch``     -> force the reference ops on GPU too (A/B and numerics checks)
+
+On a GPU the HIP extension is REQUIRED: if ``dalle_amd._C`` cannot be imported the first GPU op
+raises instead of silently running the eager fallback.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import reference
+from .ext import hip_available, load_extension  # noqa: F401
+
+COMPUTE_DTYPE = torch.bfloat16
+
+
+def backend_for(t: torch.Tensor) -> str:
+    forced = os.environ.get("DALLE_AMD_BACKEND", "auto")
+    if not t.is_cuda:
+        return "torch"
+    if forced == "torch":
+        return "torch_gpu"
+    load_extension(required=True)
+    return "hip"
+
+
+def _hip():
+    from . import hip_ops
+    return hip_ops
+
+
+# ---------------------------------------------------------------------------------------------
+def layernorm_shift(x, weight, bias, text_len: int, image_size: int, shift: bool = True):
+    be = backend_for(x)
+    if be == "torch":
+        return reference.layernorm_shift(x, weight, bias, text_len, image_size, shift)
+    if be == "torch_gpu":
+        return reference.layernorm_shift(x, weight, bias, text_len, image_size, shift).to(COMPUTE_DTYPE)
+    return _hip().layernorm_shift(x, weight, bias, text_len, image_size, shift)
+
+
+def attention_block(h, w_qkv, w_out, b_out, heads: int, geom, attn_type: str):
+    be = backend_for(h)
+    if be == "hip":
+        return _hip().attention_block(h, w_qkv, w_out, b_out, heads, geom, attn_type)
+    from ..models.rotary import rotary_tables
+    cos, sin = rotary_tables(geom.text_len, geom.image_size, w_qkv.shape[0] // 3 // heads, device=h.device)
+    if be == "torch_gpu":
+        dt = COMPUTE_DTYPE
+        return reference.attention_block(h.to(dt), w_qkv.to(dt), w_out.to(dt), b_out.to(dt), heads, geom, attn_type, cos, sin)
+    return reference.attention_block(h, w_qkv, w_out, b_out, heads, geom, attn_type, cos, sin)
+
+
+def feed_forward(h, w1, b1, w2, b2):
+    be = backend_for(h)
+    if be == "hip":
+        return _hip().feed_forward(h, w1, b1, w2, b2)
+    if be == "torch_gpu":
+        dt = COMPUTE_DTYPE
+        return reference.feed_forward(h.to(dt), w1.to(dt), b1.to(dt), w2.to(dt), b2.to(dt))
+    return reference.feed_forward(h, w1, b1, w2, b2)
+
+
+def begin_forward():
+    """Start of a model forward: drops the per-forward bf16 weight casts of the HIP path."""
+    if hip_available():
+        _hip().begin_forward()
+
+
+def scale_rows(o, scale):
+    """LayerScale multiply (reversible branches; fused into the residual add otherwise)."""
+    return o * scale.to(o.dtype)
+
+
+def scale_residual(x, o, scale):
+    """x + scale * o  -- residual add with the LayerScale fused in (K8/K10 epilogue)."""
+    if x.is_cuda and backend_for(x) == "hip":
+        return _hip().scale_residual(x, o, scale)
+    return x + (o * scale.to(o.dtype)).to(x.dtype)
+
+
+def residual_add(x, y):
+    return x + y.to(x.dtype)
+
+
+def logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len: int, num_text_tokens: int, loss_img_weight: float):
+    be = backend_for(out)
+    if be == "hip":
+        return _hip().logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len, num_text_tokens, loss_img_weight)
+    h = torch.nn.functional.layer_norm(out, (out.shape[-1],), norm_w, norm_b)
+    if be == "torch_gpu":
+        dt = COMPUTE_DTYPE
+        return reference.split_logits_loss(h.to(dt), weight.to(dt), bias.to(dt), labels, text_seq_len, num_text_tokens, loss_img_weight)
+    return reference.split_logits_loss(h, weight, bias, labels, text_seq_len, num_text_tokens, loss_img_weight)

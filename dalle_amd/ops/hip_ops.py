@@ -1,0 +1,258 @@
+"""HIP execution path: autograd Functions over the ``dalle_amd._C`` kernels + hipBLASLt GEMMs.
+
+Numerics: fp32 residual stream and fp32 master weights; bf16 GEMM operands / activations with
+fp32 accumulation; weight gradients are produced directly in fp32 by the GEMM
+(``torch.mm(..., out_dtype=float32)`` -> hipBLASLt bf16-in / fp32-out), so gradients of the shared
+blocks (summed over every layer that reuses them) never round through bf16.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .ext import load_extension
+from ..models.patterns import PATTERN_IDS, AttnGeometry
+from ..models.rotary import rotary_tables
+
+_C = None
+
+
+def C():
+    global _C
+    if _C is None:
+        _C = load_extension(required=True)
+    return _C
+
+
+# ---------------------------------------------------------------------------------------------
+# bf16 weight cast cache (one cast per unique weight per forward; invalidated by begin_forward)
+# ---------------------------------------------------------------------------------------------
+_wcache: Dict[int, Tuple[int, torch.Tensor]] = {}
+_epoch = 0
+
+
+def begin_forward():
+    global _epoch
+    _epoch += 1
+    _wcache.clear()
+
+
+def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    if w.dtype == torch.bfloat16:
+        return w
+    key = id(w)
+    hit = _wcache.get(key)
+    if hit is not None and hit[0] == w.data_ptr():
+        return hit[1]
+    wb = w.detach().to(torch.bfloat16)
+    _wcache[key] = (w.data_ptr(), wb)
+    return wb
+
+
+_tables: Dict[tuple, tuple] = {}
+
+
+def _rope_tables(geom: AttnGeometry, dim_head: int, device):
+    key = (geom.text_len, geom.image_size, dim_head, str(device))
+    t = _tables.get(key)
+    if t is None:
+        t = rotary_tables(geom.text_len, geom.image_size, dim_head, device=device)
+        _tables[key] = t
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+# Linear: bf16 GEMM forward, fp32 weight grads
+# ---------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        wb = bf16_weight(w)
+        x2 = x.reshape(-1, x.shape[-1])
+        if b is not None:
+            y = torch.addmm(bf16_weight(b), x2, wb.t())
+        else:
+            y = torch.mm(x2, wb.t())
+        ctx.save_for_backward(x2, wb)
+        ctx.has_bias = b is not None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, wb = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1])
+        if g2.dtype != torch.bfloat16:
+            g2 = g2.to(torch.bfloat16)
+        g2 = g2.contiguous()
+        dx = torch.mm(g2, wb).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(g2.t(), x2, out_dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        db = torch.sum(g2, 0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    return _Linear.apply(x, w, b)
+
+
+# ---------------------------------------------------------------------------------------------
+# K3+K4: LayerNorm + token shift
+# ---------------------------------------------------------------------------------------------
+class _LNShift(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, T, S, shift):
+        x = x.contiguous()
+        y, mean, rstd = C().ln_shift_fwd(x, w.contiguous(), b.contiguous(), T, S, shift, 1e-5)
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.geo = (T, S, shift)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, mean, rstd = ctx.saved_tensors
+        T, S, shift = ctx.geo
+        gy = gy.to(torch.bfloat16).contiguous()
+        dx, dw, db = C().ln_shift_bwd(x, w.contiguous(), gy, mean, rstd, T, S, shift)
+        return dx, dw, db, None, None, None
+
+
+def layernorm_shift(x, weight, bias, text_len: int, image_size: int, shift: bool = True):
+    if x.dtype != torch.float32:
+        x = x.float()
+    return _LNShift.apply(x, weight, bias, text_len, image_size, bool(shift))
+
+
+# ---------------------------------------------------------------------------------------------
+# K6 + K7: rotary + sparse attention core
+# ---------------------------------------------------------------------------------------------
+class _AttnCore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, T, S, K, H, pattern):
+        qkv = qkv.contiguous()
+        B, n = qkv.shape[0], qkv.shape[1]
+        col = pattern == PATTERN_IDS["axial_col"]
+        q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+        out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
+        ctx.save_for_backward(q, k, v, out, lse, cos, sin)
+        ctx.geo = (B, T, S, n, K, H, pattern, col)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        q, k, v, out, lse, cos, sin = ctx.saved_tensors
+        B, T, S, n, K, H, pattern, col = ctx.geo
+        gout = gout.to(torch.bfloat16).contiguous()
+        dq, dk, dv = C().attn_bwd(q, k, v, out, gout, lse, B, T, S, n, K, H, pattern)
+        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def attention_core(qkv, heads: int, geom: AttnGeometry, attn_type: str):
+    dim_head = qkv.shape[-1] // 3 // heads
+    assert dim_head == 64, "the HIP attention kernels are specialised for dim_head = 64"
+    cos, sin = _rope_tables(geom, dim_head, qkv.device)
+    return _AttnCore.apply(qkv, cos, sin, geom.text_len, geom.image_size, geom.kernel_size, heads, PATTERN_IDS[attn_type])
+
+
+def attention_block(h, w_qkv, w_out, b_out, heads: int, geom: AttnGeometry, attn_type: str):
+    qkv = linear(h, w_qkv)
+    o = attention_core(qkv, heads, geom, attn_type)
+    return linear(o, w_out, b_out)
+
+
+# ---------------------------------------------------------------------------------------------
+# K9: GEGLU feed-forward
+# ---------------------------------------------------------------------------------------------
+class _GEGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        h = h.contiguous()
+        ctx.save_for_backward(h)
+        return C().geglu_fwd(h)
+
+    @staticmethod
+    def backward(ctx, g):
+        (h,) = ctx.saved_tensors
+        return C().geglu_bwd(h, g.to(torch.bfloat16).contiguous())
+
+
+def feed_forward(h, w1, b1, w2, b2):
+    return linear(_GEGLU.apply(linear(h, w1, b1)), w2, b2)
+
+
+# ---------------------------------------------------------------------------------------------
+# K8/K10 epilogue: x + scale * y (fp32 residual stream)
+# ---------------------------------------------------------------------------------------------
+class _ScaleResidual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, scale):
+        out = x.contiguous().clone()
+        y = y.contiguous()
+        s = scale.reshape(-1).contiguous()
+        C().scale_residual_(out, y, s)
+        ctx.save_for_backward(y, s)
+        ctx.sshape = scale.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, s = ctx.saved_tensors
+        dy, ds = C().scale_residual_bwd(g.contiguous(), y, s)
+        return g, dy, ds.view(ctx.sshape)
+
+
+def scale_residual(x, y, scale):
+    return _ScaleResidual.apply(x, y, scale)
+
+
+# ---------------------------------------------------------------------------------------------
+# K12: final LayerNorm + split-vocabulary logits + fused softmax cross entropy
+# ---------------------------------------------------------------------------------------------
+class _SplitXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, w, b, labels, text_seq_len, Vt, img_w):
+        # h: (B, n, d) bf16 normed hidden; w/b fp32 master head
+        B, n, d = h.shape
+        wb, bb = bf16_weight(w), bf16_weight(b)
+        ht = h[:, :text_seq_len].reshape(-1, d).contiguous()
+        hi = h[:, text_seq_len:].reshape(-1, d).contiguous()
+        lt = labels[:, :text_seq_len].reshape(-1).contiguous()
+        li = (labels[:, text_seq_len:] - Vt).reshape(-1).contiguous()
+        Nt, Ni = ht.shape[0], hi.shape[0]
+        den = 1.0 + img_w
+        logit_t = torch.addmm(bb[:Vt], ht, wb[:Vt].t())
+        logit_i = torch.addmm(bb[Vt:], hi, wb[Vt:].t())
+        loss_t = C().xent_fwd_bwd_(logit_t, lt, 1.0 / (den * Nt))  # logits now hold dL/dlogits
+        loss_i = C().xent_fwd_bwd_(logit_i, li, img_w / (den * Ni))
+        loss = (loss_t.mean() + img_w * loss_i.mean()) / den
+        ctx.save_for_backward(ht, hi, logit_t, logit_i, wb)
+        ctx.meta = (B, n, d, text_seq_len, Vt)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        ht, hi, dt, di, wb = ctx.saved_tensors
+        B, n, d, tsl, Vt = ctx.meta
+        g = gl.float()
+        dh = torch.empty(B, n, d, dtype=torch.bfloat16, device=ht.device)
+        dh[:, :tsl] = (torch.mm(dt, wb[:Vt]) * g).view(B, tsl, d)
+        dh[:, tsl:] = (torch.mm(di, wb[Vt:]) * g).view(B, n - tsl, d)
+        dw = torch.empty(wb.shape, dtype=torch.float32, device=wb.device)
+        dw[:Vt] = torch.mm(dt.t(), ht, out_dtype=torch.float32)
+        dw[Vt:] = torch.mm(di.t(), hi, out_dtype=torch.float32)
+        dw.mul_(g)
+        db = torch.cat([torch.sum(dt, 0, dtype=torch.float32), torch.sum(di, 0, dtype=torch.float32)]) * g
+        return dh, dw, db, None, None, None, None
+
+
+def logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len: int, num_text_tokens: int, loss_img_weight: float):
+    h = _LNShift.apply(out.float() if out.dtype != torch.float32 else out, norm_w, norm_b, 0, 1, False)
+    return _SplitXent.apply(h, weight, bias, labels, text_seq_len, num_text_tokens, float(loss_img_weight))
+
+
+def nonfinite_flag(x: torch.Tensor) -> torch.Tensor:
+    return C().nonfinite(x.contiguous())

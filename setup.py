@@ -1,0 +1,58 @@
+"""Build the in-tree native extensions for MI355X (gfx950).
+
+    PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
+
+* ``dalle_amd._C``       -- hand-written HIP/CDNA4 kernels (csrc/kernels, csrc/optim) + torch bindings
+* ``dalle_amd._kvstore`` -- C++ TCP key-value store with subkeys / expiration (the DHT replacement)
+"""
+import os
+
+from setuptools import Extension, setup
+from torch.utils.cpp_extension import BuildExtension, CppExtension, include_paths, library_paths
+
+os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+hip_sources = [
+    "csrc/binding.cpp",
+    "csrc/kernels/attention.hip",
+    "csrc/kernels/rotary.hip",
+    "csrc/kernels/layernorm_shift.hip",
+    "csrc/kernels/elementwise.hip",
+    "csrc/kernels/xent.hip",
+    "csrc/optim/lamb.hip",
+]
+
+# Plain setuptools Extension (not CUDAExtension): CUDAExtension would run hipify over the sources.
+# These kernels are written for CDNA4 directly; BuildExtension compiles the .hip files with hipcc.
+ext_modules = [
+    Extension(
+        "dalle_amd._C",
+        hip_sources,
+        include_dirs=[os.path.join(ROOT, "csrc")] + include_paths(device_type="cuda"),
+        library_dirs=library_paths(device_type="cuda"),
+        libraries=["c10", "torch", "torch_cpu", "torch_python", "amdhip64", "c10_hip", "torch_hip"],
+        language="c++",
+        extra_compile_args={
+            "cxx": ["-O3", "-std=c++17"],
+            "nvcc": ["-O3", "--offload-arch=gfx950", "-std=c++17", "-munsafe-fp-atomics"],
+        },
+    ),
+]
+
+if os.path.exists(os.path.join(ROOT, "csrc/store/kvstore.cpp")):
+    ext_modules.append(
+        CppExtension(
+            "dalle_amd._kvstore",
+            ["csrc/store/kvstore.cpp"],
+            extra_compile_args=["-O2", "-std=c++17"],
+        )
+    )
+
+setup(
+    name="dalle_amd",
+    version="0.1.0",
+    packages=["dalle_amd"],
+    ext_modules=ext_modules,
+    cmdclass={"build_ext": BuildExtension.with_options(use_ninja=True)},
+)

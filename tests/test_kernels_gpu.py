@@ -1,0 +1,148 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dalle_amd.models.patterns import AttnGeometry, PATTERN_IDS
+from dalle_amd.models.rotary import rotary_tables
+from dalle_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [(65, 16), (257, 32)]  # (text_len, image side): tiny and the reference geometry
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("T,S", GEOMS)
+@pytest.mark.parametrize("D", [256, 1024])
+@pytest.mark.parametrize("shift", [True, False])
+def test_layernorm_shift(cuda, T, S, D, shift):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    B, n = 2, T + S * S - 1
+    x = torch.randn(B, n, D, device=cuda, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(D, device=cuda)).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device=cuda)).requires_grad_(True)
+    y = hip_ops.layernorm_shift(x, w, b, T, S, shift)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = ref.layernorm_shift(xr, wr, br, T, S, shift)
+    assert y.dtype == torch.bfloat16
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("T,S", GEOMS)
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
+def test_sparse_attention(cuda, T, S, attn_type):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(1)
+    B, H, Dh = 2, 2, 64
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = (torch.randn(B, n, 3 * H * Dh, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_(True)
+    out = hip_ops.attention_core(qkv, H, geom, attn_type)
+    cos, sin = rotary_tables(T, S, Dh, device=cuda)
+    qr_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref.qkv_rotary(qr_in, H, cos, sin)
+    out_ref = ref.sparse_attention_core(q, k, v, geom, attn_type)
+    assert torch.isfinite(out.float()).all()
+    assert _rel(out, out_ref) < 2e-2, attn_type
+    g = torch.randn_like(out_ref)
+    out.backward(g.to(torch.bfloat16))
+    out_ref.backward(g.to(torch.bfloat16).float())
+    assert _rel(qkv.grad, qr_in.grad) < 3e-2, attn_type
+
+
+def test_geglu(cuda):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(2)
+    h = torch.randn(300, 2 * 512, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    y = hip_ops._GEGLU.apply(h)
+    hr = h.detach().float().requires_grad_(True)
+    yr = ref.geglu(hr)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(h.grad, hr.grad) < 1e-2
+
+
+def test_scale_residual(cuda):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(3)
+    x = torch.randn(4, 100, 256, device=cuda, requires_grad=True)
+    y = torch.randn(4, 100, 256, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    s = torch.rand(1, 1, 256, device=cuda, requires_grad=True)
+    o = hip_ops.scale_residual(x, y, s)
+    xr, yr, sr = x.detach().clone().requires_grad_(True), y.detach().float().requires_grad_(True), s.detach().clone().requires_grad_(True)
+    orf = xr + yr * sr
+    assert _rel(o, orf) < 1e-5
+    g = torch.randn_like(orf)
+    o.backward(g)
+    orf.backward(g)
+    assert _rel(x.grad, xr.grad) < 1e-6
+    assert _rel(y.grad, yr.grad) < 1e-2
+    assert _rel(s.grad, sr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("V", [8192, 32356, 1000])
+def test_xent(cuda, V):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(4)
+    R = 37
+    logits = (torch.randn(R, V, device=cuda) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (R,), device=cuda)
+    ref_logits = logits.float().requires_grad_(True)
+    loss_ref = F.cross_entropy(ref_logits, labels, reduction="none")
+    loss_ref.sum().backward()
+    buf = logits.clone()
+    loss = hip_ops.C().xent_fwd_bwd_(buf, labels, 1.0)
+    assert torch.allclose(loss, loss_ref, atol=2e-3, rtol=1e-3)
+    assert _rel(buf, ref_logits.grad) < 1e-2
+
+
+def test_split_logits_loss(cuda):
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(5)
+    B, tsl, n_img, d, Vt, Vi = 2, 64, 256, 256, 1064, 512
+    n = tsl + n_img
+    out = torch.randn(B, n, d, device=cuda, requires_grad=True)
+    nw = torch.ones(d, device=cuda, requires_grad=True)
+    nb = torch.zeros(d, device=cuda, requires_grad=True)
+    W = (torch.randn(Vt + Vi, d, device=cuda) * 0.05).requires_grad_(True)
+    bias = torch.zeros(Vt + Vi, device=cuda, requires_grad=True)
+    labels = torch.cat([torch.randint(0, Vt, (B, tsl)), torch.randint(Vt, Vt + Vi, (B, n_img))], 1).to(cuda)
+    hip_ops.begin_forward()
+    loss = hip_ops.logits_loss(out, nw, nb, W, bias, labels, tsl, Vt, 7.0)
+    loss.backward()
+    o2, W2, b2 = (t.detach().clone().requires_grad_(True) for t in (out, W, bias))
+    h = F.layer_norm(o2, (d,))
+    loss_r = ref.split_logits_loss(h, W2, b2, labels, tsl, Vt, 7.0)
+    loss_r.backward()
+    assert abs(loss.item() - loss_r.item()) < 1e-2
+    assert _rel(out.grad, o2.grad) < 3e-2
+    assert _rel(W.grad, W2.grad) < 3e-2
+    assert _rel(bias.grad, b2.grad) < 3e-2
+
+
+def test_nonfinite(cuda):
+    from dalle_amd.ops import hip_ops
+
+    x = torch.randn(100003, device=cuda)
+    assert int(hip_ops.nonfinite_flag(x)) == 0
+    x[77777] = float("nan")
+    assert int(hip_ops.nonfinite_flag(x)) == 1

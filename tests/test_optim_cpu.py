@@ -1,0 +1,138 @@
+"""Optimizer tests (SURVEY §4 tier 3): dynamic maps, blockwise quantisation, 8-bit LAMB."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from dalle_amd.optim import FlatArena, LAMB8bit, LambWithGradientClipping, get_linear_schedule_with_warmup
+from dalle_amd.optim import quant
+
+
+def _numpy_dynamic_map(signed):
+    # independent NumPy re-derivation of bitsandbytes.functional.create_dynamic_map(signed, n=7)
+    data = []
+    for i in range(7):
+        items = 2 ** i + 1 if signed else 2 ** (i + 1) + 1
+        b = np.linspace(0.1, 1, items, dtype=np.float32)
+        means = (b[:-1] + b[1:]) / 2.0
+        data += list((10 ** (-6 + i)) * means)
+        if signed:
+            data += list(-(10 ** (-6 + i)) * means)
+    data += [0.0, 1.0]
+    return np.sort(np.array(data, dtype=np.float32))
+
+
+@pytest.mark.parametrize("signed", [True, False])
+def test_dynamic_map(signed):
+    m = quant.dynamic_map(signed).numpy()
+    assert m.shape == (256,)
+    assert np.all(np.diff(m) >= 0)
+    assert np.allclose(m, _numpy_dynamic_map(signed), rtol=1e-6, atol=1e-12)
+    assert m.max() == 1.0
+    assert (m.min() < -0.99) if signed else (m.min() == 0.0)
+
+
+def test_quantize_roundtrip_and_nearest():
+    torch.manual_seed(0)
+    x = torch.randn(3 * 4096 + 123) * torch.logspace(-4, 0, 3 * 4096 + 123)
+    code = quant.dynamic_map(True)
+    q, absmax = quant.quantize_blockwise(x, code)
+    assert q.dtype == torch.uint8 and absmax.shape == (4,)
+    y = quant.dequantize_blockwise(q, absmax, code)
+    # nearest-entry property: no other code gives a smaller error
+    normed = x / absmax.repeat_interleave(4096)[: x.numel()]
+    err_best = (code[None, :] - normed[:, None]).abs().min(dim=1).values
+    err = (code[q.long()] - normed).abs()
+    assert torch.allclose(err, err_best, atol=1e-7)
+    rel = ((y - x).norm() / x.norm()).item()
+    assert rel < 0.05
+
+
+def test_lamb_8bit_close_to_fp32():
+    torch.manual_seed(0)
+    w0 = torch.randn(256, 512) * 0.02
+    p8, p32 = torch.nn.Parameter(w0.clone()), torch.nn.Parameter(w0.clone())
+    kw = dict(lr=0.01, betas=(0.9, 0.96), eps=1e-6, weight_decay=0.045, clamp_value=10000.0, max_grad_norm=4.0)
+    o8 = LAMB8bit([p8], **kw)
+    o32 = LambWithGradientClipping([p32], **kw)
+    for _ in range(5):
+        g = torch.randn_like(w0)
+        p8.grad, p32.grad = g.clone(), g.clone()
+        o8.step()
+        o32.step()
+    st = o8.state[p8]
+    assert st["state1"].dtype == torch.uint8 and st["state2"].dtype == torch.uint8
+    assert st["absmax1"].shape == (32,)
+    assert o32.state[p32]["state1"].dtype == torch.float32
+    d8, d32 = p8 - w0, p32 - w0
+    assert ((d8 - d32).norm() / d32.norm()).item() < 0.1
+    for k in ("step", "state1", "state2", "qmap1", "qmap2", "absmax1", "absmax2", "weight_norm", "step_norm", "trust_ratio"):
+        assert k in st
+
+
+def test_lamb_small_tensor_fp32_states_and_trust_ratio():
+    p = torch.nn.Parameter(torch.ones(1000))
+    opt = LAMB8bit([p], lr=0.1, weight_decay=0.0, clamp_value=10.0)
+    p.grad = torch.ones(1000)
+    opt.step()
+    st = opt.state[p]
+    assert st["state1"].dtype == torch.float32  # numel < min_8bit_size
+    # m = 0.1, v = 0.001 -> delta = 0.1/(sqrt(0.001)+eps) ~ 3.162 per elem; |p| = 31.6 clamps to 10
+    d = 0.1 / (0.001 ** 0.5 + 1e-6)
+    trust = 10.0 / (d * 1000 ** 0.5)
+    assert torch.allclose(p.data, torch.full((1000,), 1 - 0.1 * trust * d), atol=1e-5)
+
+
+def test_lamb_validation_errors():
+    p = torch.nn.Parameter(torch.zeros(3))
+    with pytest.raises(ValueError):
+        LAMB8bit([p], lr=-1)
+    with pytest.raises(ValueError):
+        LAMB8bit([p], betas=(1.0, 0.9))
+    with pytest.raises(ValueError):
+        LAMB8bit([p], weight_decay=-1)
+
+
+def test_flat_arena_views_and_grad_accumulation():
+    lin = torch.nn.Linear(10, 7)
+    arena = FlatArena(lin.parameters())
+    assert arena.numel == 2 * 4096
+    assert lin.weight.data_ptr() == arena.data.data_ptr()
+    lin(torch.randn(3, 10)).sum().backward()
+    assert lin.weight.grad.data_ptr() == arena.grad.data_ptr()
+    g1 = arena.grad.clone()
+    lin(torch.randn(3, 10)).sum().backward()  # accumulates in place
+    assert not torch.equal(g1, arena.grad)
+    arena.zero_grad()
+    assert arena.grad.abs().sum() == 0
+    assert arena.block_tensor.tolist() == [0, 1]
+
+
+def test_linear_schedule():
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=1.0)
+    sch = get_linear_schedule_with_warmup(opt, 10, 100)
+    lrs = []
+    for _ in range(100):
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sch.step()
+    assert lrs[0] == 0.0 and abs(lrs[10] - 1.0) < 1e-9 and abs(lrs[55] - 0.5) < 1e-9
+
+
+def test_state_dict_roundtrip():
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(100, 1000))
+    opt = LAMB8bit([p], lr=0.01)
+    p.grad = torch.randn_like(p)
+    opt.step()
+    sd = copy.deepcopy(opt.state_dict())  # state_dict() returns live references
+    p2 = torch.nn.Parameter(p.detach().clone())
+    opt2 = LAMB8bit([p2], lr=0.01)
+    opt2.load_state_dict(sd)
+    g = torch.randn_like(p)
+    p.grad, p2.grad = g.clone(), g.clone()
+    opt.step()
+    opt2.step()
+    assert torch.allclose(p, p2)
