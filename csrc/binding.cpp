@@ -85,14 +85,14 @@ std::vector<Tensor> ln_shift_bwd(Tensor x, Tensor w, Tensor dy, Tensor mean, Ten
   const int B = x.size(0), n = x.size(1), D = x.size(2);
   TORCH_CHECK(dy.sizes() == x.sizes() && mean.numel() == B * n && rstd.numel() == B * n);
   auto dx = torch::empty_like(x);
-  auto dw = torch::zeros({D}, x.options());
-  auto db = torch::zeros({D}, x.options());
+  auto part = torch::empty({512, 2 * D}, x.options());  // per-block partial [dw | db] rows
+  auto dwdb = torch::empty({2 * D}, x.options());
   dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
   bool ok = dalle::ln_shift_bwd(x.data_ptr<float>(), w.data_ptr<float>(), dy.data_ptr(), mean.data_ptr<float>(),
-                                rstd.data_ptr<float>(), dx.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(), g,
+                                rstd.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), dwdb.data_ptr<float>(), g,
                                 B * n, D, cur_stream());
   TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
-  return {dx, dw, db};
+  return {dx, dwdb.slice(0, 0, D), dwdb.slice(0, D, 2 * D)};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -207,10 +207,10 @@ std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale) {
   const long D = g.size(-1);
   TORCH_CHECK(D % 8 == 0 && D <= 2048 && y.numel() == g.numel() && scale.numel() == D);
   auto dy = torch::empty(g.sizes(), y.options());
-  auto dscale = torch::zeros({D}, g.options());
-  dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), dscale.data_ptr<float>(),
+  auto ws = torch::empty({(512 + 1) * D}, g.options());  // 512 partial rows + the reduced row
+  dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), ws.data_ptr<float>(),
                             g.numel() / D, D, cur_stream());
-  return {dy, dscale};
+  return {dy, ws.slice(0, 512 * D, 513 * D)};
 }
 
 Tensor nonfinite(Tensor x) {

@@ -4,6 +4,9 @@
 
 namespace dalle {
 
+void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st);
+constexpr int SR_BWD_BLOCKS = 512;
+
 // GEGLU: h (M, 2F) -> out (M, F) = h[:, :F] * gelu(h[:, F:])   (exact erf GELU)
 __global__ void geglu_fwd_kernel(const __bf16* __restrict__ h, __bf16* __restrict__ out, long M, int F) {
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -68,13 +71,13 @@ __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __
   const int tcol = threadIdx.x % cols8;
   const int rows_per_iter = blockDim.x / cols8;
   const int trow = threadIdx.x / cols8;
-  if (trow >= rows_per_iter) return;
+  const bool on = trow < rows_per_iter;
   const int c = tcol * 8;
   float acc[8] = {};
   float sc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) sc[i] = scale[c + i];
-  for (long r = (long)blockIdx.x * rows_per_iter + trow; r < M; r += (long)gridDim.x * rows_per_iter) {
+  for (long r = (long)blockIdx.x * rows_per_iter + trow; on && r < M; r += (long)gridDim.x * rows_per_iter) {
     const f32x4* gp = reinterpret_cast<const f32x4*>(g + r * D + c);
     const f32x4 g0 = gp[0], g1 = gp[1];
     float yv[8], o[8];
@@ -88,8 +91,19 @@ __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __
     }
     *reinterpret_cast<s16x8*>(dy + r * D + c) = pack8(o);
   }
+  // deterministic reduction: threads of one column -> LDS -> one partial row per block (no atomics)
+  __shared__ float red[256 * 8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) atomicAdd(dscale + c + i, acc[i]);
+  for (int i = 0; i < 8; ++i) red[threadIdx.x * 8 + i] = on ? acc[i] : 0.f;
+  __syncthreads();
+  if (on && trow == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float sum = 0.f;
+      for (int r = 0; r < rows_per_iter; ++r) sum += red[(r * cols8 + tcol) * 8 + i];
+      dscale[(size_t)blockIdx.x * D + c + i] = sum;
+    }
+  }
 }
 
 // Non-finite detector over an fp32 buffer: flag[0] = 1 if any element is NaN/Inf
@@ -120,9 +134,11 @@ void scale_residual(float* x, const void* y, const float* scale, long M, int D, 
 }
 void scale_residual_bwd(const float* g, const void* y, const float* scale, void* dy, float* dscale, long M, int D,
                         hipStream_t st) {
-  int blocks = 1024;
+  // dscale points at [SR_BWD_BLOCKS x D partial rows | D outputs]
+  const int blocks = SR_BWD_BLOCKS;
   hipLaunchKernelGGL(scale_residual_bwd_kernel, dim3(blocks), dim3(256), 0, st, g, (const __bf16*)y, scale, (__bf16*)dy, dscale,
                      M, D);
+  column_sum(dscale, blocks, D, dscale + (size_t)blocks * D, st);
 }
 void nonfinite(const float* x, long n, int* flag, hipStream_t st) {
   long blocks = (n / 4 + 255) / 256;

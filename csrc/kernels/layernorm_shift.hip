@@ -14,6 +14,8 @@
 
 namespace dalle {
 
+constexpr int LN_BWD_BLOCKS = 512;
+
 // destination position of channel group `grp` (0: [0,D/4), 1: [D/4,D/2), 2: [D/2,D)) of source p,
 // or -1 if dropped
 __device__ __forceinline__ int shift_dest(const ShiftGeom& g, int p, int grp) {
@@ -127,15 +129,50 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
       *reinterpret_cast<f32x4*>(dx + (size_t)row * D + c) = o;
     }
   }
+  // deterministic two-stage reduction of dweight / dbias (no atomics: every workgroup adding into the
+  // same D columns is the worst case for float atomics): waves -> LDS -> one partial row per block.
+  __shared__ float red[4][2 * D];
+  const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = 4 * (lane + 64 * j);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      atomicAdd(dw + c + i, dwa[j][i]);
-      atomicAdd(db + c + i, dba[j][i]);
+      red[wv][c + i] = dwa[j][i];
+      red[wv][D + c + i] = dba[j][i];
     }
   }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x)
+    dw[(size_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// sum `nrows` partial rows of width `width` (column-parallel, fixed order)
+// 256 threads = 64 columns x 4 row groups; 8 independent loads in flight per thread
+__global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part, int nrows, int width,
+                                                         float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < width) {
+    int r = rg;
+    for (; r + 28 < nrows; r += 32) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(size_t)(r + 4 * u) * width + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; r < nrows; r += 4) s += part[(size_t)r * width + c];
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < width) out[c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(column_sum_kernel, dim3((width + 63) / 64), dim3(256), 0, st, part, nrows, width, out);
 }
 
 // plain LayerNorm variants for the final norm (no shift): same kernels with shift = 0
@@ -149,9 +186,12 @@ static void launch_fwd(const float* x, const float* w, const float* b, void* y, 
 template <int D>
 static void launch_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, float* dx, float* dw,
                        float* db, const ShiftGeom& g, int rows, hipStream_t st) {
+  // dw points at a (LN_BWD_BLOCKS x 2D) partial buffer; db receives [dw | db] (2D floats)
   int blocks = (rows + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, dx, dw, db, g, rows);
+  if (blocks > LN_BWD_BLOCKS) blocks = LN_BWD_BLOCKS;
+  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, dx, dw, nullptr, g,
+                     rows);
+  column_sum(dw, blocks, 2 * D, db, st);
 }
 
 bool ln_shift_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g, int rows,
