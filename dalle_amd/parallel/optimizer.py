@@ -1,0 +1,409 @@
+"""The collaborative optimizer: hivemind.Optimizer semantics on RCCL collectives.
+
+Normative behaviour (``task.py:127-134``, ``arguments.py:59-78``):
+
+1. Local accumulation: every ``.step()`` adds ``batch_size_per_step`` samples; gradients accumulate in
+   ``.grad`` (``reuse_grad_buffers``: the trainer's ``zero_grad`` is bypassed) or in separate buffers.
+2. Epoch trigger: when the peers together accumulated ``target_batch_size`` samples.
+3. Gradient averaging: ``G = sum_p s_p * (g_p / t_p) / sum_p s_p`` (sample-weighted mean of per-peer
+   mean gradients) -- plain RCCL all-reduce, compressed butterfly all-reduce (fp16 / uniform 8-bit,
+   ``averaging.py``) or PowerSGD rank-r (``powersgd.py``). On failure a peer keeps its own ``g_p / t_p``.
+4. Optimizer step (inner optimizer, e.g. fused 8-bit LAMB with global clipping), ``scheduler.step()``,
+   ``local_epoch += 1``.
+5. State averaging every ``average_state_every`` epochs (parameters, optionally compressed).
+6. Reset accumulators.
+7. Resync: a peer whose epoch lags the collaboration loads the state from a donor peer.
+
+Peers are the ranks of a ``torch.distributed`` process group (backend "nccl" = RCCL over xGMI on a
+MI355X node; "gloo" for CPU peers). Progress is tracked with one tiny all-reduce per local step
+(``progress.py``), which makes the epoch decision identical on every rank, so the static RCCL
+communicator replaces hivemind's matchmaking.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Iterable, List, Optional, Union
+
+import torch
+import torch.distributed as dist
+
+from .averaging import allreduce_weighted
+from .compression import CompressionBase, NoCompression
+from .powersgd import PowerSGD
+from .progress import ProgressTracker
+from ..optim.flat import FlatArena
+from ..utils.logging import get_logger
+
+logger = get_logger(__name__)
+
+
+def _group_world(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+class GradientAverager:
+    """Accumulates local gradients and averages them across peers (D15)."""
+
+    def __init__(self, params: List[torch.nn.Parameter], arena: Optional[FlatArena] = None, group=None,
+                 reuse_grad_buffers: bool = False, compression: Optional[CompressionBase] = None,
+                 powersgd: Optional[PowerSGD] = None, client_mode: bool = False):
+        self.params = params
+        self.arena = arena
+        self.group = group
+        self.reuse_grad_buffers = reuse_grad_buffers
+        self.compression = compression or NoCompression()
+        self.powersgd = powersgd
+        self.client_mode = client_mode
+        self.local_samples_accumulated = 0
+        self.local_times_accumulated = 0
+        self._acc: Optional[List[torch.Tensor]] = None
+        self.last_averaging_ok = True
+
+    # -- accumulation -----------------------------------------------------------------------------
+    @torch.no_grad()
+    def accumulate_grads_(self, batch_size: int):
+        self.local_samples_accumulated += int(batch_size)
+        self.local_times_accumulated += 1
+        if self.reuse_grad_buffers:
+            return
+        if self._acc is None:
+            self._acc = [torch.zeros_like(p, dtype=torch.float32) for p in self.params]
+        for a, p in zip(self._acc, self.params):
+            if p.grad is not None:
+                a.add_(p.grad)
+
+    def _grads(self) -> List[torch.Tensor]:
+        if self.reuse_grad_buffers:
+            for p in self.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            return [p.grad for p in self.params]
+        return self._acc if self._acc is not None else [torch.zeros_like(p) for p in self.params]
+
+    # -- averaging --------------------------------------------------------------------------------
+    @torch.no_grad()
+    def step(self, total_samples: Optional[int] = None) -> bool:
+        """Replace the accumulated grads with the collaboration-wide weighted mean (in the params'
+        ``.grad``). Returns False if averaging failed and the local mean was used instead."""
+        t = max(1, self.local_times_accumulated)
+        s = float(self.local_samples_accumulated)
+        world, _ = _group_world(self.group)
+        grads = self._grads()
+        ok = True
+        try:
+            if world == 1:
+                for g in grads:
+                    g.div_(t)
+            elif self.powersgd is not None:
+                total = float(total_samples) if total_samples else None
+                if total is None:
+                    tt = torch.tensor([s], device=grads[0].device, dtype=torch.float32)
+                    dist.all_reduce(tt, group=self.group)
+                    total = float(tt.item())
+                if not self.reuse_grad_buffers:
+                    for p, g in zip(self.params, grads):
+                        p.grad = g
+                self.powersgd.allreduce_(scale=(s / t) * world / max(total, 1e-30))
+            else:
+                # x_p = per-peer MEAN gradient (g_p / t_p), weighted by its sample count s_p
+                flat, views = self._flat(grads)
+                shards = None if isinstance(self.compression, NoCompression) else self._shard_weights(world)
+                allreduce_weighted(flat, weight=s, group=self.group, compression=self.compression,
+                                   shard_weights=shards, total_weight=total_samples)
+                if views is not None:
+                    self._unflat(flat, views)
+        except Exception as e:  # noqa: BLE001 - a dead / slow peer must not kill training
+            logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
+            ok = False
+            if not (self.arena is not None and self.reuse_grad_buffers and world > 1):
+                for g in grads:
+                    g.div_(t)
+        if not self.reuse_grad_buffers:
+            for p, g in zip(self.params, grads):
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
+        self.last_averaging_ok = ok
+        return ok
+
+    def _shard_weights(self, world: int):
+        """Butterfly shard sizes: client-mode peers host no shard (D17). Gathered once, then cached."""
+        if world == 1:
+            return None
+        if getattr(self, "_shards", None) is None:
+            flags = torch.tensor([0.0 if self.client_mode else 1.0], device=self._device())
+            allf = [torch.zeros_like(flags) for _ in range(world)]
+            dist.all_gather(allf, flags, group=self.group)
+            self._shards = [float(f.item()) for f in allf]
+        return self._shards
+
+    def _device(self):
+        return self.params[0].device
+
+    def _flat(self, grads):
+        """Per-peer mean gradient as one flat buffer (the arena's grad buffer when available)."""
+        t = max(1, self.local_times_accumulated)
+        if self.arena is not None and self.reuse_grad_buffers:
+            self.arena.grad.div_(t)
+            return self.arena.grad, None
+        flat = torch.cat([g.reshape(-1).float() for g in grads]) / t
+        return flat, grads
+
+    @staticmethod
+    def _unflat(flat, views):
+        off = 0
+        for g in views:
+            k = g.numel()
+            g.copy_(flat[off:off + k].view_as(g))
+            off += k
+
+    @torch.no_grad()
+    def reset_accumulated_grads_(self):
+        self.local_samples_accumulated = 0
+        self.local_times_accumulated = 0
+        if self.arena is not None and self.reuse_grad_buffers:
+            self.arena.zero_grad()
+        else:
+            for p in self.params:
+                if p.grad is not None:
+                    p.grad.zero_()
+            if self._acc is not None:
+                for a in self._acc:
+                    a.zero_()
+
+
+class TrainingStateAverager:
+    """Holds the inner optimizer + scheduler, the local epoch, and averages parameters (D16)."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, scheduler=None, params=None, arena: Optional[FlatArena] = None,
+                 group=None, compression: Optional[CompressionBase] = None, average_state_every: int = 1):
+        self.optimizer = optimizer
+        self.scheduler = scheduler
+        self.params = params
+        self.arena = arena
+        self.group = group
+        self.compression = compression or NoCompression()
+        self.average_state_every = average_state_every
+        self.local_epoch = 0
+
+    @torch.no_grad()
+    def step(self, optimizer_step: bool = True, averaging_round: bool = True):
+        if optimizer_step:
+            self.optimizer.step()
+            if self.scheduler is not None:
+                self.scheduler.step()
+            self.local_epoch += 1
+        if averaging_round and self.average_state_every and self.local_epoch % self.average_state_every == 0:
+            self.average_parameters()
+
+    @torch.no_grad()
+    def average_parameters(self):
+        world, _ = _group_world(self.group)
+        if world == 1:
+            return
+        try:
+            if self.arena is not None:
+                allreduce_weighted(self.arena.data, 1.0, self.group, self.compression, total_weight=float(world))
+            else:
+                flat = torch.cat([p.detach().reshape(-1).float() for p in self.params])
+                allreduce_weighted(flat, 1.0, self.group, self.compression, total_weight=float(world))
+                off = 0
+                for p in self.params:
+                    k = p.numel()
+                    p.data.copy_(flat[off:off + k].view_as(p))
+                    off += k
+        except Exception as e:  # noqa: BLE001
+            logger.warning(f"state averaging failed ({e!r}); keeping local parameters")
+
+
+class CollaborativeOptimizer(torch.optim.Optimizer):
+    """Drop-in for ``hivemind.Optimizer`` as constructed at ``task.py:127-134``."""
+
+    def __init__(self, *, dht=None, run_id: str, params: Union[Iterable, List[dict]],
+                 optimizer: Union[Callable, torch.optim.Optimizer], scheduler: Optional[Callable] = None,
+                 target_batch_size: int, batch_size_per_step: Optional[int] = None, matchmaking_time: float = 15.0,
+                 allreduce_timeout: float = 60.0, averaging_timeout: float = 180.0, offload_optimizer: bool = False,
+                 delay_grad_averaging: bool = False, delay_optimizer_step: bool = False, reuse_grad_buffers: bool = False,
+                 grad_compression: Optional[CompressionBase] = None,
+                 state_averaging_compression: Optional[CompressionBase] = None, average_state_every: int = 1,
+                 client_mode: bool = False, auxiliary: bool = False, verbose: bool = False, process_group=None,
+                 arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "collective",
+                 device=None, **kwargs):
+        self.dht, self.run_id = dht, run_id
+        self.target_batch_size = target_batch_size
+        self.batch_size_per_step = batch_size_per_step
+        self.matchmaking_time, self.allreduce_timeout, self.averaging_timeout = matchmaking_time, allreduce_timeout, averaging_timeout
+        self.offload_optimizer = offload_optimizer
+        self.delay_grad_averaging, self.delay_optimizer_step = delay_grad_averaging, delay_optimizer_step
+        self.client_mode, self.auxiliary, self.verbose = client_mode, auxiliary, verbose
+        self.group = process_group
+        self.arena = arena
+
+        param_groups = list(params)
+        if param_groups and isinstance(param_groups[0], dict):
+            flat_params = [p for g in param_groups for p in g["params"]]
+        else:
+            flat_params = param_groups
+            param_groups = [{"params": flat_params}]
+        self._params = flat_params
+        inner = optimizer(param_groups) if callable(optimizer) and not isinstance(optimizer, torch.optim.Optimizer) else optimizer
+        if arena is not None and getattr(inner, "arena", "missing") is None:
+            inner.arena = arena
+        sched = scheduler(inner) if callable(scheduler) else scheduler
+        device = device or (flat_params[0].device if flat_params else torch.device("cpu"))
+        self.device = device
+        peer_id = dht.peer_id if dht is not None else f"rank{_group_world(process_group)[1]}"
+        self.tracker = ProgressTracker(dht=dht, prefix=run_id, target_batch_size=target_batch_size, group=process_group,
+                                       device=device, client_mode=client_mode, peer_id=peer_id, mode=tracker_mode)
+        psgd = PowerSGD(flat_params, rank=powersgd_rank, group=process_group) if powersgd_rank else None
+        self.grad_averager = GradientAverager(flat_params, arena=arena, group=process_group,
+                                              reuse_grad_buffers=reuse_grad_buffers, compression=grad_compression,
+                                              powersgd=psgd, client_mode=client_mode)
+        self.state_averager = TrainingStateAverager(inner, sched, flat_params, arena=arena, group=process_group,
+                                                    compression=state_averaging_compression,
+                                                    average_state_every=average_state_every)
+        self.last_epoch_time = None
+        if offload_optimizer and device.type == "cuda" and verbose:
+            logger.info("offload_optimizer=True: keeping the optimizer on-GPU (fused HIP LAMB; 288 GB HBM)")
+        # torch.optim.Optimizer protocol (param_groups / state) for trainers and schedulers
+        self.defaults = inner.defaults
+        self._optimizer_step_pre_hooks = {}
+        self._optimizer_step_post_hooks = {}
+
+    # -- torch.optim.Optimizer protocol ------------------------------------------------------------
+    @property
+    def param_groups(self):
+        return self.state_averager.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.state_averager.optimizer.state
+
+    @property
+    def opt(self):
+        return self.state_averager.optimizer
+
+    @property
+    def scheduler(self):
+        return self.state_averager.scheduler
+
+    @property
+    def local_epoch(self) -> int:
+        return self.state_averager.local_epoch
+
+    @local_epoch.setter
+    def local_epoch(self, v: int):
+        self.state_averager.local_epoch = int(v)
+
+    def zero_grad(self, set_to_none: bool = False):
+        if self.grad_averager.reuse_grad_buffers:
+            raise ValueError("zero_grad must not be called with reuse_grad_buffers=True: the optimizer zeroes "
+                             "the accumulated gradients itself after each global step")
+        for p in self._params:
+            if p.grad is not None:
+                if set_to_none:
+                    p.grad = None
+                else:
+                    p.grad.zero_()
+
+    # -- main entry -----------------------------------------------------------------------------------
+    def step(self, closure=None, batch_size: Optional[int] = None, grad_scaler=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self.auxiliary:
+            return loss
+        bs = batch_size if batch_size is not None else self.batch_size_per_step
+        if bs is None:
+            raise ValueError("batch_size_per_step (ctor) or batch_size (step) is required")
+        self.grad_averager.accumulate_grads_(bs)
+        self.tracker.report_local_progress(self.local_epoch, self.grad_averager.local_samples_accumulated)
+        if self.tracker.max_epoch_seen > self.local_epoch + 1:
+            logger.info(f"local epoch {self.local_epoch} lags the collaboration ({self.tracker.max_epoch_seen}); loading state")
+            self.load_state_from_peers()
+            self.grad_averager.reset_accumulated_grads_()
+            return loss
+        if self.tracker.ready_to_update_epoch:
+            self._update_global_epoch()
+        return loss
+
+    def _update_global_epoch(self):
+        t0 = time.perf_counter()
+        total = self.tracker.global_progress.samples_accumulated
+        self.grad_averager.step(total_samples=total)
+        self.state_averager.step(optimizer_step=True, averaging_round=True)
+        self.grad_averager.reset_accumulated_grads_()
+        self.tracker.update_epoch(self.local_epoch)
+        self.last_epoch_time = time.perf_counter() - t0
+        if self.verbose:
+            logger.info(f"{self.run_id}: epoch {self.local_epoch} (averaged {total} samples across "
+                        f"{self.tracker.global_progress.num_peers} peers in {self.last_epoch_time * 1e3:.1f} ms)")
+
+    # -- state --------------------------------------------------------------------------------------
+    def state_dict(self) -> dict:
+        sd = self.opt.state_dict()
+        sd["state"]["local_epoch"] = self.local_epoch
+        return sd
+
+    def load_state_dict(self, state_dict: dict):
+        sd = dict(state_dict)
+        sd["state"] = dict(sd["state"])
+        if "local_epoch" in sd["state"]:
+            self.local_epoch = int(sd["state"].pop("local_epoch"))
+        self.opt.load_state_dict(sd)
+
+    @torch.no_grad()
+    def load_state_from_peers(self, **kwargs) -> bool:
+        """Collective: every rank participates; the donor is the rank with the highest epoch
+        (lowest rank on ties). Broadcasts parameters, optimizer state, scheduler state, epoch (C3)."""
+        world, rank = _group_world(self.group)
+        if world == 1:
+            return False
+        dev = self.device
+        score = torch.tensor([float(self.local_epoch * world + (world - 1 - rank))], device=dev, dtype=torch.float64 if dev.type == "cpu" else torch.float32)
+        dist.all_reduce(score, op=dist.ReduceOp.MAX, group=self.group)
+        best = int(round(score.item()))
+        donor = world - 1 - (best % world)
+        donor_global = dist.get_global_rank(self.group, donor) if self.group is not None else donor
+        if self.arena is not None:
+            dist.broadcast(self.arena.data, src=donor_global, group=self.group)
+        else:
+            for p in self._params:
+                dist.broadcast(p.data, src=donor_global, group=self.group)
+        objs = [self.state_dict() if rank == donor else None]
+        # optimizer state is small relative to params for the 8-bit path; ship it as an object
+        if dev.type == "cuda":
+            objs_cpu = [_to_cpu(objs[0]) if rank == donor else None]
+            dist.broadcast_object_list(objs_cpu, src=donor_global, group=self.group, device=dev)
+            objs = objs_cpu
+        else:
+            dist.broadcast_object_list(objs, src=donor_global, group=self.group)
+        sched = [self.scheduler.state_dict() if (rank == donor and self.scheduler is not None) else None]
+        dist.broadcast_object_list(sched, src=donor_global, group=self.group, device=dev if dev.type == "cuda" else None)
+        if rank != donor:
+            self.load_state_dict(objs[0])
+            if self.scheduler is not None and sched[0] is not None:
+                self.scheduler.load_state_dict(sched[0])
+        self.tracker.update_epoch(self.local_epoch)
+        return rank != donor
+
+    def shutdown(self):
+        self.tracker.shutdown()
+
+
+def _to_cpu(obj):
+    if torch.is_tensor(obj):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
+# hivemind name
+Optimizer = CollaborativeOptimizer
