@@ -86,6 +86,13 @@ def scale_residual(x, o, scale):
     return x + (o * scale.to(o.dtype)).to(x.dtype)
 
 
+def grads_finite(buf: torch.Tensor) -> bool:
+    """K17: one fused NaN/Inf check over a flat fp32 buffer (HIP kernel on GPU)."""
+    if buf.is_cuda and backend_for(buf) == "hip":
+        return int(_hip().nonfinite_flag(buf).item()) == 0
+    return bool(torch.isfinite(buf).all())
+
+
 def residual_add(x, y):
     return x + y.to(x.dtype)
 

@@ -1,0 +1,74 @@
+"""BASELINE config 1 on CPU: tiny DALL-E, two run_trainer.py peers (torchrun, gloo) + an aux peer
+that reads their metrics from the key-value store and snapshots the training state."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    for _ in range(50):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        s2 = socket.socket()
+        try:
+            s2.bind(("127.0.0.1", p + 1))
+            s2.close()
+            return p
+        except OSError:
+            s2.close()
+    raise RuntimeError("no free port pair")
+
+
+COMMON = ["--model_preset", "tiny", "--text_seq_length", "64", "--authorize", "False", "--experiment_prefix", "cfg1",
+          "--dataloader_num_workers", "0"]
+
+
+@pytest.mark.slow
+def test_two_peers_plus_aux(tmp_path):
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", DALLE_AMD_LOGLEVEL="INFO")
+    out = tmp_path / "out"
+    trainer = subprocess.Popen(
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+         "--master-port", str(port), os.path.join(ROOT, "run_trainer.py"), *COMMON, "--per_device_train_batch_size", "2",
+         "--target_batch_size", "8", "--max_steps", "120", "--warmup_steps", "2", "--total_steps", "100",
+         "--output_dir", str(out), "--backup_every_steps", "2", "--state_path", str(tmp_path / "state.zip")],
+        cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    time.sleep(8)
+    metrics_log = tmp_path / "metrics.jsonl"
+    aux = subprocess.run(
+        [sys.executable, os.path.join(ROOT, "run_aux_peer.py"), *COMMON, "--initial_peers", f"/ip4/127.0.0.1/tcp/{port + 1}",
+         "--refresh_period", "0.5", "--max_iterations", "14", "--metrics_log", str(metrics_log),
+         "--save_checkpoint_step_interval", "2", "--local_path", str(tmp_path / "repo"), "--output_dir", str(tmp_path / "aux")],
+        cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    try:
+        tout, _ = trainer.communicate(timeout=300)
+    except subprocess.TimeoutExpired:
+        trainer.kill()
+        raise
+    assert trainer.returncode == 0, tout[-4000:]
+    assert aux.returncode == 0, aux.stdout[-4000:]
+    # 2 peers x 2 samples per step, target 8 -> an epoch every 2 local steps
+    assert "cfg1: epoch 5 (averaged 8 samples across 2 peers" in tout, tout[-3000:]
+    records = [json.loads(l) for l in metrics_log.read_text().splitlines()]
+    assert records and max(r["alive peers"] for r in records) == 2
+    assert all(r["performance"] > 0 for r in records)
+    # the aux peer fetched a state snapshot from the group and wrote reference-format checkpoints
+    assert (tmp_path / "repo" / "model_state.pt").exists()
+    sd = torch.load(tmp_path / "repo" / "model_state.pt", weights_only=True)
+    assert "model.to_logits.1.weight" in sd
+    osd = torch.load(tmp_path / "repo" / "optimizer_state.pt", weights_only=True)
+    assert "local_epoch" in osd["state"]
+    # backups written by the training callback
+    st = torch.load(tmp_path / "state.zip", weights_only=True)
+    assert set(st) == {"model", "training", "scheduler", "local_epoch"}
