@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: text->image top-k sampling, batch 64 on one MI355X, hipGraph-replayed decode.
+
+Reference model recipe (64 layers, 5 shared blocks, reversible) with random-init weights and a
+random-init VQGAN decoder; prints one JSON line with images/s (end-to-end: prefill + 1024 decode
+steps + VQGAN decode) and the per-token decode latency.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dalle_amd.config import get_config  # noqa: E402
+from dalle_amd.models.dalle import DALLE  # noqa: E402
+from dalle_amd.models.vqgan import VQGanVAE  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--model", default="reference")
+    ap.add_argument("--top-k", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-vae", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config(args.model)
+    model = DALLE(cfg).to(dev).eval()
+    if not args.no_vae:
+        model.vae = VQGanVAE().to(dev).eval()
+    text = torch.randint(2, cfg.num_text_tokens, (args.batch, cfg.text_seq_len), device=dev)
+    use_graph = not args.no_graph
+    from dalle_amd.models.generation import DecodeEngine
+    eng = DecodeEngine(model, args.batch, device=dev)
+    model._decode_engine = eng
+    t = time.perf_counter()
+    eng.prefill(model.prepare_text(text))
+    torch.cuda.synchronize()
+    print(f"# prefill {cfg.text_len} positions (eager): {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
+    t = time.perf_counter()
+    for _ in range(8):
+        eng._image_step()
+    torch.cuda.synchronize()
+    print(f"# eager decode step: {(time.perf_counter() - t) / 8 * 1e3:.2f} ms", file=sys.stderr, flush=True)
+    if use_graph:
+        t = time.perf_counter()
+        eng._capture()
+        torch.cuda.synchronize()
+        print(f"# graph capture: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
+    # warm-up generate
+    model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
+    torch.cuda.synchronize()
+    print("# warm-up generate done", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        out = model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.iters
+    eng = model._decode_engine
+    # decode-only timing (graph replays)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if use_graph:
+        for _ in range(64):
+            eng.graph.replay()
+    else:
+        for _ in range(64):
+            eng._image_step()
+    torch.cuda.synchronize()
+    per_tok = (time.perf_counter() - t1) / 64
+    print(json.dumps({"metric": "text->image generation throughput (batch 64, top-k, hipGraph decode)",
+                      "value": round(args.batch / el, 3), "unit": "images/s", "n_gpus": 1,
+                      "seconds_per_batch": round(el, 3), "ms_per_decode_step": round(per_tok * 1e3, 3),
+                      "batch": args.batch, "model": args.model, "depth": cfg.depth, "graph": use_graph,
+                      "vae": not args.no_vae, "out_shape": list(out.shape), "dtype": "bf16",
+                      "data": "random-init weights, synthetic captions"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,10 +19,17 @@ bool ln_shift_bwd(const float*, const float*, const void*, const float*, const f
                   int, int, hipStream_t);
 void geglu_fwd(const void*, void*, long, int, hipStream_t);
 void geglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
-void scale_residual(float*, const void*, const float*, long, int, hipStream_t);
+void geglu_bwd_bias(const void*, const void*, void*, float*, float*, long, int, hipStream_t);
+void scale_residual(const float*, const void*, const float*, float*, long, int, hipStream_t);
 void scale_residual_bwd(const float*, const void*, const float*, void*, float*, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
+void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
+                     hipStream_t);
+void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
+                 hipStream_t);
+void decode_attn(const void*, const void*, const void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
+void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
 void lamb_step(const float*, float*, const float*, float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*,
                const float*, const int*, const long*, const long*, const int*, const float*, const float*, const float*,
@@ -195,11 +202,34 @@ Tensor geglu_bwd(Tensor h, Tensor dout) {
   return dh;
 }
 
+// GEGLU backward + FF-in bias grad (column sums of dh) in one pass: returns {dh, dbias(2F, fp32)}
+std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout) {
+  CHECK_IN(h, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16);
+  const long F2 = h.size(-1);
+  const long M = h.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0 && dout.numel() == M * F2 / 2);
+  auto dh = torch::empty_like(h);
+  auto part = torch::empty({256, F2}, h.options().dtype(torch::kFloat32));
+  auto db = torch::empty({F2}, h.options().dtype(torch::kFloat32));
+  dalle::geglu_bwd_bias(h.data_ptr(), dout.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), db.data_ptr<float>(), M, F2 / 2,
+                        cur_stream());
+  return {dh, db};
+}
+
 void scale_residual_(Tensor x, Tensor y, Tensor scale) {
   CHECK_IN(x, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
   const long D = x.size(-1);
   TORCH_CHECK(D % 8 == 0 && y.numel() == x.numel() && scale.numel() == D);
-  dalle::scale_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), x.numel() / D, D, cur_stream());
+  dalle::scale_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), x.data_ptr<float>(), x.numel() / D, D,
+                        cur_stream());
+}
+
+void scale_residual_out(Tensor x, Tensor y, Tensor scale, Tensor out) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32); CHECK_IN(out, torch::kFloat32);
+  const long D = x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && y.numel() == x.numel() && out.numel() == x.numel() && scale.numel() == D);
+  dalle::scale_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), out.data_ptr<float>(), x.numel() / D, D,
+                        cur_stream());
 }
 
 std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale) {
@@ -207,10 +237,11 @@ std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale) {
   const long D = g.size(-1);
   TORCH_CHECK(D % 8 == 0 && D <= 2048 && y.numel() == g.numel() && scale.numel() == D);
   auto dy = torch::empty(g.sizes(), y.options());
-  auto ws = torch::empty({(512 + 1) * D}, g.options());  // 512 partial rows + the reduced row
+  auto ws = torch::empty({(512 + 1) * 2 * D}, g.options());  // 512 partial rows + the reduced row (2D wide)
   dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), ws.data_ptr<float>(),
                             g.numel() / D, D, cur_stream());
-  return {dy, ws.slice(0, 512 * D, 513 * D)};
+  // {dy = bf16(scale * g), dscale = sum_rows(g * y), gsum = sum_rows(g)}
+  return {dy, ws.slice(0, 512 * 2 * D, 512 * 2 * D + D), ws.slice(0, 512 * 2 * D + D, 513 * 2 * D)};
 }
 
 Tensor nonfinite(Tensor x) {
@@ -227,6 +258,57 @@ Tensor xent_fwd_bwd_(Tensor logits, Tensor labels, double gscale) {
   dalle::xent_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), logits.size(0), logits.size(1),
                       (float)gscale, cur_stream());
   return loss;
+}
+
+// ---------------------------------------------------------------------------------------------
+// decode (KV-cache) path: all positions come from the device scalar `pos` (hipGraph-capturable)
+static dalle::DecodeGeom make_decode_geom(int T, int S, int n, int H, int K, int pattern) {
+  dalle::DecodeGeom g{T, S, n, H, K, pattern};
+  TORCH_CHECK(n <= 2048, "decode attention supports up to 2048 cached positions");
+  TORCH_CHECK(pattern >= 0 && pattern <= 3);
+  return g;
+}
+
+void decode_ln_shift_(Tensor x, Tensor w, Tensor b, Tensor hist, Tensor y, Tensor pos, int64_t T, int64_t S, bool shift) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(b, torch::kFloat32);
+  CHECK_IN(hist, torch::kBFloat16); CHECK_IN(y, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  const int B = x.size(0), D = x.size(-1);
+  TORCH_CHECK(x.numel() == (long)B * D && hist.size(0) == B && hist.size(2) == D && y.numel() == (long)B * D);
+  TORCH_CHECK(D == 256 || D == 512 || D == 1024 || D == 2048, "decode_ln_shift: unsupported hidden size");
+  auto g = make_decode_geom(T, S, hist.size(1), 1, 1, 0);
+  dalle::decode_ln_shift(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), hist.data_ptr(), y.data_ptr(),
+                         pos.data_ptr<int>(), g, B, D, shift ? 1 : 0, cur_stream());
+}
+
+void decode_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, Tensor pos, int64_t H, double qscale) {
+  CHECK_IN(qkv, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  const int B = qkv.size(0);
+  TORCH_CHECK(qkv.numel() == (long)B * 3 * H * 64 && q.numel() == (long)B * H * 64);
+  TORCH_CHECK(kc.size(0) == B * H && kc.size(2) == 64 && vc.sizes() == kc.sizes() && cosT.size(0) >= kc.size(1));
+  auto g = make_decode_geom(1, 1, kc.size(1), H, 1, 0);
+  dalle::decode_rope(qkv.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                     pos.data_ptr<int>(), g, B, (float)qscale, cur_stream());
+}
+
+void decode_attn_(Tensor q, Tensor kc, Tensor vc, Tensor out, Tensor pos, int64_t T, int64_t S, int64_t H, int64_t K,
+                  int64_t pattern) {
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16);
+  CHECK_IN(out, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  const int BH = kc.size(0);
+  TORCH_CHECK(BH % H == 0 && q.numel() == (long)BH * 64 && out.numel() == (long)BH * 64 && vc.sizes() == kc.sizes());
+  TORCH_CHECK(kc.size(1) == T + S * S - 1, "decode cache must hold the full sequence");
+  auto g = make_decode_geom(T, S, kc.size(1), H, K, pattern);
+  dalle::decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, BH / H, cur_stream());
+}
+
+Tensor vq_embed(Tensor idx, Tensor codebook, int64_t side) {
+  CHECK_IN(idx, torch::kInt64); CHECK_IN(codebook, torch::kFloat32);
+  const int B = idx.size(0), HW = idx.size(1), C = codebook.size(1);
+  TORCH_CHECK(HW == side * side);
+  auto z = torch::empty({B, C, side, side}, codebook.options());
+  dalle::vq_embed(idx.data_ptr<int64_t>(), codebook.data_ptr<float>(), z.data_ptr<float>(), HW, C, B, cur_stream());
+  return z;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -270,10 +352,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
+  m.def("geglu_bwd_bias", &geglu_bwd_bias);
   m.def("scale_residual_", &scale_residual_);
+  m.def("scale_residual_out", &scale_residual_out);
   m.def("scale_residual_bwd", &scale_residual_bwd);
   m.def("nonfinite", &nonfinite);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
+  m.def("decode_ln_shift_", &decode_ln_shift_);
+  m.def("decode_rope_", &decode_rope_);
+  m.def("decode_attn_", &decode_attn_);
+  m.def("vq_embed", &vq_embed);
   m.def("lamb_grad_norm", &lamb_grad_norm);
   m.def("lamb_step", &lamb_step);
 }

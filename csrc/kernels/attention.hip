@@ -368,8 +368,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
   const int bh = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nkb = g.Np >> 5, ntext = g.Tp >> 5;
-  // heaviest (text) key blocks first: blockIdx.x enumerates key-block groups in order
-  const int kb0 = blockIdx.x * 4;
+  // image (local) key blocks only: text key blocks go to attn_bwd_dkdv_text_kernel
+  const int kb0 = ntext + blockIdx.x * 4;
   const int kb = kb0 + wave;
   const int kb_last = min(kb0 + 3, nkb - 1);
   const bool active = kb < nkb;
@@ -478,6 +478,142 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
 }
 
 // ------------------------------------------------------------------------------------------------
+// Backward dK / dV for the TEXT key blocks: every later query tile (all image queries see all
+// text keys) attends to them, so one workgroup owns ONE 32-key block and its 4 waves split the
+// query tiles round-robin (balanced; 4x shorter critical path than one wave per key block). Each
+// wave stages its own Q/dO tile (wave-private double buffer, register prefetch one tile ahead);
+// the four partial dK/dV accumulators are summed through LDS at the end.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
+                                                                    const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
+                                                                    const float* __restrict__ lse, const float* __restrict__ delta,
+                                                                    __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
+  // per wave: 2 buffers x {Q, dO} x 32 rows x RS   +  2 buffers x {lse, delta} x 32
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * 2 * 32 * RS];
+  __shared__ float stats[4][2][2][32];
+  const int bh = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
+  const int nqb = g.Np >> 5;
+  const int kb = blockIdx.x;
+  const size_t base = (size_t)bh * g.Np * 64;
+  const int ks = kb * 32 + c32;
+  bf16x8 kf[4], vf[4];
+  {
+    const __bf16* kp = Kt + base + (size_t)ks * 64 + 8 * hl;
+    const __bf16* vp = V + base + (size_t)ks * 64 + 8 * hl;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { kf[s] = ld16(kp + 16 * s); vf[s] = ld16(vp + 16 * s); }
+  }
+  __bf16* wsm = smem + wave * (2 * 2 * 32 * RS);
+  const int first = kb + wave;
+  const int ntiles = first < nqb ? (nqb - first + 3) / 4 : 0;
+  // lane-private staging: 4 chunks of Q and 4 of dO per tile (32 rows x 8 chunks of 16 B)
+  s16x8 qreg[4], dreg[4];
+  float lreg = 0.f, dlreg = 0.f;
+  auto load_tile = [&](int qt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      const size_t off = base + (size_t)(qt * 32 + row) * 64 + col;
+      qreg[j] = *reinterpret_cast<const s16x8*>(Q + off);
+      dreg[j] = *reinterpret_cast<const s16x8*>(dO + off);
+    }
+    if (lane < 32) {
+      lreg = lse[(size_t)bh * g.Np + qt * 32 + lane];
+      dlreg = delta[(size_t)bh * g.Np + qt * 32 + lane];
+    }
+  };
+  auto store_tile = [&](int buf) {
+    __bf16* Qs = wsm + buf * (2 * 32 * RS);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<s16x8*>(Qs + row * RS + col) = qreg[j];
+      *reinterpret_cast<s16x8*>(Qs + 32 * RS + row * RS + col) = dreg[j];
+    }
+    if (lane < 32) { stats[wave][buf][0][lane] = lreg; stats[wave][buf][1][lane] = dlreg; }
+  };
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  if (ntiles > 0) {
+    load_tile(first);
+    store_tile(0);
+  }
+  for (int i = 0; i < ntiles; ++i) {
+    const int qt = first + 4 * i;
+    const bool more = i + 1 < ntiles;
+    if (more) load_tile(qt + 4);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores of the current tile landed
+    __builtin_amdgcn_wave_barrier();
+    const int buf = i & 1;
+    const __bf16* Qs = wsm + buf * (2 * 32 * RS);
+    const __bf16* Ds = Qs + 32 * RS;
+    f32x16 s = {}, dp = {};
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) {
+      s = MFMA32(ld16(Qs + c32 * RS + 16 * ss + 8 * hl), kf[ss], s);
+      dp = MFMA32(ld16(Ds + c32 * RS + 16 * ss + 8 * hl), vf[ss], dp);
+    }
+    f32x16 ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = acc_row(r, hl);
+      const int qs = qt * 32 + ql;
+      const float p = allowed_st(g, qs, ks) ? exp2f(s[r] * LOG2E - stats[wave][buf][0][ql]) : 0.f;
+      s[r] = p;
+      ds[r] = p * (dp[r] - stats[wave][buf][1][ql]);
+    }
+    const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
+    const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
+    dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
+    dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
+    dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
+    dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
+    dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
+    dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
+    dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
+    dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
+    if (more) {
+      __builtin_amdgcn_wave_barrier();  // every lane finished reading the other buffer (tile i-1)
+      store_tile(buf ^ 1);
+    }
+  }
+  // reduce the 4 waves' partial dK^T / dV^T through LDS (reuse the staging area: 4 x 64 x 64 floats)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // 4 waves x 64 lanes x 64 values (16 KB... x4 = 64 KB)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[(wave * 64 + lane) * 64 + r] = dk0[r];
+    red[(wave * 64 + lane) * 64 + 16 + r] = dk1[r];
+    red[(wave * 64 + lane) * 64 + 32 + r] = dv0[r];
+    red[(wave * 64 + lane) * 64 + 48 + r] = dv1[r];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    __bf16* kp = dK + base + (size_t)ks * 64;
+    __bf16* vp = dV + base + (size_t)ks * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        float fa[4], fc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * gq + i;
+          fa[i] = fc[i] = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            fa[i] += red[(w * 64 + lane) * 64 + dt * 16 + r];
+            fc[i] += red[(w * 64 + lane) * 64 + 32 + dt * 16 + r];
+          }
+        }
+        *reinterpret_cast<s16x4*>(kp + 32 * dt + 8 * gq + 4 * hl) = pack4(fa);
+        *reinterpret_cast<s16x4*>(vp + 32 * dt + 8 * gq + 4 * hl) = pack4(fc);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
@@ -494,8 +630,13 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   dim3 grid((g.Np / 32 + 3) / 4, BH);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                      (const __bf16*)do_st, lse, delta, (__bf16*)dq, g);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                     (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
+  const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
+  // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
+  hipLaunchKernelGGL(attn_bwd_dkdv_text_kernel, dim3(ntext, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                     (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
+  // image key blocks (short, local patterns): four blocks per workgroup
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((nimg + 3) / 4, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                     (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
 }
 
 }  // namespace dalle

@@ -1,0 +1,218 @@
+// Autoregressive decode kernels (SURVEY K7f, K4 cached token shift, K6 rotary into the KV cache,
+// K19 VQGAN codebook embed). Every positional argument is a DEVICE scalar (`pos`) so one decode
+// step -- all layers plus sampling -- can be captured once into a hipGraph and replayed for each of
+// the 1024 image tokens.
+#include "common.h"
+#include "geom.h"
+
+namespace dalle {
+
+// ---- LayerNorm of the new token, append to the per-branch LN history, emit the shifted row ----
+template <int D>
+__global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, __bf16* __restrict__ hist,
+                                                             __bf16* __restrict__ y, const int* __restrict__ pos_ptr,
+                                                             DecodeGeom g, int shift) {
+  constexpr int PER = D / 256;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int pos = *pos_ptr;
+  const float* xr = x + (size_t)b * D;
+  f32x4 v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = *reinterpret_cast<const f32x4*>(xr + 4 * (lane + 64 * j));
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+  __bf16* hb = hist + (size_t)b * g.n * D;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[i] + bv[i];
+    const s16x4 packed = pack4(o);
+    *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
+    s16x4 outv = packed;
+    if (shift && c < D / 2) {
+      int src = -1;
+      if (pos < g.T) {
+        src = pos - 1;
+      } else {
+        const int k = pos - g.T;
+        if (c < D / 4) src = (k >= g.S) ? pos - g.S : -1;
+        else src = (k % g.S) ? pos - 1 : -1;
+      }
+      if (src >= 0) outv = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
+      else outv = s16x4{};
+    }
+    *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = outv;
+  }
+}
+
+// ---- rotary on q/k/v of the new token; k, v appended to the cache at `pos` ----
+__global__ void decode_rope_kernel(const __bf16* __restrict__ qkv, const float* __restrict__ cosT, const float* __restrict__ sinT,
+                                   __bf16* __restrict__ q_out, __bf16* __restrict__ kc, __bf16* __restrict__ vc,
+                                   const int* __restrict__ pos_ptr, DecodeGeom g, int B, float qscale) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;  // (b, h, chunk)
+  if (gid >= B * g.H * 8) return;
+  const int chunk = gid & 7, bh = gid >> 3;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int pos = *pos_ptr;
+  const int HD = g.H * 64;
+  const size_t src = (size_t)b * 3 * HD + h * 64 + chunk * 8;
+  float c[8], sn[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { c[i] = cosT[pos * 64 + chunk * 8 + i]; sn[i] = sinT[pos * 64 + chunk * 8 + i]; }
+  __bf16* dst[3] = {q_out + (size_t)bh * 64 + chunk * 8, kc + ((size_t)bh * g.n + pos) * 64 + chunk * 8,
+                    vc + ((size_t)bh * g.n + pos) * 64 + chunk * 8};
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    float x[8];
+    unpack8(*reinterpret_cast<const s16x8*>(qkv + src + t * HD), x);
+    float r[8];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      r[i] = x[i] * c[i] + x[i + 1] * sn[i];
+      r[i + 1] = x[i + 1] * c[i + 1] + x[i] * sn[i + 1];
+    }
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] *= qscale;
+    }
+    *reinterpret_cast<s16x8*>(dst[t]) = pack8(r);
+  }
+}
+
+__device__ __forceinline__ int decode_num_keys(const DecodeGeom& g, int pos, int& nloc, int& r0, int& c0, int& nr, int& nc) {
+  // text keys [0, min(T, pos+1)), then an image-local rectangle (rows r0.., cols c0..) clipped by causality
+  if (pos < g.T) { nloc = 0; return pos + 1; }
+  const int k = pos - g.T, r = k / g.S, c = k % g.S;
+  if (g.pattern == 0) { nloc = k + 1; r0 = 0; c0 = 0; nr = 0; nc = 0; return g.T + nloc; }
+  if (g.pattern == 1) { r0 = r; nr = 1; c0 = 0; nc = c + 1; }
+  else if (g.pattern == 2) { r0 = 0; nr = r + 1; c0 = c; nc = 1; }
+  else { r0 = max(0, r - g.K + 1); nr = r - r0 + 1; c0 = max(0, c - g.K + 1); nc = c - c0 + 1; }
+  nloc = nr * nc;
+  return g.T + nloc;
+}
+
+__device__ __forceinline__ int decode_key_at(const DecodeGeom& g, int i, int pos, int r0, int c0, int nc) {
+  if (pos < g.T || i < g.T) return i;  // text keys
+  const int l = i - g.T;
+  if (g.pattern == 0) return g.T + l;
+  const int rr = r0 + l / nc, cc = c0 + l % nc;
+  return g.T + rr * g.S + cc;
+}
+
+// ---- one query per (b, h) against its allowed cached keys; scores in LDS, PV over 4 key groups ----
+__global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ kc,
+                                                          const __bf16* __restrict__ vc, __bf16* __restrict__ out,
+                                                          const int* __restrict__ pos_ptr, DecodeGeom g) {
+  __shared__ float qs[64];
+  __shared__ float sc[2048];
+  __shared__ float red[8];
+  __shared__ float part[4][64];
+  const int bh = blockIdx.x, tid = threadIdx.x;
+  const int pos = *pos_ptr;
+  if (tid < 64) qs[tid] = bf2f(reinterpret_cast<const bf16_raw*>(q)[(size_t)bh * 64 + tid]);
+  __syncthreads();
+  int nloc, r0 = 0, c0 = 0, nr = 0, nc = 1;
+  const int nkeys = decode_num_keys(g, pos, nloc, r0, c0, nr, nc);
+  const __bf16* kb = kc + (size_t)bh * g.n * 64;
+  const __bf16* vb = vc + (size_t)bh * g.n * 64;
+  float mloc = NEG_BIG;
+  for (int i = tid; i < nkeys; i += 256) {
+    const int j = decode_key_at(g, i, pos, r0, c0, nc);
+    const __bf16* kr = kb + (size_t)j * 64;
+    float acc = 0.f;
+#pragma unroll
+    for (int d8 = 0; d8 < 8; ++d8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const s16x8*>(kr + 8 * d8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += f[e] * qs[8 * d8 + e];
+    }
+    acc *= LOG2E;
+    sc[i] = acc;
+    mloc = fmaxf(mloc, acc);
+  }
+  mloc = wave_max(mloc);
+  if ((tid & 63) == 0) red[tid >> 6] = mloc;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float ssum = 0.f;
+  for (int i = tid; i < nkeys; i += 256) {
+    const float p = exp2f(sc[i] - m);
+    sc[i] = p;
+    ssum += p;
+  }
+  ssum = wave_sum(ssum);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = ssum;
+  __syncthreads();
+  const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
+  const int d = tid & 63, grp = tid >> 6;
+  float acc = 0.f;
+  for (int i = grp; i < nkeys; i += 4) {
+    const int j = decode_key_at(g, i, pos, r0, c0, nc);
+    acc += sc[i] * bf2f(reinterpret_cast<const bf16_raw*>(vb)[(size_t)j * 64 + d]);
+  }
+  part[grp][d] = acc;
+  __syncthreads();
+  if (grp == 0) {
+    const int b = bh / g.H, h = bh - b * g.H;
+    const float o = (part[0][d] + part[1][d] + part[2][d] + part[3][d]) * inv;
+    reinterpret_cast<bf16_raw*>(out)[(size_t)b * g.H * 64 + h * 64 + d] = f2bf(o);
+  }
+}
+
+// ---- VQGAN codebook embed: z[b, c, y, x] = codebook[idx[b, y*W + x], c]  (one_hot @ codebook) ----
+__global__ void vq_embed_kernel(const int64_t* __restrict__ idx, const float* __restrict__ codebook, float* __restrict__ z,
+                                int HW, int C, int B) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over (b, c, pixel): pixel fastest
+  if (gid >= (long)B * C * HW) return;
+  const int p = gid % HW;
+  const long bc = gid / HW;
+  const int c = bc % C, b = bc / C;
+  const int64_t code = idx[(long)b * HW + p];
+  z[gid] = codebook[code * C + c];
+}
+
+void decode_ln_shift(const float* x, const float* w, const float* b, void* hist, void* y, const int* pos, const DecodeGeom& g,
+                     int B, int D, int shift, hipStream_t st) {
+  switch (D) {
+    case 256: hipLaunchKernelGGL(decode_ln_shift_kernel<256>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
+    case 512: hipLaunchKernelGGL(decode_ln_shift_kernel<512>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
+    case 1024: hipLaunchKernelGGL(decode_ln_shift_kernel<1024>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
+    case 2048: hipLaunchKernelGGL(decode_ln_shift_kernel<2048>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
+  }
+}
+
+void decode_rope(const void* qkv, const float* cosT, const float* sinT, void* q, void* kc, void* vc, const int* pos,
+                 const DecodeGeom& g, int B, float qscale, hipStream_t st) {
+  const int threads = B * g.H * 8;
+  hipLaunchKernelGGL(decode_rope_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, (const __bf16*)qkv, cosT, sinT,
+                     (__bf16*)q, (__bf16*)kc, (__bf16*)vc, pos, g, B, qscale);
+}
+
+void decode_attn(const void* q, const void* kc, const void* vc, void* out, const int* pos, const DecodeGeom& g, int B,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(decode_attn_kernel, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vc,
+                     (__bf16*)out, pos, g);
+}
+
+void vq_embed(const int64_t* idx, const float* codebook, float* z, int HW, int C, int B, hipStream_t st) {
+  const long t = (long)B * C * HW;
+  hipLaunchKernelGGL(vq_embed_kernel, dim3((t + 255) / 256), dim3(256), 0, st, idx, codebook, z, HW, C, B);
+}
+
+}  // namespace dalle

@@ -42,9 +42,41 @@ __global__ void geglu_bwd_kernel(const __bf16* __restrict__ h, const __bf16* __r
   *reinterpret_cast<s16x8*>(dh + r * 2 * F + F + c) = pack8(dg);
 }
 
+// GEGLU backward fused with the FF-in bias gradient: grid (row blocks, F/2048 column blocks); each
+// thread owns 8 columns j (and F+j), walks its rows, and leaves one partial [2F] row per row block
+// (column-summed afterwards) -- no separate reduction over the (M, 2F) gradient.
+__global__ __launch_bounds__(256) void geglu_bwd_bias_kernel(const __bf16* __restrict__ h, const __bf16* __restrict__ dout,
+                                                             __bf16* __restrict__ dh, float* __restrict__ part, long M, int F) {
+  const int j = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (j >= F) return;
+  float sa[8] = {}, sg[8] = {};
+  for (long r = blockIdx.x; r < M; r += gridDim.x) {
+    float a[8], gg[8], d[8], da[8], dg[8];
+    unpack8(*reinterpret_cast<const s16x8*>(h + r * 2 * F + j), a);
+    unpack8(*reinterpret_cast<const s16x8*>(h + r * 2 * F + F + j), gg);
+    unpack8(*reinterpret_cast<const s16x8*>(dout + r * F + j), d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      da[i] = d[i] * gelu_erf(gg[i]);
+      dg[i] = d[i] * a[i] * gelu_erf_grad(gg[i]);
+    }
+    const s16x8 pa = pack8(da), pg = pack8(dg);
+    *reinterpret_cast<s16x8*>(dh + r * 2 * F + j) = pa;
+    *reinterpret_cast<s16x8*>(dh + r * 2 * F + F + j) = pg;
+    float ra[8], rg[8];
+    unpack8(pa, ra);  // bias grad of the values actually propagated (bf16), as a GEMM epilogue would
+    unpack8(pg, rg);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sa[i] += ra[i]; sg[i] += rg[i]; }
+  }
+  float* prow = part + (size_t)blockIdx.x * 2 * F;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { prow[j + i] = sa[i]; prow[F + j + i] = sg[i]; }
+}
+
 // x (fp32, M x D) += scale[D] * y (bf16)   -- LayerScale fused into the residual add, in place
-__global__ void scale_residual_kernel(float* __restrict__ x, const __bf16* __restrict__ y, const float* __restrict__ scale,
-                                      long M, int D) {
+__global__ void scale_residual_kernel(const float* x, const __bf16* __restrict__ y, const float* __restrict__ scale,
+                                      float* out, long M, int D) {
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int per_row = D / 8;
   if (gid >= M * per_row) return;
@@ -52,14 +84,15 @@ __global__ void scale_residual_kernel(float* __restrict__ x, const __bf16* __res
   const int c = (gid - r * per_row) * 8;
   float yv[8];
   unpack8(*reinterpret_cast<const s16x8*>(y + r * D + c), yv);
-  f32x4* xp = reinterpret_cast<f32x4*>(x + r * D + c);
+  const f32x4* xp = reinterpret_cast<const f32x4*>(x + r * D + c);
   const f32x4* sp = reinterpret_cast<const f32x4*>(scale + c);
   f32x4 x0 = xp[0], x1 = xp[1];
   const f32x4 s0 = sp[0], s1 = sp[1];
 #pragma unroll
   for (int i = 0; i < 4; ++i) { x0[i] += s0[i] * yv[i]; x1[i] += s1[i] * yv[4 + i]; }
-  xp[0] = x0;
-  xp[1] = x1;
+  f32x4* op = reinterpret_cast<f32x4*>(out + r * D + c);
+  op[0] = x0;
+  op[1] = x1;
 }
 
 // dy = bf16(scale * g); dscale partials: per block column sums of g * y -> atomics into dscale
@@ -73,7 +106,7 @@ __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __
   const int trow = threadIdx.x / cols8;
   const bool on = trow < rows_per_iter;
   const int c = tcol * 8;
-  float acc[8] = {};
+  float acc[8] = {}, gsum[8] = {};
   float sc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) sc[i] = scale[c + i];
@@ -86,23 +119,28 @@ __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __
     for (int i = 0; i < 4; ++i) {
       acc[i] += g0[i] * yv[i];
       acc[4 + i] += g1[i] * yv[4 + i];
+      gsum[i] += g0[i];
+      gsum[4 + i] += g1[i];
       o[i] = g0[i] * sc[i];
       o[4 + i] = g1[i] * sc[4 + i];
     }
     *reinterpret_cast<s16x8*>(dy + r * D + c) = pack8(o);
   }
-  // deterministic reduction: threads of one column -> LDS -> one partial row per block (no atomics)
+  // deterministic reduction: threads of one column -> LDS -> one partial row [sum g*y | sum g] per block
   __shared__ float red[256 * 8];
+  for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) red[threadIdx.x * 8 + i] = on ? acc[i] : 0.f;
-  __syncthreads();
-  if (on && trow == 0) {
+    for (int i = 0; i < 8; ++i) red[threadIdx.x * 8 + i] = on ? (pass ? gsum[i] : acc[i]) : 0.f;
+    __syncthreads();
+    if (on && trow == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float sum = 0.f;
-      for (int r = 0; r < rows_per_iter; ++r) sum += red[(r * cols8 + tcol) * 8 + i];
-      dscale[(size_t)blockIdx.x * D + c + i] = sum;
+      for (int i = 0; i < 8; ++i) {
+        float sum = 0.f;
+        for (int r = 0; r < rows_per_iter; ++r) sum += red[(r * cols8 + tcol) * 8 + i];
+        dscale[(size_t)blockIdx.x * 2 * D + pass * D + c + i] = sum;
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -128,17 +166,23 @@ void geglu_bwd(const void* h, const void* dout, void* dh, long M, int F, hipStre
   hipLaunchKernelGGL(geglu_bwd_kernel, dim3((t + 255) / 256), dim3(256), 0, st, (const __bf16*)h, (const __bf16*)dout,
                      (__bf16*)dh, M, F);
 }
-void scale_residual(float* x, const void* y, const float* scale, long M, int D, hipStream_t st) {
+constexpr int GEGLU_ROW_BLOCKS = 256;
+void geglu_bwd_bias(const void* h, const void* dout, void* dh, float* part, float* dbias, long M, int F, hipStream_t st) {
+  dim3 grid(GEGLU_ROW_BLOCKS, (F / 8 + 255) / 256);
+  hipLaunchKernelGGL(geglu_bwd_bias_kernel, grid, dim3(256), 0, st, (const __bf16*)h, (const __bf16*)dout, (__bf16*)dh, part, M, F);
+  column_sum(part, GEGLU_ROW_BLOCKS, 2 * F, dbias, st);
+}
+void scale_residual(const float* x, const void* y, const float* scale, float* out, long M, int D, hipStream_t st) {
   const long t = M * (D / 8);
-  hipLaunchKernelGGL(scale_residual_kernel, dim3((t + 255) / 256), dim3(256), 0, st, x, (const __bf16*)y, scale, M, D);
+  hipLaunchKernelGGL(scale_residual_kernel, dim3((t + 255) / 256), dim3(256), 0, st, x, (const __bf16*)y, scale, out, M, D);
 }
 void scale_residual_bwd(const float* g, const void* y, const float* scale, void* dy, float* dscale, long M, int D,
                         hipStream_t st) {
-  // dscale points at [SR_BWD_BLOCKS x D partial rows | D outputs]
+  // dscale points at [SR_BWD_BLOCKS x 2D partial rows | 2D outputs = (sum_rows g*y, sum_rows g)]
   const int blocks = SR_BWD_BLOCKS;
   hipLaunchKernelGGL(scale_residual_bwd_kernel, dim3(blocks), dim3(256), 0, st, g, (const __bf16*)y, scale, (__bf16*)dy, dscale,
                      M, D);
-  column_sum(dscale, blocks, D, dscale + (size_t)blocks * D, st);
+  column_sum(dscale, blocks, 2 * D, dscale + (size_t)blocks * 2 * D, st);
 }
 void nonfinite(const float* x, long n, int* flag, hipStream_t st) {
   long blocks = (n / 4 + 255) / 256;

@@ -16,6 +16,14 @@ struct AttnGeom {
 struct RopeGeom {
   int T, Tp, S, logS, n, Np, H, col_major;
 };
+struct DecodeGeom {
+  int T;        // text positions incl. BOS
+  int S;        // image side
+  int n;        // cache length (seq_len)
+  int H;        // heads
+  int K;        // conv window
+  int pattern;  // 0 full, 1 axial_row, 2 axial_col, 3 conv_like
+};
 struct ShiftGeom {
   int n;      // sequence length
   int T;      // text_len (BOS + text)

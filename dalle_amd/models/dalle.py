@@ -174,9 +174,16 @@ class Transformer(nn.Module):
             fns = [(lambda t, f=f: ops.scale_rows(self._attn_out(f, t), f.scale),
                     lambda t, g=g: ops.scale_rows(self._ff_out(g, t), g.scale)) for f, g in pairs]
             return reversible_sequence(x, fns)
+        cfg = self.cfg
         for f, g in pairs:
-            x = ops.scale_residual(x, self._attn_out(f, x), f.scale)
-            x = ops.scale_residual(x, self._ff_out(g, x), g.scale)
+            pre, attn = f.fn, f.fn.fn.fn
+            h = ops.layernorm_shift(x, pre.norm.weight, pre.norm.bias, cfg.text_len, cfg.image_fmap_size, pre.fn.enabled)
+            o = ops.attention_out(h, attn.to_qkv.weight, attn.heads, self.geom, attn.attn_type)
+            x = ops.proj_residual(x, o, attn.to_out[0].weight, attn.to_out[0].bias, f.scale)
+            pre, ff = g.fn, g.fn.fn.fn
+            h = ops.layernorm_shift(x, pre.norm.weight, pre.norm.bias, cfg.text_len, cfg.image_fmap_size, pre.fn.enabled)
+            u = ops.ff_hidden(h, ff.net[0].weight, ff.net[0].bias)
+            x = ops.proj_residual(x, u, ff.net[3].weight, ff.net[3].bias, g.scale)
         return x
 
 
@@ -254,6 +261,27 @@ class DALLE(nn.Module):
         labels = torch.cat([text_bos[:, 1:], image + self.num_text_tokens], dim=1)
         return ops.logits_loss(out, norm.weight, norm.bias, head.weight, head.bias, labels,
                                self.text_seq_len, self.num_text_tokens, self.loss_img_weight)
+
+    # -- generation (D11) -------------------------------------------------------------------------
+    @torch.no_grad()
+    def generate_images(self, text, *, clip=None, mask=None, filter_thres=None, temperature: float = 1.0, img=None,
+                        num_init_img_tokens=None, top_k: int = 0, top_p: float = 1.0, use_cache: bool = True,
+                        return_codes: bool = False, use_graph=None):
+        """Sample 1024 image tokens per caption with the KV-cache decoder (hipGraph-replayed on MI355X)
+        and decode them with ``self.vae`` to (b, 3, H, W) images in [0, 1] (codes if no VAE)."""
+        from .generation import DecodeEngine
+
+        if filter_thres is not None and not top_k:
+            top_k = max(1, int((1 - filter_thres) * self.num_image_tokens))
+        text_bos = self.prepare_text(text)
+        eng = getattr(self, "_decode_engine", None)
+        if eng is None or eng.B != text.shape[0] or eng.device != text.device:
+            eng = DecodeEngine(self, text.shape[0], device=text.device)
+            self._decode_engine = eng
+        codes = eng.generate(text_bos, temperature=temperature, top_k=top_k, top_p=top_p, use_graph=use_graph)
+        if return_codes or self.vae is None:
+            return codes
+        return self.vae.decode(codes)
 
     # -- checkpoint helpers --------------------------------------------------------------------
     def unique_parameters(self) -> List[nn.Parameter]:

@@ -1,0 +1,256 @@
+"""Autoregressive text->image decoding with a KV cache (BASELINE config 5).
+
+One decode step pushes ONE position through every layer: fused LayerNorm + cached token shift
+(per-branch LN history), QKV GEMM, rotary into the KV cache, sparse decode attention over only the
+keys the layer's static pattern allows (text prefix + row / column / 5x5 window), output GEMM,
+LayerScale residual, then the final norm, the image-vocabulary head and sampling (temperature,
+top-k, top-p, Gumbel-max). Every positional quantity is read from a device scalar, so on MI355X the
+whole step is captured ONCE into a hipGraph and replayed for each of the 1024 image tokens.
+
+The CPU path runs the same step with the reference ops (tests compare it against the full forward).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .patterns import PATTERN_IDS, static_mask
+from .rotary import rotary_tables
+
+
+def filter_logits(logits: torch.Tensor, top_k: int = 0, top_p: float = 1.0) -> torch.Tensor:
+    """K18: top-k then nucleus filtering (fill -inf); graph-capturable (no host sync)."""
+    if top_k and top_k > 0:
+        kth = torch.topk(logits, min(top_k, logits.shape[-1]), dim=-1).values[..., -1:]
+        logits = logits.masked_fill(logits < kth, float("-inf"))
+    if top_p is not None and top_p < 1.0:
+        sorted_logits, sorted_idx = torch.sort(logits, descending=True, dim=-1)
+        cum = torch.softmax(sorted_logits, dim=-1).cumsum(-1)
+        remove = cum - torch.softmax(sorted_logits, dim=-1) > top_p  # keep the token that crosses top_p
+        sorted_logits = sorted_logits.masked_fill(remove, float("-inf"))
+        logits = torch.full_like(logits, float("-inf")).scatter(-1, sorted_idx, sorted_logits)
+    return logits
+
+
+def gumbel_sample(logits: torch.Tensor, temperature: float = 1.0, generator=None) -> torch.Tensor:
+    u = torch.rand(logits.shape, device=logits.device, generator=generator).clamp_(1e-20, 1.0)
+    return torch.argmax(logits / max(temperature, 1e-10) - torch.log(-torch.log(u)), dim=-1)
+
+
+class DecodeEngine:
+    def __init__(self, model, batch_size: int, device=None, use_hip: Optional[bool] = None):
+        self.model = model
+        cfg = self.cfg = model.cfg
+        self.B = batch_size
+        self.device = device or next(model.parameters()).device
+        dev = self.device
+        if use_hip is None:
+            from ..ops.ext import hip_available
+            use_hip = dev.type == "cuda" and hip_available()
+        self.use_hip = use_hip
+        self.T, self.S, self.n = cfg.text_len, cfg.image_fmap_size, cfg.seq_len
+        self.H, self.Dh, self.d = cfg.heads, cfg.dim_head, cfg.dim
+        self.Vt = cfg.total_text_tokens
+        self.cdt = torch.bfloat16 if use_hip else torch.float32
+        tr = model.transformer
+        self.pairs = tr.layers.pairs()
+        self.geom = tr.geom
+        L, B = len(self.pairs), batch_size
+        self.kc = [torch.zeros(B * self.H, self.n, self.Dh, dtype=self.cdt, device=dev) for _ in range(L)]
+        self.vc = [torch.zeros_like(k) for k in self.kc]
+        self.hist = [[torch.zeros(B, self.n, self.d, dtype=self.cdt, device=dev) for _ in range(2)] for _ in range(L)]
+        self.cos, self.sin = rotary_tables(self.T, self.S, self.Dh, device=dev)
+        self.pos = torch.zeros((), dtype=torch.int32, device=dev)
+        self.tok = torch.zeros(B, dtype=torch.long, device=dev)
+        self.hbuf = torch.zeros(B, self.d, dtype=self.cdt, device=dev)
+        self.qbuf = torch.zeros(B, self.H, self.Dh, dtype=self.cdt, device=dev)
+        self.obuf = torch.zeros(B, self.H * self.Dh, dtype=self.cdt, device=dev)
+        self.codes = torch.zeros(B, cfg.image_seq_len, dtype=torch.long, device=dev)
+        self.temperature, self.top_k, self.top_p = 1.0, 0, 1.0
+        self.graph = None
+        self._static_logits = None
+        self._w = {}
+
+    # -- weights (one bf16 cast per generate call) --------------------------------------------------
+    def _wt(self, p):
+        w = self._w.get(id(p))
+        if w is None:
+            w = p.detach().to(self.cdt)
+            self._w[id(p)] = w
+        return w
+
+    def reset(self):
+        self.pos.zero_()
+        self._w.clear()
+        for k in self.kc + self.vc:
+            k.zero_()
+
+    # -- branch steps -------------------------------------------------------------------------------
+    def _ln_shift(self, ls, hist, x):
+        pre = ls.fn
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            C().decode_ln_shift_(x.contiguous(), pre.norm.weight.detach(), pre.norm.bias.detach(), hist, self.hbuf, self.pos,
+                                 self.T, self.S, bool(pre.fn.enabled))
+            return self.hbuf
+        y = F.layer_norm(x, (self.d,), pre.norm.weight, pre.norm.bias)
+        p = int(self.pos)
+        hist[:, p] = y
+        if not pre.fn.enabled:
+            return y
+        out = y.clone()
+        q, h2 = self.d // 4, self.d // 2
+        if p < self.T:
+            out[:, :h2] = hist[:, p - 1, :h2] if p >= 1 else 0.0
+        else:
+            k = p - self.T
+            out[:, :q] = hist[:, p - self.S, :q] if k >= self.S else 0.0
+            out[:, q:h2] = hist[:, p - 1, q:h2] if k % self.S else 0.0
+        return out
+
+    def _attn(self, li, ls, x):
+        attn = ls.fn.fn.fn
+        h = self._ln_shift(ls, self.hist[li][0], x)
+        qkv = F.linear(h, self._wt(attn.to_qkv.weight))
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            C().decode_rope_(qkv.contiguous(), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li], self.pos, self.H,
+                             self.Dh ** -0.5)
+            C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
+                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+            o = self.obuf
+        else:
+            o = self._attn_torch(li, attn, qkv)
+        return F.linear(o, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias))
+
+    def _attn_torch(self, li, attn, qkv):
+        from ..ops.reference import split_heads
+        from .rotary import apply_rotary
+        p = int(self.pos)
+        B, H, Dh = self.B, self.H, self.Dh
+        q, k, v = (t.view(B, H, 1, Dh) for t in qkv.chunk(3, dim=-1))
+        c, s = self.cos[p:p + 1], self.sin[p:p + 1]
+        q, k, v = (apply_rotary(t, c, s) for t in (q, k, v))
+        kc = self.kc[li].view(B, H, self.n, Dh)
+        vc = self.vc[li].view(B, H, self.n, Dh)
+        kc[:, :, p] = k[:, :, 0]
+        vc[:, :, p] = v[:, :, 0]
+        mask = static_mask(self.geom, attn.attn_type, self.n, device=q.device)[p, : p + 1]
+        sc = (q * Dh ** -0.5) @ kc[:, :, : p + 1].transpose(-1, -2)
+        sc = sc.masked_fill(~mask, float("-inf"))
+        o = torch.softmax(sc, -1) @ vc[:, :, : p + 1]
+        return o.reshape(B, H * Dh)
+
+    def _ff(self, li, ls, x):
+        ff = ls.fn.fn.fn
+        h = self._ln_shift(ls, self.hist[li][1], x)
+        a = F.linear(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias))
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            a = C().geglu_fwd(a.contiguous())
+        else:
+            a1, g = a.chunk(2, -1)
+            a = a1 * F.gelu(g)
+        return F.linear(a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias))
+
+    # -- one position through the whole network ------------------------------------------------------
+    def _forward_position(self) -> torch.Tensor:
+        W = self.model.to_logits[1].weight
+        x = F.embedding(self.tok, W.detach()).float()
+        if self.cfg.reversible:
+            x1, x2 = x, x
+            for li, (f, g) in enumerate(self.pairs):
+                x1 = x1 + self._attn(li, f, x2).float() * f.scale.detach().view(1, -1)
+                x2 = x2 + self._ff(li, g, x1).float() * g.scale.detach().view(1, -1)
+            out = (x1 + x2) * 0.5
+        else:
+            for li, (f, g) in enumerate(self.pairs):
+                x = x + self._attn(li, f, x).float() * f.scale.detach().view(1, -1)
+                x = x + self._ff(li, g, x).float() * g.scale.detach().view(1, -1)
+            out = x
+        norm, head = self.model.to_logits[0], self.model.to_logits[1]
+        h = F.layer_norm(out, (self.d,), norm.weight.detach(), norm.bias.detach())
+        return F.linear(h.to(self.cdt), self._wt(head.weight)[self.Vt:], self._wt(head.bias)[self.Vt:]).float()
+
+    def _image_step(self):
+        """Graph body: position pos (>= T-1) -> sample image token (pos - T + 1) -> feed it next."""
+        logits = self._forward_position()
+        logits = filter_logits(logits, self.top_k, self.top_p)
+        nxt = gumbel_sample(logits, self.temperature)
+        idx = (self.pos - (self.T - 1)).long().clamp(0, self.cfg.image_seq_len - 1).view(1, 1).expand(self.B, 1)
+        self.codes.scatter_(1, idx, nxt.view(self.B, 1))
+        self.tok.copy_(nxt + self.Vt)
+        self.pos.add_(1)
+        return logits
+
+    # -- public API ---------------------------------------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, text_bos: torch.Tensor):
+        """Feed BOS + text positions 0..T-2; position T-1 (last text token) is the first image step."""
+        self.reset()
+        for p in range(self.T - 1):
+            self.tok.copy_(text_bos[:, p])
+            self._forward_position()
+            self.pos.add_(1)
+        self.tok.copy_(text_bos[:, self.T - 1])
+
+    @torch.no_grad()
+    def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                 use_graph: Optional[bool] = None) -> torch.Tensor:
+        self.temperature, self.top_k, self.top_p = temperature, top_k, top_p
+        self.prefill(text_bos)
+        steps = self.cfg.image_seq_len
+        use_graph = self.use_hip if use_graph is None else use_graph
+        if not use_graph:
+            for _ in range(steps):
+                self._image_step()
+            return self.codes.clone()
+        self._capture()
+        # the first captured replay starts from the same state as an eager step
+        for _ in range(steps):
+            self.graph.replay()
+        return self.codes.clone()
+
+    def _capture(self):
+        """Capture one image step into a hipGraph (warm-up on a side stream as torch requires)."""
+        if self.graph is not None and self._graph_cfg == (self.temperature, self.top_k, self.top_p):
+            return
+        saved_pos = self.pos.clone()
+        saved_tok = self.tok.clone()
+        kv_state = [(k.clone(), v.clone()) for k, v in zip(self.kc, self.vc)]
+        hist_state = [[h.clone() for h in hs] for hs in self.hist]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._image_step()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_logits = self._image_step()
+        # restore the pre-capture state (warm-up + capture advanced it)
+        self.pos.copy_(saved_pos)
+        self.tok.copy_(saved_tok)
+        for (k, v), (k0, v0) in zip(zip(self.kc, self.vc), kv_state):
+            k.copy_(k0)
+            v.copy_(v0)
+        for hs, hs0 in zip(self.hist, hist_state):
+            for h, h0 in zip(hs, hs0):
+                h.copy_(h0)
+        self.graph = g
+        self._graph_cfg = (self.temperature, self.top_k, self.top_p)
+
+    @torch.no_grad()
+    def teacher_forced_logits(self, text_bos: torch.Tensor, image: torch.Tensor) -> torch.Tensor:
+        """Image-vocab logits at every position >= T-1 when feeding the given image codes (tests)."""
+        self.prefill(text_bos)
+        outs = []
+        for i in range(self.cfg.image_seq_len):
+            outs.append(self._forward_position())
+            if i + 1 < self.cfg.image_seq_len:
+                self.tok.copy_(image[:, i] + self.Vt)
+                self.pos.add_(1)
+        return torch.stack(outs, dim=1)

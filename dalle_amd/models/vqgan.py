@@ -1,0 +1,171 @@
+"""VQGAN (taming-transformers) decoder for image reconstruction from codes.
+
+``VQGanVAE(ckpt_path, config_path)``: ``decode(seq)`` = codebook embed (HIP gather kernel on MI355X,
+``one_hot(seq) @ codebook``) -> ``post_quant_conv`` -> conv decoder (ResNet blocks, GroupNorm,
+swish, nearest x2 upsampling, attention at the 32x32 resolution) -> ``(clamp(-1,1)+1)/2``.
+Parameter names follow taming's ``VQModel`` / ``GumbelVQ`` so a real checkpoint's state dict loads
+(``torch.load(weights_only=True)``); without a checkpoint the decoder is random-init (benchmarks).
+Default config = the LAION ``vqgan_gumbel_f8`` one: 8192 codes x 256 dims, ch 128, ch_mult
+(1,1,2,4), 2 res blocks, attention at 32.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def Normalize(c):
+    return nn.GroupNorm(num_groups=32, num_channels=c, eps=1e-6, affine=True)
+
+
+class ResnetBlock(nn.Module):
+    def __init__(self, in_channels, out_channels=None):
+        super().__init__()
+        out_channels = out_channels or in_channels
+        self.norm1 = Normalize(in_channels)
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, 1, 1)
+        self.norm2 = Normalize(out_channels)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, 1, 1)
+        self.nin_shortcut = nn.Conv2d(in_channels, out_channels, 1) if in_channels != out_channels else None
+
+    def forward(self, x):
+        h = self.conv1(F.silu(self.norm1(x)))
+        h = self.conv2(F.silu(self.norm2(h)))
+        if self.nin_shortcut is not None:
+            x = self.nin_shortcut(x)
+        return x + h
+
+
+class AttnBlock(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.norm = Normalize(c)
+        self.q, self.k, self.v = nn.Conv2d(c, c, 1), nn.Conv2d(c, c, 1), nn.Conv2d(c, c, 1)
+        self.proj_out = nn.Conv2d(c, c, 1)
+
+    def forward(self, x):
+        h = self.norm(x)
+        b, c, hh, ww = h.shape
+        q = self.q(h).reshape(b, c, hh * ww).transpose(1, 2)
+        k = self.k(h).reshape(b, c, hh * ww).transpose(1, 2)
+        v = self.v(h).reshape(b, c, hh * ww).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0]
+        return x + self.proj_out(o.transpose(1, 2).reshape(b, c, hh, ww))
+
+
+class Upsample(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, 1, 1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+class Decoder(nn.Module):
+    def __init__(self, *, ch=128, out_ch=3, ch_mult: Sequence[int] = (1, 1, 2, 4), num_res_blocks=2,
+                 attn_resolutions: Sequence[int] = (32,), resolution=256, z_channels=256, **ignore):
+        super().__init__()
+        self.num_resolutions = len(ch_mult)
+        self.num_res_blocks = num_res_blocks
+        block_in = ch * ch_mult[-1]
+        curr_res = resolution // 2 ** (self.num_resolutions - 1)
+        self.conv_in = nn.Conv2d(z_channels, block_in, 3, 1, 1)
+        self.mid = nn.Module()
+        self.mid.block_1 = ResnetBlock(block_in, block_in)
+        self.mid.attn_1 = AttnBlock(block_in)
+        self.mid.block_2 = ResnetBlock(block_in, block_in)
+        self.up = nn.ModuleList()
+        for i_level in reversed(range(self.num_resolutions)):
+            block, attn = nn.ModuleList(), nn.ModuleList()
+            block_out = ch * ch_mult[i_level]
+            for _ in range(num_res_blocks + 1):
+                block.append(ResnetBlock(block_in, block_out))
+                block_in = block_out
+                if curr_res in attn_resolutions:
+                    attn.append(AttnBlock(block_in))
+            up = nn.Module()
+            up.block, up.attn = block, attn
+            if i_level != 0:
+                up.upsample = Upsample(block_in)
+                curr_res *= 2
+            self.up.insert(0, up)
+        self.norm_out = Normalize(block_in)
+        self.conv_out = nn.Conv2d(block_in, out_ch, 3, 1, 1)
+
+    def forward(self, z):
+        h = self.conv_in(z)
+        h = self.mid.block_2(self.mid.attn_1(self.mid.block_1(h)))
+        for i_level in reversed(range(self.num_resolutions)):
+            up = self.up[i_level]
+            for i_block in range(self.num_res_blocks + 1):
+                h = up.block[i_block](h)
+                if len(up.attn) > 0:
+                    h = up.attn[i_block](h)
+            if i_level != 0:
+                h = up.upsample(h)
+        return self.conv_out(F.silu(self.norm_out(h)))
+
+
+class GumbelQuantize(nn.Module):
+    def __init__(self, n_embed: int, embedding_dim: int):
+        super().__init__()
+        self.embed = nn.Embedding(n_embed, embedding_dim)
+
+
+class VQGanVAE(nn.Module):
+    def __init__(self, vqgan_model_path: Optional[str] = None, vqgan_config_path: Optional[str] = None, *,
+                 n_embed: int = 8192, embed_dim: int = 256, ddconfig: Optional[dict] = None, is_gumbel: bool = True):
+        super().__init__()
+        if vqgan_config_path is not None:
+            import yaml
+
+            with open(vqgan_config_path) as f:
+                conf = yaml.load(f, Loader=yaml.SafeLoader)
+            params = conf["model"]["params"]
+            ddconfig = params["ddconfig"]
+            n_embed, embed_dim = params["n_embed"], params["embed_dim"]
+            is_gumbel = "Gumbel" in conf["model"].get("target", "GumbelVQ")
+        ddconfig = ddconfig or dict(ch=128, out_ch=3, ch_mult=(1, 1, 2, 4), num_res_blocks=2, attn_resolutions=(32,),
+                                    resolution=256, z_channels=256)
+        self.decoder = Decoder(**ddconfig)
+        self.post_quant_conv = nn.Conv2d(embed_dim, ddconfig["z_channels"], 1)
+        self.quantize = GumbelQuantize(n_embed, embed_dim)
+        self.is_gumbel = is_gumbel
+        self.num_tokens = n_embed
+        self.num_layers = len(ddconfig["ch_mult"]) - 1
+        self.image_size = ddconfig["resolution"]
+        if vqgan_model_path is not None:
+            sd = torch.load(vqgan_model_path, map_location="cpu", weights_only=True)
+            sd = sd.get("state_dict", sd)
+            missing, unexpected = self.load_state_dict({k: v for k, v in sd.items()
+                                                        if k.startswith(("decoder.", "post_quant_conv.", "quantize."))}, strict=False)
+            if missing:
+                raise RuntimeError(f"VQGAN checkpoint is missing decoder weights: {missing[:5]}")
+
+    @property
+    def codebook(self) -> torch.Tensor:
+        return self.quantize.embed.weight
+
+    def embed_codes(self, seq: torch.Tensor) -> torch.Tensor:
+        b, n = seq.shape
+        side = int(round(n ** 0.5))
+        cb = self.codebook
+        if seq.is_cuda and cb.dtype == torch.float32:
+            from ..ops.ext import load_extension
+
+            return load_extension(required=True).vq_embed(seq.contiguous().long(), cb.detach().contiguous(), side)
+        z = F.one_hot(seq, num_classes=self.num_tokens).to(cb.dtype) @ cb
+        return z.view(b, side, side, -1).permute(0, 3, 1, 2).contiguous()
+
+    @torch.no_grad()
+    def decode(self, img_seq: torch.Tensor) -> torch.Tensor:
+        z = self.embed_codes(img_seq)
+        img = self.decoder(self.post_quant_conv(z))
+        return (img.clamp(-1.0, 1.0) + 1) * 0.5
+
+    def get_codebook_indices(self, images):  # pragma: no cover - training uses precomputed codes
+        raise NotImplementedError("the encoder is not needed: LAION codes are precomputed (data.py)")

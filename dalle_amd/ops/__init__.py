@@ -68,6 +68,38 @@ def feed_forward(h, w1, b1, w2, b2):
     return reference.feed_forward(h, w1, b1, w2, b2)
 
 
+def attention_out(h, w_qkv, heads: int, geom, attn_type: str):
+    """QKV projection + rotary + sparse attention, before the output projection."""
+    be = backend_for(h)
+    if be == "hip":
+        return _hip().attention_out(h, w_qkv, heads, geom, attn_type)
+    from ..models.rotary import rotary_tables
+    cos, sin = rotary_tables(geom.text_len, geom.image_size, w_qkv.shape[0] // 3 // heads, device=h.device)
+    dt = COMPUTE_DTYPE if be == "torch_gpu" else h.dtype
+    qkv = torch.nn.functional.linear(h.to(dt), w_qkv.to(dt))
+    q, k, v = reference.qkv_rotary(qkv, heads, cos, sin)
+    return reference.sparse_attention_core(q, k, v, geom, attn_type)
+
+
+def ff_hidden(h, w1, b1):
+    """FF-in projection + GEGLU (the FF block before its output projection)."""
+    be = backend_for(h)
+    if be == "hip":
+        return _hip().ff_hidden(h, w1, b1)
+    dt = COMPUTE_DTYPE if be == "torch_gpu" else h.dtype
+    return reference.geglu(torch.nn.functional.linear(h.to(dt), w1.to(dt), b1.to(dt)))
+
+
+def proj_residual(x, o, w, b, scale):
+    """x + scale * (o W^T + b): output projection with the LayerScale residual epilogue."""
+    be = backend_for(x)
+    if be == "hip":
+        return _hip().proj_residual(x, o, w, b, scale)
+    dt = o.dtype
+    y = torch.nn.functional.linear(o, w.to(dt), b.to(dt))
+    return x + (y * scale.to(dt)).to(x.dtype)
+
+
 def begin_forward():
     """Start of a model forward: drops the per-forward bf16 weight casts of the HIP path."""
     if hip_available():

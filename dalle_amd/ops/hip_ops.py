@@ -64,8 +64,27 @@ def _rope_tables(geom: AttnGeometry, dim_head: int, device):
 
 
 # ---------------------------------------------------------------------------------------------
-# Linear: bf16 GEMM forward, fp32 weight grads
+# Linear: bf16 GEMM forward, fp32 weight grads accumulated straight into the fp32 grad buffer
 # ---------------------------------------------------------------------------------------------
+FUSE_WGRAD = True
+
+
+def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
+    """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate IN the
+    GEMM (hipBLASLt beta = 1, bf16 in / fp32 out) and return None: no temporary dW, no separate add
+    kernel, and the shared blocks' grads (one per reusing layer) sum in fp32 inside the GEMM."""
+    gw = w.grad
+    if FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape:
+        torch.addmm(gw, g2.t(), x2, out_dtype=torch.float32, out=gw)
+        return None
+    return torch.mm(g2.t(), x2, out_dtype=torch.float32)
+
+
+def _bf16c(t):
+    t = t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+    return t.contiguous()
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -76,6 +95,7 @@ class _Linear(torch.autograd.Function):
         else:
             y = torch.mm(x2, wb.t())
         ctx.save_for_backward(x2, wb)
+        ctx.w = w
         ctx.has_bias = b is not None
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -83,14 +103,70 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x2, wb = ctx.saved_tensors
-        g2 = gy.reshape(-1, gy.shape[-1])
-        if g2.dtype != torch.bfloat16:
-            g2 = g2.to(torch.bfloat16)
-        g2 = g2.contiguous()
+        g2 = _bf16c(gy.reshape(-1, gy.shape[-1]))
         dx = torch.mm(g2, wb).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = torch.mm(g2.t(), x2, out_dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        dw = weight_grad(ctx.w, g2, x2) if ctx.needs_input_grad[1] else None
         db = torch.sum(g2, 0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db
+
+
+class _FF1GEGLU(torch.autograd.Function):
+    """FF-in GEMM (+bias) -> GEGLU; backward = fused GEGLU-bwd + bias-grad kernel, then two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, h, w, b):
+        wb = bf16_weight(w)
+        h2 = _bf16c(h.reshape(-1, h.shape[-1]))
+        a = torch.addmm(bf16_weight(b), h2, wb.t())
+        out = C().geglu_fwd(a)
+        ctx.save_for_backward(h2, a, wb)
+        ctx.w = w
+        ctx.hshape = h.shape
+        return out.view(*h.shape[:-1], out.shape[-1])
+
+    @staticmethod
+    def backward(ctx, gout):
+        h2, a, wb = ctx.saved_tensors
+        g = _bf16c(gout.reshape(a.shape[0], -1))
+        da, db = C().geglu_bwd_bias(a, g)
+        dh = torch.mm(da, wb).view(ctx.hshape)
+        dw = weight_grad(ctx.w, da, h2)
+        return dh, dw, db
+
+
+class _ProjResidual(torch.autograd.Function):
+    """out = x + scale * (o W^T + b): output GEMM with the LayerScale + residual epilogue (K8/K10).
+    Backward: one kernel produces dy = bf16(scale*g), dscale = colsum(g*y) and colsum(g) (-> dbias)."""
+
+    @staticmethod
+    def forward(ctx, x, o, w, b, scale):
+        wb = bf16_weight(w)
+        o2 = _bf16c(o.reshape(-1, o.shape[-1]))
+        y = torch.addmm(bf16_weight(b), o2, wb.t())
+        s = scale.reshape(-1).contiguous()
+        out = torch.empty_like(x)
+        C().scale_residual_out(x.contiguous(), y, s, out)
+        ctx.save_for_backward(o2, y, wb, s)
+        ctx.w = w
+        ctx.oshape, ctx.sshape = o.shape, scale.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        o2, y, wb, s = ctx.saved_tensors
+        dy, dscale, gsum = C().scale_residual_bwd(g.contiguous(), y, s)
+        do = torch.mm(dy, wb).view(ctx.oshape)
+        dw = weight_grad(ctx.w, dy, o2)
+        db = gsum * s
+        return g, do, dw, db, dscale.view(ctx.sshape)
+
+
+def ff_hidden(h, w1, b1):
+    return _FF1GEGLU.apply(h, w1, b1)
+
+
+def proj_residual(x, o, w, b, scale):
+    return _ProjResidual.apply(x, o, w, b, scale)
 
 
 def linear(x, w, b=None):
@@ -158,10 +234,13 @@ def attention_core(qkv, heads: int, geom: AttnGeometry, attn_type: str):
     return _AttnCore.apply(qkv, cos, sin, geom.text_len, geom.image_size, geom.kernel_size, heads, PATTERN_IDS[attn_type])
 
 
+def attention_out(h, w_qkv, heads: int, geom: AttnGeometry, attn_type: str):
+    """QKV GEMM -> rotary -> sparse attention; returns the pre-projection output (B, n, H*64)."""
+    return attention_core(linear(h, w_qkv), heads, geom, attn_type)
+
+
 def attention_block(h, w_qkv, w_out, b_out, heads: int, geom: AttnGeometry, attn_type: str):
-    qkv = linear(h, w_qkv)
-    o = attention_core(qkv, heads, geom, attn_type)
-    return linear(o, w_out, b_out)
+    return linear(attention_out(h, w_qkv, heads, geom, attn_type), w_out, b_out)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -181,7 +260,7 @@ class _GEGLU(torch.autograd.Function):
 
 
 def feed_forward(h, w1, b1, w2, b2):
-    return linear(_GEGLU.apply(linear(h, w1, b1)), w2, b2)
+    return linear(_FF1GEGLU.apply(h, w1, b1), w2, b2)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -201,7 +280,7 @@ class _ScaleResidual(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         y, s = ctx.saved_tensors
-        dy, ds = C().scale_residual_bwd(g.contiguous(), y, s)
+        dy, ds, _ = C().scale_residual_bwd(g.contiguous(), y, s)
         return g, dy, ds.view(ctx.sshape)
 
 

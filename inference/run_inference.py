@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Text -> image generation (reference ``inference/run_inference.py:1-146``), CLI-compatible.
+
+For every query: 16 x 8 = 128 images (temperature / top-k / top-p sampling with the KV-cache decoder,
+one hipGraph-captured step replayed per image token on MI355X), decoded by the VQGAN, optionally
+re-ranked with CLIP (only when the ``clip`` package and weights are available locally), and saved
+as ``{output_dir}/{query}.pickle`` with keys ``query, temperature, images, clip_scores``.
+
+Checkpoints in the training layout are accepted (the reference's CachedAs rename
+``net.fn.fn -> net.fn.fn.fn`` / ``to_qkv -> fn.to_qkv`` / ``to_out -> fn.to_out`` is undone when present).
+"""
+import argparse
+import os
+import pickle
+import sys
+from collections import OrderedDict
+from datetime import datetime
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dalle_amd.config import get_config  # noqa: E402
+from dalle_amd.data.tokenizer import load_tokenizer  # noqa: E402
+from dalle_amd.models.dalle import DALLE  # noqa: E402
+from dalle_amd.models.vqgan import VQGanVAE  # noqa: E402
+
+torch.set_grad_enabled(False)
+
+
+class ModelWrapper(torch.nn.Module):
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, input_ids, attention_mask, image):
+        return {'loss': self.model.forward(text=input_ids, image=image, mask=attention_mask, return_loss=True)}
+
+
+def make_model(preset: str = "reference", tokenizer_path: str = "t5-small"):
+    cfg = get_config(preset)
+    tokenizer = load_tokenizer(tokenizer_path, vocab_size=cfg.num_text_tokens)
+    tokenizer.pad_token = tokenizer.eos_token
+    return tokenizer, ModelWrapper(DALLE(cfg))
+
+
+def normalize_state_dict_keys(state_dict):
+    """Map inference-layout (CachedAs) keys back onto the training layout."""
+    out = OrderedDict()
+    for k, v in state_dict.items():
+        k = k.replace("net.fn.fn.fn.fn.to_qkv", "net.fn.fn.fn.to_qkv").replace("net.fn.fn.fn.fn.to_out", "net.fn.fn.fn.to_out")
+        k = k.replace("fn.fn.fn.fn.net.", "fn.fn.fn.net.")
+        out[k] = v
+    return out
+
+
+def generate(query, *, tokenizer, model, batch_size, n_iters, temperature, top_k, top_p, text_seq_len=256, device="cuda"):
+    ids = tokenizer(query, add_special_tokens=False, max_length=text_seq_len, truncation=True)['input_ids']
+    input_ids = torch.full((text_seq_len,), 1, dtype=torch.long)
+    input_ids[: len(ids)] = torch.tensor(ids, dtype=torch.long)
+    input_ids = input_ids.repeat(batch_size, 1).to(device)
+    result = []
+    for _ in range(n_iters):
+        output = model.model.generate_images(input_ids, temperature=temperature, top_k=top_k, top_p=top_p, use_cache=True)
+        output = output.permute(0, 2, 3, 1).float().cpu().numpy()
+        result.extend(output)
+    return result
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser()
+    parser.add_argument('--queries', type=str, help='List of queries (*.txt, newline-separated)')
+    parser.add_argument('--temperature', type=float, help='Sampling temperature', default=1.0)
+    parser.add_argument('--top-k', type=int, default=0)
+    parser.add_argument('--top-p', type=float, default=1.0)
+    parser.add_argument('--model', type=str, help='DALL-E checkpoint (*.pt)', default=None)
+    parser.add_argument('--vqgan', type=str, help='VQGAN checkpoint (*.ckpt)', default=None)
+    parser.add_argument('--vqgan-config', type=str, help='VQGAN config (*.yaml)', default=None)
+    parser.add_argument('--output-dir', type=str, help='Output directory')
+    parser.add_argument('--model-preset', type=str, default='reference', help='[new] dalle_amd.config preset')
+    parser.add_argument('--batch-size', type=int, default=16, help='[new] images per generate call (reference: 16)')
+    parser.add_argument('--n-iters', type=int, default=8, help='[new] generate calls per query (reference: 8)')
+    args = parser.parse_args(argv)
+
+    with open(args.queries) as f:
+        queries = [line.rstrip() for line in f]
+        queries = [item for item in queries if len(item) > 0]
+    print(f'[*] Loaded {len(queries)} queries')
+
+    device = "cuda" if torch.cuda.is_available() else "cpu"
+    tokenizer, model = make_model(args.model_preset)
+    if args.model is not None:
+        print(f'[*] Model modification time: {datetime.fromtimestamp(os.stat(args.model).st_mtime)}')
+        state_dict = normalize_state_dict_keys(torch.load(args.model, map_location="cpu", weights_only=True))
+        ok = model.load_state_dict(state_dict, strict=False)
+        print(f'[*] Loaded model: {ok}')
+    else:
+        print('[*] No --model given: random-init weights')
+
+    gan = VQGanVAE(args.vqgan, args.vqgan_config)
+    model.model.vae = gan.eval()
+    model = model.to(device).eval()
+
+    clip_model = None
+    try:
+        import clip  # noqa: F401
+
+        clip_model, clip_preprocess = clip.load("ViT-B/32", device=device)
+    except Exception:  # noqa: BLE001 - CLIP weights are not available offline
+        print('[*] CLIP unavailable: clip_scores will be uniform')
+
+    os.makedirs(args.output_dir, exist_ok=True)
+    print(f'[*] Saving results to `{args.output_dir}`')
+    for query in queries:
+        images = generate(query, tokenizer=tokenizer, model=model, batch_size=args.batch_size, n_iters=args.n_iters,
+                          temperature=args.temperature, top_k=args.top_k, top_p=args.top_p,
+                          text_seq_len=model.model.text_seq_len, device=device)
+        if clip_model is not None:
+            from PIL import Image
+
+            images_for_clip = torch.cat([clip_preprocess(Image.fromarray((img * 255).astype(np.uint8))).unsqueeze(0).to(device)
+                                         for img in images])
+            text = clip.tokenize([query]).to(device)
+            _, logits_per_text = clip_model(images_for_clip, text)
+            clip_scores = logits_per_text[0].softmax(dim=-1).cpu().numpy()
+        else:
+            clip_scores = np.full(len(images), 1.0 / len(images), dtype=np.float32)
+        with open(os.path.join(args.output_dir, f'{query}.pickle'), 'wb') as f:
+            outputs = {'query': query, 'temperature': args.temperature, 'images': images, 'clip_scores': clip_scores}
+            pickle.dump(outputs, f)
+
+
+if __name__ == '__main__':
+    main()

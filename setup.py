@@ -20,6 +20,7 @@ hip_sources = [
     "csrc/kernels/layernorm_shift.hip",
     "csrc/kernels/elementwise.hip",
     "csrc/kernels/xent.hip",
+    "csrc/kernels/decode.hip",
     "csrc/optim/lamb.hip",
 ]
 
