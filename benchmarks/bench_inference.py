@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-vae", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0, help="prefill + N eager decode steps, then exit (rocprof)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -49,22 +50,30 @@ def main():
         eng._image_step()
     torch.cuda.synchronize()
     print(f"# eager decode step: {(time.perf_counter() - t) / 8 * 1e3:.2f} ms", file=sys.stderr, flush=True)
+    if args.profile_steps:
+        for _ in range(args.profile_steps):
+            eng._image_step()
+        torch.cuda.synchronize()
+        return
     if use_graph:
         t = time.perf_counter()
         eng._capture()
         torch.cuda.synchronize()
         print(f"# graph capture: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     # warm-up generate
+    t = time.perf_counter()
     model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
     torch.cuda.synchronize()
-    print("# warm-up generate done", file=sys.stderr, flush=True)
+    print(f"# warm-up generate done: {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    for _ in range(args.iters):
+    for i in range(args.iters):
         out = model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        print(f"# generate {i}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
     el = (time.perf_counter() - t0) / args.iters
     eng = model._decode_engine
-    # decode-only timing (graph replays)
+    # decode-only timing (graph replays) from a fresh start: positions 0..63 -- never past seq_len
+    eng._start(model.prepare_text(text))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if use_graph:
@@ -72,7 +81,7 @@ def main():
             eng.graph.replay()
     else:
         for _ in range(64):
-            eng._image_step()
+            eng._step()
     torch.cuda.synchronize()
     per_tok = (time.perf_counter() - t1) / 64
     print(json.dumps({"metric": "text->image generation throughput (batch 64, top-k, hipGraph decode)",

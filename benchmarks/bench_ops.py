@@ -34,8 +34,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--only", default="")
+    ap.add_argument("--tunable", action="store_true", help="enable PyTorch TunableOp GEMM search")
     args = ap.parse_args()
     dev = torch.device("cuda")
+    if args.tunable:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(os.path.join("gpurun_out", "tunableop_results.csv"))
     B, H, T, S = args.batch, 16, 257, 32
     n = T + S * S - 1
     geom = AttnGeometry(T, S, 5)
@@ -65,11 +70,24 @@ def main():
             t_dw32 = timeit(lambda: torch.mm(g.t(), x, out_dtype=torch.float32))
             t_dwacc = timeit(lambda: torch.addmm(acc, g.t(), x, out_dtype=torch.float32, out=acc))
             t_dw16 = timeit(lambda: torch.mm(g.t(), x))
-            res.append({"op": f"gemm_M{M}_N{N}_K{K}", "fwd_TF": round(fl / t_fwd / 1e9), "dx_TF": round(fl / t_dx / 1e9),
-                        "dw_fp32out_TF": round(fl / t_dw32 / 1e9), "dw_accum_TF": round(fl / t_dwacc / 1e9),
-                        "dw_bf16out_TF": round(fl / t_dw16 / 1e9)})
+            t_dwT = timeit(lambda: torch.mm(x.t(), g, out_dtype=torch.float32))
+            r = {"op": f"gemm_M{M}_N{N}_K{K}", "fwd_TF": round(fl / t_fwd / 1e9), "dx_TF": round(fl / t_dx / 1e9),
+                 "dw_fp32out_TF": round(fl / t_dw32 / 1e9), "dw_accum_TF": round(fl / t_dwacc / 1e9),
+                 "dw_bf16out_TF": round(fl / t_dw16 / 1e9), "dwT_fp32out_TF": round(fl / t_dwT / 1e9)}
+            for s in (4, 8, 16):
+                gs, xs = g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K)
+                try:
+                    t_sk = timeit(lambda: torch.bmm(gs, xs, out_dtype=torch.float32).sum(0, out=acc))
+                    r[f"dw_splitk{s}_bmm32_TF"] = round(fl / t_sk / 1e9)
+                except Exception as e:  # out_dtype for bmm may be unsupported on this build
+                    r[f"dw_splitk{s}_bmm32_TF"] = str(e)[:60]
+                t_sk16 = timeit(lambda: torch.bmm(gs, xs).float().sum(0, out=acc))
+                r[f"dw_splitk{s}_bmm16_TF"] = round(fl / t_sk16 / 1e9)
+            res.append(r)
+            print(json.dumps(r), flush=True)
     for r in res:
-        print(json.dumps(r), flush=True)
+        if not r["op"].startswith("gemm"):
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

@@ -42,6 +42,18 @@ __device__ __forceinline__ bool allowed_st(const AttnGeom& g, int qs, int ks) {
   return (kr > qr - g.K) && (kc <= qc) && (kc > qc - g.K);
 }
 
+// wave-uniform: every (query, key) pair of the 32x32 tile (query tile qt, key tile kt) is allowed, so
+// the per-element predicate can be skipped (all text tiles but the padded boundary one for image
+// queries, tiles strictly below the diagonal for text queries / the dense pattern)
+__device__ __forceinline__ bool tile_full(const AttnGeom& g, int qt, int kt) {
+  const int ntext = g.Tp >> 5;
+  if (kt < ntext) {
+    if (kt * 32 + 31 >= g.T) return false;
+    return qt >= ntext || kt < qt;
+  }
+  return g.pattern == 0 && qt >= ntext && kt < qt;
+}
+
 // first local (image) key tile needed by image query block qb
 __device__ __forceinline__ int local_lo_tile(const AttnGeom& g, int qb) {
   const int kq0 = qb * 32 - g.Tp;
@@ -165,10 +177,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
 #pragma unroll
       for (int ss = 0; ss < 4; ++ss) s = MFMA32(ld16(Ks + c32 * RS + 16 * ss + 8 * hl), qf[ss], s);
       float mt = NEG_BIG;
+      const bool full = tile_full(g, qb, tile);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ks = tile * 32 + acc_row(r, hl);
-        const float x = allowed_st(g, qs, ks) ? s[r] * LOG2E : NEG_BIG;
+        const float x = (full || allowed_st(g, qs, ks)) ? s[r] * LOG2E : NEG_BIG;
         s[r] = x;
         mt = fmaxf(mt, x);
       }
@@ -322,10 +335,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
         s = MFMA32(ld16(Ks + c32 * RS + 16 * ss + 8 * hl), qf[ss], s);
         dp = MFMA32(ld16(Vs + c32 * RS + 16 * ss + 8 * hl), dof[ss], dp);
       }
+      const bool full = tile_full(g, qb, tile);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ks = tile * 32 + acc_row(r, hl);
-        const float p = allowed_st(g, qs, ks) ? exp2f(s[r] * LOG2E - lq) : 0.f;
+        const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - lq) : 0.f;
         s[r] = p * (dp[r] - dl);
       }
       const bf16x8 d0 = cvt8(s, 0), d1 = cvt8(s, 8);
@@ -430,11 +444,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
         dp = MFMA32(ld16(Ds + c32 * RS + 16 * ss + 8 * hl), vf[ss], dp);
       }
       f32x16 ds;
+      const bool full = tile_full(g, qt, kb);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = acc_row(r, hl);
         const int qs = qt * 32 + ql;
-        const float p = allowed_st(g, qs, ks) ? exp2f(s[r] * LOG2E - stats[buf][0][ql]) : 0.f;
+        const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - stats[buf][0][ql]) : 0.f;
         s[r] = p;
         ds[r] = p * (dp[r] - stats[buf][1][ql]);
       }
@@ -554,11 +569,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
       dp = MFMA32(ld16(Ds + c32 * RS + 16 * ss + 8 * hl), vf[ss], dp);
     }
     f32x16 ds;
+    const bool full = tile_full(g, qt, kb);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ql = acc_row(r, hl);
       const int qs = qt * 32 + ql;
-      const float p = allowed_st(g, qs, ks) ? exp2f(s[r] * LOG2E - stats[wave][buf][0][ql]) : 0.f;
+      const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - stats[wave][buf][0][ql]) : 0.f;
       s[r] = p;
       ds[r] = p * (dp[r] - stats[wave][buf][1][ql]);
     }

@@ -16,6 +16,7 @@ __global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __rest
   constexpr int PER = D / 256;
   const int b = blockIdx.x, lane = threadIdx.x;
   const int pos = *pos_ptr;
+  if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   const float* xr = x + (size_t)b * D;
   f32x4 v[PER];
   float s = 0.f;
@@ -68,6 +69,7 @@ __global__ void decode_rope_kernel(const __bf16* __restrict__ qkv, const float* 
   const int chunk = gid & 7, bh = gid >> 3;
   const int b = bh / g.H, h = bh - b * g.H;
   const int pos = *pos_ptr;
+  if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   const int HD = g.H * 64;
   const size_t src = (size_t)b * 3 * HD + h * 64 + chunk * 8;
   float c[8], sn[8];
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
   __shared__ float part[4][64];
   const int bh = blockIdx.x, tid = threadIdx.x;
   const int pos = *pos_ptr;
+  if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   if (tid < 64) qs[tid] = bf2f(reinterpret_cast<const bf16_raw*>(q)[(size_t)bh * 64 + tid]);
   __syncthreads();
   int nloc, r0 = 0, c0 = 0, nr = 0, nc = 1;

@@ -76,15 +76,18 @@ class DecodeEngine:
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
     def _wt(self, p):
-        w = self._w.get(id(p))
-        if w is None:
-            w = p.detach().to(self.cdt)
-            self._w[id(p)] = w
-        return w
+        ent = self._w.get(id(p))
+        if ent is None:
+            ent = (p, p.detach().to(self.cdt))
+            self._w[id(p)] = ent
+        return ent[1]
 
     def reset(self):
+        """Zero position/caches and refresh the compute-dtype weight copies IN PLACE (a captured graph
+        keeps pointing at the same buffers, so weight updates between calls are still seen)."""
         self.pos.zero_()
-        self._w.clear()
+        for p, w in self._w.values():
+            w.copy_(p.detach())
         for k in self.kc + self.vc:
             k.zero_()
 
@@ -156,41 +159,62 @@ class DecodeEngine:
             a = a1 * F.gelu(g)
         return F.linear(a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias))
 
+    def _residual(self, x, y, ls):
+        """x += LayerScale * y (fp32 residual stream), one fused kernel on the HIP path."""
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            C().scale_residual_(x, y.contiguous(), ls.scale.detach().reshape(-1).contiguous())
+            return x
+        return x + y.float() * ls.scale.detach().view(1, -1)
+
     # -- one position through the whole network ------------------------------------------------------
     def _forward_position(self) -> torch.Tensor:
         W = self.model.to_logits[1].weight
         x = F.embedding(self.tok, W.detach()).float()
         if self.cfg.reversible:
-            x1, x2 = x, x
+            x1, x2 = x, x.clone()
             for li, (f, g) in enumerate(self.pairs):
-                x1 = x1 + self._attn(li, f, x2).float() * f.scale.detach().view(1, -1)
-                x2 = x2 + self._ff(li, g, x1).float() * g.scale.detach().view(1, -1)
+                x1 = self._residual(x1, self._attn(li, f, x2), f)
+                x2 = self._residual(x2, self._ff(li, g, x1), g)
             out = (x1 + x2) * 0.5
         else:
             for li, (f, g) in enumerate(self.pairs):
-                x = x + self._attn(li, f, x).float() * f.scale.detach().view(1, -1)
-                x = x + self._ff(li, g, x).float() * g.scale.detach().view(1, -1)
+                x = self._residual(x, self._attn(li, f, x), f)
+                x = self._residual(x, self._ff(li, g, x), g)
             out = x
         norm, head = self.model.to_logits[0], self.model.to_logits[1]
         h = F.layer_norm(out, (self.d,), norm.weight.detach(), norm.bias.detach())
         return F.linear(h.to(self.cdt), self._wt(head.weight)[self.Vt:], self._wt(head.bias)[self.Vt:]).float()
 
-    def _image_step(self):
-        """Graph body: position pos (>= T-1) -> sample image token (pos - T + 1) -> feed it next."""
+    def _step(self):
+        """Graph body for ANY position: run position ``pos``; choose the next input token on device --
+        the next caption token while ``pos + 1 < T`` (prefill), else the sampled image token -- and
+        record the sample as image code ``pos - T + 1`` (prefill writes are overwritten later)."""
         logits = self._forward_position()
         logits = filter_logits(logits, self.top_k, self.top_p)
         nxt = gumbel_sample(logits, self.temperature)
-        idx = (self.pos - (self.T - 1)).long().clamp(0, self.cfg.image_seq_len - 1).view(1, 1).expand(self.B, 1)
+        p = self.pos.long()
+        idx = (p - (self.T - 1)).clamp(0, self.cfg.image_seq_len - 1).view(1, 1).expand(self.B, 1)
         self.codes.scatter_(1, idx, nxt.view(self.B, 1))
-        self.tok.copy_(nxt + self.Vt)
+        nxt_text = self.text_bos.gather(1, (p + 1).clamp(max=self.T - 1).view(1, 1).expand(self.B, 1)).view(self.B)
+        self.tok.copy_(torch.where(p + 1 < self.T, nxt_text, nxt + self.Vt))
         self.pos.add_(1)
         return logits
 
+    _image_step = _step
+
     # -- public API ---------------------------------------------------------------------------------
+    def _start(self, text_bos: torch.Tensor):
+        self.reset()
+        if not hasattr(self, "text_bos") or self.text_bos.shape != text_bos.shape:
+            self.text_bos = torch.zeros_like(text_bos)
+        self.text_bos.copy_(text_bos)
+        self.tok.copy_(text_bos[:, 0])
+
     @torch.no_grad()
     def prefill(self, text_bos: torch.Tensor):
-        """Feed BOS + text positions 0..T-2; position T-1 (last text token) is the first image step."""
-        self.reset()
+        """Eagerly feed BOS + text positions 0..T-2 (position T-1 is the first sampling step)."""
+        self._start(text_bos)
         for p in range(self.T - 1):
             self.tok.copy_(text_bos[:, p])
             self._forward_position()
@@ -200,46 +224,36 @@ class DecodeEngine:
     @torch.no_grad()
     def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
                  use_graph: Optional[bool] = None) -> torch.Tensor:
+        """All ``seq_len`` positions (caption prefill + 1024 sampled image tokens) through one step
+        function; on MI355X that step is a single hipGraph replayed ``seq_len`` times."""
         self.temperature, self.top_k, self.top_p = temperature, top_k, top_p
-        self.prefill(text_bos)
-        steps = self.cfg.image_seq_len
         use_graph = self.use_hip if use_graph is None else use_graph
-        if not use_graph:
-            for _ in range(steps):
-                self._image_step()
-            return self.codes.clone()
-        self._capture()
-        # the first captured replay starts from the same state as an eager step
-        for _ in range(steps):
-            self.graph.replay()
+        self._start(text_bos)
+        if use_graph:
+            self._capture()
+            self._start(text_bos)
+            for _ in range(self.n):
+                self.graph.replay()
+        else:
+            for _ in range(self.n):
+                self._step()
         return self.codes.clone()
 
     def _capture(self):
         """Capture one image step into a hipGraph (warm-up on a side stream as torch requires)."""
         if self.graph is not None and self._graph_cfg == (self.temperature, self.top_k, self.top_p):
             return
-        saved_pos = self.pos.clone()
-        saved_tok = self.tok.clone()
-        kv_state = [(k.clone(), v.clone()) for k, v in zip(self.kc, self.vc)]
-        hist_state = [[h.clone() for h in hs] for hs in self.hist]
+        # warm-up on a side stream (allocator / library handles), then capture; the caller resets the
+        # state (pos, tokens, caches) afterwards, so the warm-up steps leave no trace
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._image_step()
+                self._step()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._static_logits = self._image_step()
-        # restore the pre-capture state (warm-up + capture advanced it)
-        self.pos.copy_(saved_pos)
-        self.tok.copy_(saved_tok)
-        for (k, v), (k0, v0) in zip(zip(self.kc, self.vc), kv_state):
-            k.copy_(k0)
-            v.copy_(v0)
-        for hs, hs0 in zip(self.hist, hist_state):
-            for h, h0 in zip(hs, hs0):
-                h.copy_(h0)
+            self._static_logits = self._step()
         self.graph = g
         self._graph_cfg = (self.temperature, self.top_k, self.top_p)
 

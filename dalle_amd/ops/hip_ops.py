@@ -155,6 +155,7 @@ class _ProjResidual(torch.autograd.Function):
     def backward(ctx, g):
         o2, y, wb, s = ctx.saved_tensors
         dy, dscale, gsum = C().scale_residual_bwd(g.contiguous(), y, s)
+        dy = dy.view(-1, dy.shape[-1])
         do = torch.mm(dy, wb).view(ctx.oshape)
         dw = weight_grad(ctx.w, dy, o2)
         db = gsum * s

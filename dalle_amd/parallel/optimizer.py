@@ -32,6 +32,7 @@ from .compression import CompressionBase, NoCompression
 from .powersgd import PowerSGD
 from .progress import ProgressTracker
 from ..optim.flat import FlatArena
+from ..utils import faults
 from ..utils.logging import get_logger
 
 logger = get_logger(__name__)
@@ -84,7 +85,7 @@ class GradientAverager:
 
     # -- averaging --------------------------------------------------------------------------------
     @torch.no_grad()
-    def step(self, total_samples: Optional[int] = None) -> bool:
+    def step(self, total_samples: Optional[int] = None, epoch: int = 0) -> bool:
         """Replace the accumulated grads with the collaboration-wide weighted mean (in the params'
         ``.grad``). Returns False if averaging failed and the local mean was used instead."""
         t = max(1, self.local_times_accumulated)
@@ -93,6 +94,7 @@ class GradientAverager:
         grads = self._grads()
         ok = True
         try:
+            faults.before_averaging(epoch)
             if world == 1:
                 for g in grads:
                     g.div_(t)
@@ -317,6 +319,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 loss = closure()
         if self.auxiliary:
             return loss
+        self._local_steps = getattr(self, "_local_steps", 0) + 1
+        faults.on_local_step(self._local_steps, self._params)
         bs = batch_size if batch_size is not None else self.batch_size_per_step
         if bs is None:
             raise ValueError("batch_size_per_step (ctor) or batch_size (step) is required")
@@ -334,8 +338,9 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
     def _update_global_epoch(self):
         t0 = time.perf_counter()
         total = self.tracker.global_progress.samples_accumulated
-        self.grad_averager.step(total_samples=total)
+        self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
         self.state_averager.step(optimizer_step=True, averaging_round=True)
+        faults.after_update(self.local_epoch, self._params)
         self.grad_averager.reset_accumulated_grads_()
         self.tracker.update_epoch(self.local_epoch)
         self.last_epoch_time = time.perf_counter() - t0

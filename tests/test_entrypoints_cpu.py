@@ -72,3 +72,19 @@ def test_two_peers_plus_aux(tmp_path):
     # backups written by the training callback
     st = torch.load(tmp_path / "state.zip", weights_only=True)
     assert set(st) == {"model", "training", "scheduler", "local_epoch"}
+
+
+def test_nan_rollback_and_averaging_fallback(tmp_path):
+    """Fault injection (SURVEY §4 tier 5): NaN parameters after epoch 3 -> the callback restores the
+    backup; an injected averaging failure at epoch 1 -> local gradients are used and training goes on."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", DALLE_AMD_FAULT_NAN_PARAMS="3",
+               DALLE_AMD_FAULT_FAIL_AVERAGING="1")
+    r = subprocess.run(
+        [sys.executable, os.path.join(ROOT, "run_trainer.py"), *COMMON, "--per_device_train_batch_size", "2",
+         "--target_batch_size", "2", "--max_steps", "6", "--warmup_steps", "1", "--total_steps", "10",
+         "--output_dir", str(tmp_path / "out"), "--backup_every_steps", "1", "--state_path", str(tmp_path / "state.zip")],
+        cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "falling back to local gradients" in r.stdout
+    assert "Parameters are invalid, reloading model from earlier state" in r.stdout
+    assert "Restored from a backup" in r.stdout
