@@ -77,11 +77,11 @@ def main():
             for s in (4, 8, 16):
                 gs, xs = g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K)
                 try:
-                    t_sk = timeit(lambda: torch.bmm(gs, xs, out_dtype=torch.float32).sum(0, out=acc))
+                    t_sk = timeit(lambda: torch.sum(torch.bmm(gs, xs, out_dtype=torch.float32), 0, out=acc))
                     r[f"dw_splitk{s}_bmm32_TF"] = round(fl / t_sk / 1e9)
                 except Exception as e:  # out_dtype for bmm may be unsupported on this build
                     r[f"dw_splitk{s}_bmm32_TF"] = str(e)[:60]
-                t_sk16 = timeit(lambda: torch.bmm(gs, xs).float().sum(0, out=acc))
+                t_sk16 = timeit(lambda: torch.sum(torch.bmm(gs, xs), 0, dtype=torch.float32, out=acc))
                 r[f"dw_splitk{s}_bmm16_TF"] = round(fl / t_sk16 / 1e9)
             res.append(r)
             print(json.dumps(r), flush=True)

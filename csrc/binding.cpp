@@ -15,14 +15,15 @@ void attn_bwd(const void*, const void*, const void*, const void*, const void*, c
 void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
 void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
 bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t);
-bool ln_shift_bwd(const float*, const float*, const void*, const float*, const float*, float*, float*, float*, const ShiftGeom&,
-                  int, int, hipStream_t);
+bool ln_shift_bwd(const float*, const float*, const void*, const float*, const float*, const float*, float*, float*,
+                  const GradSink&, const ShiftGeom&, int, int, hipStream_t);
 void geglu_fwd(const void*, void*, long, int, hipStream_t);
 void geglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
-void geglu_bwd_bias(const void*, const void*, void*, float*, float*, long, int, hipStream_t);
+void geglu_bwd_bias(const void*, const void*, void*, float*, const GradSink&, long, int, hipStream_t);
 void scale_residual(const float*, const void*, const float*, float*, long, int, hipStream_t);
-void scale_residual_bwd(const float*, const void*, const float*, void*, float*, long, int, hipStream_t);
+void scale_residual_bwd(const float*, const void*, const float*, void*, float*, const GradSink&, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
+void splitk_accum(const float*, float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
                      hipStream_t);
@@ -86,19 +87,48 @@ std::vector<Tensor> ln_shift_fwd(Tensor x, Tensor w, Tensor b, int64_t T, int64_
   return {y, mean, rstd};
 }
 
-std::vector<Tensor> ln_shift_bwd(Tensor x, Tensor w, Tensor dy, Tensor mean, Tensor rstd, int64_t T, int64_t S, bool shift) {
+// grad sink: an fp32 contiguous buffer of `n` floats that the kernel ACCUMULATES into (a .grad view
+// of the flat arena); returns its pointer or nullptr when absent
+static float* sink_ptr(const c10::optional<Tensor>& t, long n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->numel() == n, what,
+              ": grad sink must be a contiguous fp32 CUDA tensor of ", n, " elements");
+  return t->data_ptr<float>();
+}
+
+// LN(+shift) backward. resid (optional, fp32 like x): residual-stream grad added into dx.
+// gw/gb (optional, together): accumulate dweight/dbias into them and return undefined (None) for both.
+std::vector<Tensor> ln_shift_bwd(Tensor x, Tensor w, Tensor dy, Tensor mean, Tensor rstd, int64_t T, int64_t S, bool shift,
+                                 c10::optional<Tensor> resid, c10::optional<Tensor> gw, c10::optional<Tensor> gb) {
   CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(dy, torch::kBFloat16);
   CHECK_IN(mean, torch::kFloat32); CHECK_IN(rstd, torch::kFloat32);
   const int B = x.size(0), n = x.size(1), D = x.size(2);
   TORCH_CHECK(dy.sizes() == x.sizes() && mean.numel() == B * n && rstd.numel() == B * n);
+  const float* rp = nullptr;
+  if (resid.has_value() && resid->defined()) {
+    CHECK_IN((*resid), torch::kFloat32);
+    TORCH_CHECK(resid->sizes() == x.sizes(), "ln_shift_bwd: residual grad shape mismatch");
+    rp = resid->data_ptr<float>();
+  }
+  float* pw = sink_ptr(gw, D, "ln_shift_bwd dweight");
+  float* pb = sink_ptr(gb, D, "ln_shift_bwd dbias");
+  TORCH_CHECK((pw == nullptr) == (pb == nullptr), "ln_shift_bwd: give both weight and bias grad sinks or neither");
   auto dx = torch::empty_like(x);
   auto part = torch::empty({512, 2 * D}, x.options());  // per-block partial [dw | db] rows
-  auto dwdb = torch::empty({2 * D}, x.options());
+  Tensor dwdb;
+  dalle::GradSink sink;
+  if (pw) {
+    sink = dalle::GradSink{pw, pb, nullptr, D, 1};
+  } else {
+    dwdb = torch::empty({2 * D}, x.options());
+    sink = dalle::GradSink{dwdb.data_ptr<float>(), dwdb.data_ptr<float>() + D, nullptr, D, 0};
+  }
   dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
   bool ok = dalle::ln_shift_bwd(x.data_ptr<float>(), w.data_ptr<float>(), dy.data_ptr(), mean.data_ptr<float>(),
-                                rstd.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), dwdb.data_ptr<float>(), g,
-                                B * n, D, cur_stream());
+                                rstd.data_ptr<float>(), rp, dx.data_ptr<float>(), part.data_ptr<float>(), sink, g, B * n, D,
+                                cur_stream());
   TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
+  if (pw) return {dx, Tensor(), Tensor()};
   return {dx, dwdb.slice(0, 0, D), dwdb.slice(0, D, 2 * D)};
 }
 
@@ -202,17 +232,23 @@ Tensor geglu_bwd(Tensor h, Tensor dout) {
   return dh;
 }
 
-// GEGLU backward + FF-in bias grad (column sums of dh) in one pass: returns {dh, dbias(2F, fp32)}
-std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout) {
+// GEGLU backward + FF-in bias grad (column sums of dh) in one pass: returns {dh, dbias(2F, fp32)}, or
+// {dh, undefined} after accumulating dbias into the optional sink `gb`
+std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout, c10::optional<Tensor> gb) {
   CHECK_IN(h, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16);
   const long F2 = h.size(-1);
   const long M = h.numel() / F2;
   TORCH_CHECK(F2 % 16 == 0 && dout.numel() == M * F2 / 2);
   auto dh = torch::empty_like(h);
   auto part = torch::empty({256, F2}, h.options().dtype(torch::kFloat32));
-  auto db = torch::empty({F2}, h.options().dtype(torch::kFloat32));
-  dalle::geglu_bwd_bias(h.data_ptr(), dout.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), db.data_ptr<float>(), M, F2 / 2,
-                        cur_stream());
+  float* pb = sink_ptr(gb, F2, "geglu_bwd_bias dbias");
+  Tensor db;
+  if (!pb) {
+    db = torch::empty({F2}, h.options().dtype(torch::kFloat32));
+    pb = db.data_ptr<float>();
+  }
+  dalle::geglu_bwd_bias(h.data_ptr(), dout.data_ptr(), dh.data_ptr(), part.data_ptr<float>(),
+                        dalle::GradSink{pb, nullptr, nullptr, (int)F2, db.defined() ? 0 : 1}, M, F2 / 2, cur_stream());
   return {dh, db};
 }
 
@@ -232,16 +268,35 @@ void scale_residual_out(Tensor x, Tensor y, Tensor scale, Tensor out) {
                         cur_stream());
 }
 
-std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale) {
+// LayerScale(+residual) backward: dy = bf16(scale * g) and the column sums (sum g*y, sum g).
+// Without sinks returns {dy, dscale, gsum}. With the optional sinks it accumulates dscale into
+// `gscale` and scale * gsum (the bias grad of a GEMM whose output was y) into `gbias` (if given),
+// returning {dy, undefined, undefined}.
+std::vector<Tensor> scale_residual_bwd(Tensor g, Tensor y, Tensor scale, c10::optional<Tensor> gscale,
+                                       c10::optional<Tensor> gbias) {
   CHECK_IN(g, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
   const long D = g.size(-1);
   TORCH_CHECK(D % 8 == 0 && D <= 2048 && y.numel() == g.numel() && scale.numel() == D);
+  float* ps = sink_ptr(gscale, D, "scale_residual_bwd dscale");
+  float* pb = sink_ptr(gbias, D, "scale_residual_bwd dbias");
+  TORCH_CHECK(ps || !pb, "scale_residual_bwd: a bias sink needs a scale sink");
   auto dy = torch::empty(g.sizes(), y.options());
-  auto ws = torch::empty({(512 + 1) * 2 * D}, g.options());  // 512 partial rows + the reduced row (2D wide)
-  dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), ws.data_ptr<float>(),
+  auto ws = torch::empty({(512 + (ps ? 0 : 1)) * 2 * D}, g.options());  // 512 partial rows (+ the reduced row)
+  float* red = ws.data_ptr<float>() + 512 * 2 * D;
+  dalle::GradSink sink = ps ? dalle::GradSink{ps, pb, scale.data_ptr<float>(), (int)D, 1}
+                            : dalle::GradSink{red, red + D, nullptr, (int)D, 0};
+  dalle::scale_residual_bwd(g.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), dy.data_ptr(), ws.data_ptr<float>(), sink,
                             g.numel() / D, D, cur_stream());
-  // {dy = bf16(scale * g), dscale = sum_rows(g * y), gsum = sum_rows(g)}
+  if (ps) return {dy, Tensor(), Tensor()};
   return {dy, ws.slice(0, 512 * 2 * D, 512 * 2 * D + D), ws.slice(0, 512 * 2 * D + D, 513 * 2 * D)};
+}
+
+// acc [+]= part.sum(0) for a (s, ...) fp32 split-K partial buffer
+void splitk_accum_(Tensor acc, Tensor part, bool accumulate) {
+  CHECK_IN(acc, torch::kFloat32); CHECK_IN(part, torch::kFloat32);
+  const long n = acc.numel();
+  TORCH_CHECK(part.dim() >= 1 && part.numel() == part.size(0) * n && n % 4 == 0, "splitk_accum: shape mismatch");
+  dalle::splitk_accum(part.data_ptr<float>(), acc.data_ptr<float>(), n, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
 }
 
 Tensor nonfinite(Tensor x) {
@@ -345,18 +400,22 @@ void lamb_step(Tensor p, Tensor g, Tensor delta, Tensor q1, Tensor q2, Tensor ab
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dalle_amd HIP/CDNA4 kernels (gfx950)";
   m.def("ln_shift_fwd", &ln_shift_fwd);
-  m.def("ln_shift_bwd", &ln_shift_bwd);
+  m.def("ln_shift_bwd", &ln_shift_bwd, py::arg("x"), py::arg("w"), py::arg("dy"), py::arg("mean"), py::arg("rstd"),
+        py::arg("T"), py::arg("S"), py::arg("shift"), py::arg("resid") = py::none(), py::arg("gw") = py::none(),
+        py::arg("gb") = py::none());
   m.def("rope_fwd", &rope_fwd);
   m.def("rope_bwd", &rope_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
-  m.def("geglu_bwd_bias", &geglu_bwd_bias);
+  m.def("geglu_bwd_bias", &geglu_bwd_bias, py::arg("h"), py::arg("dout"), py::arg("gb") = py::none());
   m.def("scale_residual_", &scale_residual_);
   m.def("scale_residual_out", &scale_residual_out);
-  m.def("scale_residual_bwd", &scale_residual_bwd);
+  m.def("scale_residual_bwd", &scale_residual_bwd, py::arg("g"), py::arg("y"), py::arg("scale"),
+        py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
+  m.def("splitk_accum_", &splitk_accum_);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);
   m.def("decode_rope_", &decode_rope_);

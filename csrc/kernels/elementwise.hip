@@ -1,10 +1,11 @@
 // Memory-bound fused elementwise kernels (SURVEY K9 GEGLU, K8/K10 LayerScale+residual, K17 finite
 // checks). All bf16 traffic is 16 bytes per lane (Guideline 13).
 #include "common.h"
+#include "geom.h"
 
 namespace dalle {
 
-void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st);
+void column_sum(const float* part, int nrows, int width, const GradSink& sink, hipStream_t st);
 constexpr int SR_BWD_BLOCKS = 512;
 
 // GEGLU: h (M, 2F) -> out (M, F) = h[:, :F] * gelu(h[:, F:])   (exact erf GELU)
@@ -95,7 +96,7 @@ __global__ void scale_residual_kernel(const float* x, const __bf16* __restrict__
   op[1] = x1;
 }
 
-// dy = bf16(scale * g); dscale partials: per block column sums of g * y -> atomics into dscale
+// dy = bf16(scale * g); per block partial column sums of g * y and of g (reduced by column_sum)
 __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __restrict__ g, const __bf16* __restrict__ y,
                                                                  const float* __restrict__ scale, __bf16* __restrict__ dy,
                                                                  float* __restrict__ dscale, long M, int D) {
@@ -144,6 +145,21 @@ __global__ __launch_bounds__(256) void scale_residual_bwd_kernel(const float* __
   }
 }
 
+// Split-K GEMM reduction: acc (n floats) [+]= sum_s part[s] (part = s x n, fp32), fixed summation
+// order (deterministic). The weight-grad GEMMs have a long reduction dimension (B x 1280 tokens) and a
+// small output (d x d): hipBLASLt fills 256 CUs only when that reduction is split into a batch of
+// GEMMs, whose fp32 partial outputs this kernel folds into the fp32 grad arena.
+__global__ void splitk_accum_kernel(const float* __restrict__ part, float* __restrict__ acc, long n, int s, int accumulate) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  f32x4 v = accumulate ? *reinterpret_cast<const f32x4*>(acc + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < s; ++k) {
+    const f32x4 p = *reinterpret_cast<const f32x4*>(part + (size_t)k * n + i);
+    v[0] += p[0]; v[1] += p[1]; v[2] += p[2]; v[3] += p[3];
+  }
+  *reinterpret_cast<f32x4*>(acc + i) = v;
+}
+
 // Non-finite detector over an fp32 buffer: flag[0] = 1 if any element is NaN/Inf
 __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
   long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -167,7 +183,8 @@ void geglu_bwd(const void* h, const void* dout, void* dh, long M, int F, hipStre
                      (__bf16*)dh, M, F);
 }
 constexpr int GEGLU_ROW_BLOCKS = 256;
-void geglu_bwd_bias(const void* h, const void* dout, void* dh, float* part, float* dbias, long M, int F, hipStream_t st) {
+void geglu_bwd_bias(const void* h, const void* dout, void* dh, float* part, const GradSink& dbias, long M, int F,
+                    hipStream_t st) {
   dim3 grid(GEGLU_ROW_BLOCKS, (F / 8 + 255) / 256);
   hipLaunchKernelGGL(geglu_bwd_bias_kernel, grid, dim3(256), 0, st, (const __bf16*)h, (const __bf16*)dout, (__bf16*)dh, part, M, F);
   column_sum(part, GEGLU_ROW_BLOCKS, 2 * F, dbias, st);
@@ -176,13 +193,17 @@ void scale_residual(const float* x, const void* y, const float* scale, float* ou
   const long t = M * (D / 8);
   hipLaunchKernelGGL(scale_residual_kernel, dim3((t + 255) / 256), dim3(256), 0, st, x, (const __bf16*)y, scale, out, M, D);
 }
-void scale_residual_bwd(const float* g, const void* y, const float* scale, void* dy, float* dscale, long M, int D,
-                        hipStream_t st) {
-  // dscale points at [SR_BWD_BLOCKS x 2D partial rows | 2D outputs = (sum_rows g*y, sum_rows g)]
+void scale_residual_bwd(const float* g, const void* y, const float* scale, void* dy, float* part, const GradSink& sink, long M,
+                        int D, hipStream_t st) {
+  // part: SR_BWD_BLOCKS x 2D partial rows [g*y | g]; the sink receives (sum_rows g*y, sum_rows g [* mul1])
   const int blocks = SR_BWD_BLOCKS;
-  hipLaunchKernelGGL(scale_residual_bwd_kernel, dim3(blocks), dim3(256), 0, st, g, (const __bf16*)y, scale, (__bf16*)dy, dscale,
-                     M, D);
-  column_sum(dscale, blocks, 2 * D, dscale + (size_t)blocks * 2 * D, st);
+  hipLaunchKernelGGL(scale_residual_bwd_kernel, dim3(blocks), dim3(256), 0, st, g, (const __bf16*)y, scale, (__bf16*)dy, part, M,
+                     D);
+  column_sum(part, blocks, 2 * D, sink, st);
+}
+void splitk_accum(const float* part, float* acc, long n, int s, int accumulate, hipStream_t st) {
+  const long t = n / 4;
+  hipLaunchKernelGGL(splitk_accum_kernel, dim3((t + 255) / 256), dim3(256), 0, st, part, acc, n, s, accumulate);
 }
 void nonfinite(const float* x, long n, int* flag, hipStream_t st) {
   long blocks = (n / 4 + 255) / 256;

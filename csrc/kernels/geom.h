@@ -30,4 +30,12 @@ struct ShiftGeom {
   int S;      // image side
   int shift;  // 0 = plain LayerNorm
 };
+// Destination of a column-reduced parameter gradient (see column_sum_kernel)
+struct GradSink {
+  float* out0;        // columns [0, split)
+  float* out1;        // columns [split, width) (nullptr: dropped)
+  const float* mul1;  // optional per-column multiplier for out1
+  int split;
+  int accumulate;     // 1: dst += v (the fp32 grad arena), 0: dst = v
+};
 }  // namespace dalle

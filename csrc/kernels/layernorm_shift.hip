@@ -6,9 +6,10 @@
 // left; missing sources are zeros. One wave per source row: it normalises its row once and scatters
 // each channel quarter to its destination row, and writes the zeros its own row is owed, so every
 // output element is written exactly once (no memset, no second pass).
-// Backward: one wave per source row gathers the shifted output grads back, then LN backward;
-// dweight / dbias are reduced per wave over a grid-stride loop and added with one fp32 atomic per
-// channel per wave.
+// Backward: one wave per source row gathers the shifted output grads back, then LN backward, and
+// adds the residual-stream grad (dx = g_resid + dLN/dx) so the caller needs no separate add;
+// dweight / dbias are reduced deterministically (per-block partial rows -> column_sum) straight
+// into the parameters' fp32 grad buffers (GradSink).
 #include "common.h"
 #include "geom.h"
 
@@ -85,8 +86,8 @@ __global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restri
 template <int D>
 __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const __bf16* __restrict__ dy, const float* __restrict__ mean_in,
-                                                           const float* __restrict__ rstd_in, float* __restrict__ dx,
-                                                           float* __restrict__ dw, float* __restrict__ db, ShiftGeom g,
+                                                           const float* __restrict__ rstd_in, const float* __restrict__ resid,
+                                                           float* __restrict__ dx, float* __restrict__ dw, ShiftGeom g,
                                                            int rows) {
   constexpr int PER = D / 256;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -123,9 +124,10 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = 4 * (lane + 64 * j);
-      f32x4 o;
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+      if (resid) o = *reinterpret_cast<const f32x4*>(resid + (size_t)row * D + c);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = rstd * (gy[j][i] - s1 - xh[j][i] * s2);
+      for (int i = 0; i < 4; ++i) o[i] += rstd * (gy[j][i] - s1 - xh[j][i] * s2);
       *reinterpret_cast<f32x4*>(dx + (size_t)row * D + c) = o;
     }
   }
@@ -149,8 +151,10 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 
 // sum `nrows` partial rows of width `width` (column-parallel, fixed order)
 // 256 threads = 64 columns x 4 row groups; 8 independent loads in flight per thread
-__global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part, int nrows, int width,
-                                                         float* __restrict__ out) {
+// The result goes to a GradSink: columns [0, split) -> out0, [split, width) -> out1 (optionally
+// multiplied per column by mul1), written or ACCUMULATED into the destination -- the destinations
+// are the parameters' fp32 .grad views in the flat arena, so no autograd add kernel follows.
+__global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part, int nrows, int width, GradSink sink) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -168,11 +172,25 @@ __global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict
   }
   red[rg][cl] = s;
   __syncthreads();
-  if (rg == 0 && c < width) out[c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (rg == 0 && c < width) {
+    float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    float* dst;
+    if (c < sink.split) {
+      dst = sink.out0 + c;
+    } else {
+      if (sink.out1 == nullptr) return;
+      dst = sink.out1 + (c - sink.split);
+      if (sink.mul1) v *= sink.mul1[c - sink.split];
+    }
+    *dst = sink.accumulate ? *dst + v : v;
+  }
 }
 
+void column_sum(const float* part, int nrows, int width, const GradSink& sink, hipStream_t st) {
+  hipLaunchKernelGGL(column_sum_kernel, dim3((width + 63) / 64), dim3(256), 0, st, part, nrows, width, sink);
+}
 void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(column_sum_kernel, dim3((width + 63) / 64), dim3(256), 0, st, part, nrows, width, out);
+  column_sum(part, nrows, width, GradSink{out, nullptr, nullptr, width, 0}, st);
 }
 
 // plain LayerNorm variants for the final norm (no shift): same kernels with shift = 0
@@ -184,14 +202,14 @@ static void launch_fwd(const float* x, const float* w, const float* b, void* y, 
 }
 
 template <int D>
-static void launch_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, float* dx, float* dw,
-                       float* db, const ShiftGeom& g, int rows, hipStream_t st) {
-  // dw points at a (LN_BWD_BLOCKS x 2D) partial buffer; db receives [dw | db] (2D floats)
+static void launch_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, const float* resid,
+                       float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, hipStream_t st) {
+  // part is a (LN_BWD_BLOCKS x 2D) partial buffer; the sink receives [dw | db]
   int blocks = (rows + 3) / 4;
   if (blocks > LN_BWD_BLOCKS) blocks = LN_BWD_BLOCKS;
-  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, dx, dw, nullptr, g,
-                     rows);
-  column_sum(dw, blocks, 2 * D, db, st);
+  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid, dx, part,
+                     g, rows);
+  column_sum(part, blocks, 2 * D, sink, st);
 }
 
 bool ln_shift_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g, int rows,
@@ -205,13 +223,13 @@ bool ln_shift_fwd(const float* x, const float* w, const float* b, void* y, float
   }
 }
 
-bool ln_shift_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, float* dx, float* dw,
-                  float* db, const ShiftGeom& g, int rows, int D, hipStream_t st) {
+bool ln_shift_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, const float* resid,
+                  float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, int D, hipStream_t st) {
   switch (D) {
-    case 256: launch_bwd<256>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
-    case 512: launch_bwd<512>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
-    case 1024: launch_bwd<1024>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
-    case 2048: launch_bwd<2048>(x, w, dy, mean, rstd, dx, dw, db, g, rows, st); return true;
+    case 256: launch_bwd<256>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
+    case 512: launch_bwd<512>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
+    case 1024: launch_bwd<1024>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
+    case 2048: launch_bwd<2048>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
     default: return false;
   }
 }

@@ -177,13 +177,11 @@ class Transformer(nn.Module):
         cfg = self.cfg
         for f, g in pairs:
             pre, attn = f.fn, f.fn.fn.fn
-            h = ops.layernorm_shift(x, pre.norm.weight, pre.norm.bias, cfg.text_len, cfg.image_fmap_size, pre.fn.enabled)
-            o = ops.attention_out(h, attn.to_qkv.weight, attn.heads, self.geom, attn.attn_type)
-            x = ops.proj_residual(x, o, attn.to_out[0].weight, attn.to_out[0].bias, f.scale)
+            x = ops.attn_sublayer(x, pre.norm.weight, pre.norm.bias, attn.to_qkv.weight, attn.to_out[0].weight,
+                                  attn.to_out[0].bias, f.scale, attn.heads, self.geom, attn.attn_type, pre.fn.enabled)
             pre, ff = g.fn, g.fn.fn.fn
-            h = ops.layernorm_shift(x, pre.norm.weight, pre.norm.bias, cfg.text_len, cfg.image_fmap_size, pre.fn.enabled)
-            u = ops.ff_hidden(h, ff.net[0].weight, ff.net[0].bias)
-            x = ops.proj_residual(x, u, ff.net[3].weight, ff.net[3].bias, g.scale)
+            x = ops.ff_sublayer(x, pre.norm.weight, pre.norm.bias, ff.net[0].weight, ff.net[0].bias, ff.net[3].weight,
+                                ff.net[3].bias, g.scale, cfg.text_len, cfg.image_fmap_size, pre.fn.enabled)
         return x
 
 

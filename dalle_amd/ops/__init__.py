@@ -100,6 +100,22 @@ def proj_residual(x, o, w, b, scale):
     return x + (y * scale.to(dt)).to(x.dtype)
 
 
+def attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads: int, geom, attn_type: str, shift: bool):
+    """x + LayerScale * Attention(PreShiftToken(LayerNorm(x))) -- one fused autograd node on HIP."""
+    if backend_for(x) == "hip":
+        return _hip().attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads, geom, attn_type, shift)
+    h = layernorm_shift(x, ln_w, ln_b, geom.text_len, geom.image_size, shift)
+    return proj_residual(x, attention_out(h, w_qkv, heads, geom, attn_type), w_out, b_out, scale)
+
+
+def ff_sublayer(x, ln_w, ln_b, w1, b1, w2, b2, scale, text_len: int, image_size: int, shift: bool):
+    """x + LayerScale * FeedForward(PreShiftToken(LayerNorm(x))) -- one fused autograd node on HIP."""
+    if backend_for(x) == "hip":
+        return _hip().ff_sublayer(x, ln_w, ln_b, w1, b1, w2, b2, scale, text_len, image_size, shift)
+    h = layernorm_shift(x, ln_w, ln_b, text_len, image_size, shift)
+    return proj_residual(x, ff_hidden(h, w1, b1), w2, b2, scale)
+
+
 def begin_forward():
     """Start of a model forward: drops the per-forward bf16 weight casts of the HIP path."""
     if hip_available():

@@ -7,6 +7,7 @@ blocks (summed over every layer that reuses them) never round through bf16.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -69,15 +70,51 @@ def _rope_tables(geom: AttnGeometry, dim_head: int, device):
 FUSE_WGRAD = True
 
 
+def wgrad_splits(M: int, N: int, K: int) -> int:
+    """Split-K factor for a weight-grad GEMM (N x K output, reduction over M tokens). Measured on
+    MI355X at M = 20480 (profiles/r1_gemm_wgrad.jsonl): 1024x1024 272 -> 576 TF at 8 splits, 3072x1024
+    533 -> 746 TF and 1024x4096 533 -> 873 TF at 4; 8192x1024 already fills the chip (917 TF)."""
+    if SPLITK_WGRAD == 0:
+        return 1
+    nk = N * K
+    s = 8 if nk <= 1536 * 1024 else (4 if nk <= 4608 * 1024 else 1)
+    while s > 1 and (M % s or M // s < 1024):
+        s //= 2
+    return s
+
+
+SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
+
+
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
-    """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate IN the
-    GEMM (hipBLASLt beta = 1, bf16 in / fp32 out) and return None: no temporary dW, no separate add
-    kernel, and the shared blocks' grads (one per reusing layer) sum in fp32 inside the GEMM."""
+    """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate into it
+    and return None: no temporary dW and no autograd add kernel, and the shared blocks' grads (one per
+    reusing layer) sum in fp32. Small outputs run as a split-K batched GEMM (fp32 partials) + one
+    deterministic fold kernel; large ones accumulate inside the GEMM (hipBLASLt beta = 1)."""
     gw = w.grad
-    if FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape:
+    fused = FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape
+    M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
+    s = wgrad_splits(M, N, K)
+    if s > 1:
+        part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
+        out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
+        C().splitk_accum_(out, part, fused)
+        return None if fused else out
+    if fused:
         torch.addmm(gw, g2.t(), x2, out_dtype=torch.float32, out=gw)
         return None
     return torch.mm(g2.t(), x2, out_dtype=torch.float32)
+
+
+def grad_sink(p: torch.Tensor, needed: bool = True):
+    """The fp32 ``.grad`` buffer (flattened view) a kernel may accumulate ``p``'s gradient into, or None
+    (then the op returns the gradient to autograd as usual). Same contract as ``weight_grad``."""
+    if not (FUSE_WGRAD and needed):
+        return None
+    g = p.grad
+    if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.shape == p.shape:
+        return g.view(-1)
+    return None
 
 
 def _bf16c(t):
@@ -186,6 +223,7 @@ class _LNShift(torch.autograd.Function):
         y, mean, rstd = C().ln_shift_fwd(x, w.contiguous(), b.contiguous(), T, S, shift, 1e-5)
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.geo = (T, S, shift)
+        ctx.params = (w, b)
         return y
 
     @staticmethod
@@ -193,7 +231,11 @@ class _LNShift(torch.autograd.Function):
         x, w, mean, rstd = ctx.saved_tensors
         T, S, shift = ctx.geo
         gy = gy.to(torch.bfloat16).contiguous()
-        dx, dw, db = C().ln_shift_bwd(x, w.contiguous(), gy, mean, rstd, T, S, shift)
+        sk = _sinks(ctx.params, ctx.needs_input_grad[1:3])
+        if sk is not None:
+            dx, dw, db = C().ln_shift_bwd(x, w.contiguous(), gy, mean, rstd, T, S, shift, None, sk[0], sk[1])
+        else:
+            dx, dw, db = C().ln_shift_bwd(x, w.contiguous(), gy, mean, rstd, T, S, shift)
         return dx, dw, db, None, None, None
 
 
@@ -242,6 +284,138 @@ def attention_out(h, w_qkv, heads: int, geom: AttnGeometry, attn_type: str):
 
 def attention_block(h, w_qkv, w_out, b_out, heads: int, geom: AttnGeometry, attn_type: str):
     return linear(attention_out(h, w_qkv, heads, geom, attn_type), w_out, b_out)
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole pre-norm sublayers, x -> x + LayerScale * branch(LN_shift(x)), as ONE autograd node each with
+# a hand-written backward (reference: dalle_pytorch/transformer.py PreNorm / PreShiftToken /
+# LayerScale around Attention and FeedForward). Versus chaining the per-op Functions this removes the
+# residual-grad add (it happens inside the LN-backward kernel) and, with the flat grad arena, every
+# parameter-grad add: GEMM weight grads accumulate in hipBLASLt (beta = 1), LayerNorm / LayerScale /
+# bias grads accumulate inside the column-reduction kernel.
+# ---------------------------------------------------------------------------------------------
+def _sinks(params, needs):
+    """Arena grad buffers for every parameter, or None if any needed one is missing (fallback: return
+    all grads to autograd)."""
+    sinks = [grad_sink(p) for p in params]
+    if all(n for n in needs) and all(s is not None for s in sinks):
+        return sinks
+    return None
+
+
+class _AttnSublayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta):
+        T, S, K, H, pattern, shift = meta
+        x = x.contiguous()
+        B, n, d = x.shape
+        h, mean, rstd = C().ln_shift_fwd(x, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+        h2 = h.view(-1, d)
+        wq = bf16_weight(w_qkv)
+        qkv = torch.mm(h2, wq.t()).view(B, n, -1)
+        col = pattern == PATTERN_IDS["axial_col"]
+        q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+        del qkv
+        out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
+        wo = bf16_weight(w_out)
+        y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())
+        s = scale.reshape(-1).contiguous()
+        xo = torch.empty_like(x)
+        C().scale_residual_out(x, y, s, xo)
+        ctx.save_for_backward(x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin)
+        ctx.params = (ln_w, ln_b, w_qkv, w_out, b_out, scale)
+        ctx.meta = (B, n, T, S, K, H, pattern, shift, col)
+        return xo
+
+    @staticmethod
+    def backward(ctx, g):
+        x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin = ctx.saved_tensors
+        ln_w, ln_b, w_qkv, w_out, b_out, scale = ctx.params
+        B, n, T, S, K, H, pattern, shift, col = ctx.meta
+        g = g.contiguous()
+        sk = _sinks(ctx.params, ctx.needs_input_grad[1:7])
+        if sk is not None:
+            dy, _, _ = C().scale_residual_bwd(g, y, s, sk[5], sk[4])
+            db = dscale = None
+        else:
+            dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
+            db, dscale = gsum * s, dscale.view(scale.shape)
+        dy = dy.view(-1, dy.shape[-1])
+        o2 = out.view(-1, out.shape[-1])
+        do = torch.mm(dy, wo).view(out.shape)
+        dwo = weight_grad(w_out, dy, o2)
+        dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
+        del do
+        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
+        del dq, dk, dv
+        dh = torch.mm(dqkv, wq).view(x.shape)
+        dwq = weight_grad(w_qkv, dqkv, h2)
+        if sk is not None:
+            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
+        else:
+            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g)
+        return dx, dlw, dlb, dwq, dwo, db, dscale, None, None, None
+
+
+class _FFSublayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, w1, b1, w2, b2, scale, meta):
+        T, S, shift = meta
+        x = x.contiguous()
+        d = x.shape[-1]
+        h, mean, rstd = C().ln_shift_fwd(x, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+        h2 = h.view(-1, d)
+        w1b, w2b = bf16_weight(w1), bf16_weight(w2)
+        a = torch.addmm(bf16_weight(b1), h2, w1b.t())
+        u = C().geglu_fwd(a)
+        y = torch.addmm(bf16_weight(b2), u, w2b.t())
+        s = scale.reshape(-1).contiguous()
+        xo = torch.empty_like(x)
+        C().scale_residual_out(x, y, s, xo)
+        ctx.save_for_backward(x, mean, rstd, h2, w1b, a, u, w2b, y, s)
+        ctx.params = (ln_w, ln_b, w1, b1, w2, b2, scale)
+        ctx.meta = meta
+        return xo
+
+    @staticmethod
+    def backward(ctx, g):
+        x, mean, rstd, h2, w1b, a, u, w2b, y, s = ctx.saved_tensors
+        ln_w, ln_b, w1, b1, w2, b2, scale = ctx.params
+        T, S, shift = ctx.meta
+        g = g.contiguous()
+        sk = _sinks(ctx.params, ctx.needs_input_grad[1:8])
+        if sk is not None:
+            dy, _, _ = C().scale_residual_bwd(g, y, s, sk[6], sk[5])
+            db2 = dscale = None
+        else:
+            dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
+            db2, dscale = gsum * s, dscale.view(scale.shape)
+        dy = dy.view(-1, dy.shape[-1])
+        du = torch.mm(dy, w2b)
+        dw2 = weight_grad(w2, dy, u)
+        da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
+        del du
+        dh = torch.mm(da, w1b).view(x.shape)
+        dw1 = weight_grad(w1, da, h2)
+        if sk is not None:
+            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
+        else:
+            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g)
+        return dx, dlw, dlb, dw1, db1, dw2, db2, dscale, None
+
+
+def attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):
+    """x + scale * to_out(sparse_attention(rotary(to_qkv(LN_shift(x))))) in one autograd node."""
+    dim_head = w_qkv.shape[0] // 3 // heads
+    assert dim_head == 64, "the HIP attention kernels are specialised for dim_head = 64"
+    cos, sin = _rope_tables(geom, dim_head, x.device)
+    meta = (geom.text_len, geom.image_size, geom.kernel_size, heads, PATTERN_IDS[attn_type], bool(shift))
+    return _AttnSublayer.apply(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta)
+
+
+def ff_sublayer(x, ln_w, ln_b, w1, b1, w2, b2, scale, text_len: int, image_size: int, shift: bool):
+    """x + scale * W2 GEGLU(W1 LN_shift(x) + b1) + b2 in one autograd node."""
+    return _FFSublayer.apply(x, ln_w, ln_b, w1, b1, w2, b2, scale, (text_len, image_size, bool(shift)))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -311,6 +485,7 @@ class _SplitXent(torch.autograd.Function):
         loss = (loss_t.mean() + img_w * loss_i.mean()) / den
         ctx.save_for_backward(ht, hi, logit_t, logit_i, wb)
         ctx.meta = (B, n, d, text_seq_len, Vt)
+        ctx.params = (w, b)
         return loss
 
     @staticmethod
@@ -321,6 +496,16 @@ class _SplitXent(torch.autograd.Function):
         dh = torch.empty(B, n, d, dtype=torch.bfloat16, device=ht.device)
         dh[:, :tsl] = (torch.mm(dt, wb[:Vt]) * g).view(B, tsl, d)
         dh[:, tsl:] = (torch.mm(di, wb[Vt:]) * g).view(B, n - tsl, d)
+        w, b = ctx.params
+        gw, gb = grad_sink(w, ctx.needs_input_grad[1]), grad_sink(b, ctx.needs_input_grad[2])
+        if gw is not None and gb is not None:
+            # accumulate into the arena: the upstream scalar is folded into the (small) activations
+            gw = gw.view(wb.shape)
+            torch.addmm(gw[:Vt], dt.t(), ht * g, out_dtype=torch.float32, out=gw[:Vt])
+            torch.addmm(gw[Vt:], di.t(), hi * g, out_dtype=torch.float32, out=gw[Vt:])
+            gb[:Vt].add_(torch.sum(dt, 0, dtype=torch.float32) * g)
+            gb[Vt:].add_(torch.sum(di, 0, dtype=torch.float32) * g)
+            return dh, None, None, None, None, None, None
         dw = torch.empty(wb.shape, dtype=torch.float32, device=wb.device)
         dw[:Vt] = torch.mm(dt.t(), ht, out_dtype=torch.float32)
         dw[Vt:] = torch.mm(di.t(), hi, out_dtype=torch.float32)
