@@ -240,7 +240,7 @@ std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout, c10::optional<Tensor> 
   const long M = h.numel() / F2;
   TORCH_CHECK(F2 % 16 == 0 && dout.numel() == M * F2 / 2);
   auto dh = torch::empty_like(h);
-  auto part = torch::empty({256, F2}, h.options().dtype(torch::kFloat32));
+  auto part = torch::empty({512, F2}, h.options().dtype(torch::kFloat32));  // GEGLU_ROW_BLOCKS partial rows
   float* pb = sink_ptr(gb, F2, "geglu_bwd_bias dbias");
   Tensor db;
   if (!pb) {

@@ -19,7 +19,16 @@
 
 namespace dalle {
 
-constexpr int RS = 72;  // LDS row stride in bf16 (144 B): conflict-free ds_read_b128 row reads
+// LDS tile image: rows of 64 bf16 (128 B, no padding); 16-byte chunk ch of row r lives at chunk
+// ch ^ swz(r). With this XOR both MFMA operand reads are bank-conflict-free: the ds_read_b128 row
+// reads (16-lane groups read 16 different rows, one chunk: the 8 same-parity rows of a group get 8
+// distinct swz values) and the ds_read_b64_tr_b16 transposed reads (a 32-lane half reads rows
+// R..R+3 x 4 chunks: rows R and R+2 share a bank row, and swz differs in bit 2 between them).
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int lds_idx(int r, int col) { return r * 64 + ((((col >> 3) ^ swz(r)) << 3) | (col & 7)); }
+constexpr int TILE = 32 * 64;  // elements of one 32-row tile image
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ int st2seq(const AttnGeom& g, int s) {
   if (s < g.T) return s;
@@ -30,21 +39,64 @@ __device__ __forceinline__ int st2seq(const AttnGeom& g, int s) {
   return p < g.n ? p : -1;
 }
 
-__device__ __forceinline__ bool allowed_st(const AttnGeom& g, int qs, int ks) {
-  if (qs < g.Tp) return ks <= qs;
-  if (ks < g.Tp) return ks < g.T;
-  const int qk = qs - g.Tp, kk = ks - g.Tp;
-  if (kk > qk) return false;
-  if (g.pattern == 0) return true;
-  const int qr = qk >> g.logS, kr = kk >> g.logS;
-  if (g.pattern != 3) return qr == kr;
-  const int qc = qk & (g.S - 1), kc = kk & (g.S - 1);
-  return (kr > qr - g.K) && (kc <= qc) && (kc > qc - g.K);
+// bits [lo, hi] of a 32-bit word (empty when hi < lo; bounds clipped to [0, 31])
+__device__ __forceinline__ uint32_t range_bits(int lo, int hi) {
+  lo = max(lo, 0);
+  hi = min(hi, 31);
+  if (hi < lo) return 0u;
+  const uint32_t upto = hi == 31 ? 0xffffffffu : ((1u << (hi + 1)) - 1u);
+  return upto & ~((1u << lo) - 1u);
+}
+
+// Allowed keys of storage query qs within key tile kt, as a bit mask over the tile's 32 keys.
+// Semantics: text query -> causal over the padded text rows; image query -> every
+// real text key plus its local pattern (full: causal; axial row/col: same row of the (possibly
+// column-major) storage, causal; conv_like: the upper-left K x K window).
+__device__ __forceinline__ uint32_t key_mask(const AttnGeom& g, int qs, int kt) {
+  const int k0 = kt * 32;
+  if (qs < g.Tp) return range_bits(0, qs - k0);
+  if (k0 < g.Tp) return range_bits(0, g.T - 1 - k0);
+  const int qk = qs - g.Tp, kk0 = k0 - g.Tp;
+  if (g.pattern == 0) return range_bits(0, qk - kk0);
+  const int qr = qk >> g.logS;
+  if (g.pattern != 3) return range_bits((qr << g.logS) - kk0, qk - kk0);
+  const int qc = qk & (g.S - 1);
+  const int c_lo = max(0, qc - g.K + 1);
+  const int rows = g.S >= 32 ? 1 : (32 >> g.logS);
+  uint32_t m = 0u;
+  for (int i = 0; i < rows; ++i) {
+    const int kr = (kk0 >> g.logS) + i;
+    if (kr > qr - g.K && kr <= qr) m |= range_bits((kr << g.logS) + c_lo - kk0, (kr << g.logS) + qc - kk0);
+  }
+  return m;
+}
+
+// Allowed queries of storage key ks within query tile qt (the transpose of key_mask).
+__device__ __forceinline__ uint32_t query_mask(const AttnGeom& g, int ks, int qt) {
+  const int q0 = qt * 32;
+  if (ks < g.Tp) {
+    if (q0 < g.Tp) return range_bits(ks - q0, 31);
+    return ks < g.T ? 0xffffffffu : 0u;
+  }
+  if (q0 < g.Tp) return 0u;
+  const int kk = ks - g.Tp, qk0 = q0 - g.Tp;
+  if (g.pattern == 0) return range_bits(kk - qk0, 31);
+  const int kr = kk >> g.logS;
+  if (g.pattern != 3) return range_bits(kk - qk0, ((kr + 1) << g.logS) - 1 - qk0);
+  const int kc = kk & (g.S - 1);
+  const int c_hi = min(g.S - 1, kc + g.K - 1);
+  const int rows = g.S >= 32 ? 1 : (32 >> g.logS);
+  uint32_t m = 0u;
+  for (int i = 0; i < rows; ++i) {
+    const int qr = (qk0 >> g.logS) + i;
+    if (qr >= kr && qr < kr + g.K) m |= range_bits((qr << g.logS) + kc - qk0, (qr << g.logS) + c_hi - qk0);
+  }
+  return m;
 }
 
 // wave-uniform: every (query, key) pair of the 32x32 tile (query tile qt, key tile kt) is allowed, so
-// the per-element predicate can be skipped (all text tiles but the padded boundary one for image
-// queries, tiles strictly below the diagonal for text queries / the dense pattern)
+// the mask can be skipped (all text tiles but the padded boundary one for image queries, tiles
+// strictly below the diagonal for text queries / the dense pattern)
 __device__ __forceinline__ bool tile_full(const AttnGeom& g, int qt, int kt) {
   const int ntext = g.Tp >> 5;
   if (kt < ntext) {
@@ -81,19 +133,27 @@ __device__ __forceinline__ s16x4 tr_read(const __bf16* lds) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds));
 }
 
-// A operand X^T (32 x 16) for k-step `ss` of a [row][64] LDS tile, where the MFMA K index is the
-// tile row in the accumulator-permuted order (element j of lane half h = row 16ss + 8(j>>2) + 4h + (j&3)).
+// A operand X^T (32 x 16) for k-step `ss` of a [row][64] swizzled LDS tile, where the MFMA K index is
+// the tile row in the accumulator-permuted order (element j of lane half h = row 16ss + 8(j>>2) + 4h + (j&3)).
 __device__ __forceinline__ bf16x8 tr_operand(const __bf16* tile, int ss, int dt, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = 16 * ss + 4 * (g >> 1) + (i >> 2);
   const int col = 32 * dt + 16 * (g & 1) + 4 * (i & 3);
-  const s16x4 lo = tr_read(tile + row * RS + col);
-  const s16x4 hi = tr_read(tile + (row + 8) * RS + col);
+  const s16x4 lo = tr_read(tile + lds_idx(row, col));
+  const s16x4 hi = tr_read(tile + lds_idx(row + 8, col));
   s16x8 v;
   v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
   v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
   return __builtin_bit_cast(bf16x8, v);
 }
+
+// B operand rows: row c32 of the tile, chunk 2ss + hl (the K index of the S / dP products)
+__device__ __forceinline__ bf16x8 row_operand(const __bf16* tile, int ss, int c32, int hl) {
+  return ld16(tile + lds_idx(c32, 16 * ss + 8 * hl));
+}
+
+// bit of accumulator register r (rows acc_row(r, hl)) in a mask already shifted right by 4*hl
+__device__ __forceinline__ bool mask_bit(uint32_t mh, int r) { return (mh >> ((r & 3) + 8 * (r >> 2))) & 1u; }
 
 __device__ __forceinline__ bf16x8 cvt8(const f32x16& a, int base) {
   bf16x8 r;
@@ -109,10 +169,14 @@ __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r 
 // ------------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------------
+// Lazy rescale threshold (log2 units, T13): the running max is only moved when a tile's max exceeds
+// it by more than this, so P <= 2^8 (exact in bf16's relative precision; fp32 sums have headroom).
+constexpr float RESCALE_THR = 8.0f;
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                           const __bf16* __restrict__ V, __bf16* __restrict__ out,
                                                           float* __restrict__ lse, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 32 * RS];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
   const int bh = blockIdx.y;
   const int b = bh / g.H, h = bh - b * g.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
@@ -144,8 +208,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
     for (int s = 0; s < 4; ++s) qf[s] = ld16(qp + 16 * s);
   }
 
-  // staging: each thread moves one 16-B chunk of K and of V per tile
+  // staging: each thread moves one 16-B chunk of K and of V per tile (swizzled image)
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
+  const int st_off = lds_idx(st_row, st_col);
   auto tile_id = [&](int t) { return t < u_text_end ? t : u_loc_lo + (t - u_text_end); };
   s16x8 kreg, vreg;
   {
@@ -153,13 +218,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
     const size_t off = base + (size_t)(t0 * 32 + st_row) * 64 + st_col;
     kreg = *reinterpret_cast<const s16x8*>(Kt + off);
     vreg = *reinterpret_cast<const s16x8*>(V + off);
-    *reinterpret_cast<s16x8*>(smem + st_row * RS + st_col) = kreg;
-    *reinterpret_cast<s16x8*>(smem + 32 * RS + st_row * RS + st_col) = vreg;
+    *reinterpret_cast<s16x8*>(smem + st_off) = kreg;
+    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = vreg;
   }
   __syncthreads();
 
+  // m: running max of the RAW scores (q carries 1/sqrt(d)); p = 2^(s*log2e - m*log2e) via one fma
   float m = NEG_BIG, lsum = 0.f;
   f32x16 o0 = {}, o1 = {};
+  constexpr float THR_RAW = RESCALE_THR / LOG2E;
 
   for (int t = 0; t < ntiles; ++t) {
     const int tile = tile_id(t);
@@ -169,36 +236,40 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
       kreg = *reinterpret_cast<const s16x8*>(Kt + off);
       vreg = *reinterpret_cast<const s16x8*>(V + off);
     }
-    const __bf16* Ks = smem + (t & 1) * (64 * RS);
-    const __bf16* Vs = Ks + 32 * RS;
+    const __bf16* Ks = smem + (t & 1) * (2 * TILE);
+    const __bf16* Vs = Ks + TILE;
     const bool need = (tile < my_text_end) || (tile >= my_lo && tile <= my_hi);
     if (need) {
       f32x16 s = {};
 #pragma unroll
-      for (int ss = 0; ss < 4; ++ss) s = MFMA32(ld16(Ks + c32 * RS + 16 * ss + 8 * hl), qf[ss], s);
-      float mt = NEG_BIG;
-      const bool full = tile_full(g, qb, tile);
+      for (int ss = 0; ss < 4; ++ss) s = MFMA32(row_operand(Ks, ss, c32, hl), qf[ss], s);
+      if (!tile_full(g, qb, tile)) {
+        const uint32_t mh = key_mask(g, qs, tile) >> (4 * hl);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ks = tile * 32 + acc_row(r, hl);
-        const float x = (full || allowed_st(g, qs, ks)) ? s[r] * LOG2E : NEG_BIG;
-        s[r] = x;
-        mt = fmaxf(mt, x);
+        for (int r = 0; r < 16; ++r) s[r] = mask_bit(mh, r) ? s[r] : NEG_BIG;
       }
+      float mt = fmaxf(fmaxf(s[0], s[1]), s[2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mt = fmaxf(fmaxf(mt, s[r]), s[r + 1]);
+      mt = fmaxf(mt, s[15]);
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mnew = fmaxf(m, mt);
-      const float alpha = exp2f(m - mnew);
-      m = mnew;
+      if (!__all(mt <= m + THR_RAW)) {
+        const float mnew = fmaxf(m, mt);
+        const float alpha = fast_exp2((m - mnew) * LOG2E);
+        m = mnew;
+        lsum *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+      const float mc = m * LOG2E;
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[r] - m);
+        const float p = fast_exp2(fmaf(s[r], LOG2E, -mc));
         s[r] = p;
         ps += p;
       }
-      lsum = lsum * alpha + ps;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      lsum += ps;
       const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
       o0 = MFMA32(tr_operand(Vs, 0, 0, lane), p0, o0);
       o0 = MFMA32(tr_operand(Vs, 1, 0, lane), p1, o0);
@@ -206,9 +277,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
       o1 = MFMA32(tr_operand(Vs, 1, 1, lane), p1, o1);
     }
     if (more) {
-      __bf16* Kn = smem + ((t + 1) & 1) * (64 * RS);
-      *reinterpret_cast<s16x8*>(Kn + st_row * RS + st_col) = kreg;
-      *reinterpret_cast<s16x8*>(Kn + 32 * RS + st_row * RS + st_col) = vreg;
+      __bf16* Kn = smem + ((t + 1) & 1) * (2 * TILE);
+      *reinterpret_cast<s16x8*>(Kn + st_off) = kreg;
+      *reinterpret_cast<s16x8*>(Kn + TILE + st_off) = vreg;
     }
     __syncthreads();
   }
@@ -216,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
   if (!active) return;
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   const float inv = 1.0f / ltot;
-  lse[(size_t)bh * g.Np + qs] = m + log2f(ltot);
+  lse[(size_t)bh * g.Np + qs] = m * LOG2E + log2f(ltot);
   const int p = st2seq(g, qs);
   if (p < 0) return;
   __bf16* op = out + ((size_t)b * g.n + p) * (g.H * 64) + h * 64;
@@ -271,7 +342,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
                                                              __bf16* __restrict__ dQ, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 32 * RS];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
   const int bh = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
@@ -305,14 +376,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
   const float dl = delta[(size_t)bh * g.Np + qrow];
 
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
+  const int st_off = lds_idx(st_row, st_col);
   auto tile_id = [&](int t) { return t < u_text_end ? t : u_loc_lo + (t - u_text_end); };
   s16x8 kreg, vreg;
   {
     const size_t off = base + (size_t)(tile_id(0) * 32 + st_row) * 64 + st_col;
     kreg = *reinterpret_cast<const s16x8*>(Kt + off);
     vreg = *reinterpret_cast<const s16x8*>(V + off);
-    *reinterpret_cast<s16x8*>(smem + st_row * RS + st_col) = kreg;
-    *reinterpret_cast<s16x8*>(smem + 32 * RS + st_row * RS + st_col) = vreg;
+    *reinterpret_cast<s16x8*>(smem + st_off) = kreg;
+    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = vreg;
   }
   __syncthreads();
 
@@ -325,22 +397,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
       kreg = *reinterpret_cast<const s16x8*>(Kt + off);
       vreg = *reinterpret_cast<const s16x8*>(V + off);
     }
-    const __bf16* Ks = smem + (t & 1) * (64 * RS);
-    const __bf16* Vs = Ks + 32 * RS;
+    const __bf16* Ks = smem + (t & 1) * (2 * TILE);
+    const __bf16* Vs = Ks + TILE;
     const bool need = (tile < my_text_end) || (tile >= my_lo && tile <= my_hi);
     if (need) {
       f32x16 s = {}, dp = {};
 #pragma unroll
       for (int ss = 0; ss < 4; ++ss) {
-        s = MFMA32(ld16(Ks + c32 * RS + 16 * ss + 8 * hl), qf[ss], s);
-        dp = MFMA32(ld16(Vs + c32 * RS + 16 * ss + 8 * hl), dof[ss], dp);
+        s = MFMA32(row_operand(Ks, ss, c32, hl), qf[ss], s);
+        dp = MFMA32(row_operand(Vs, ss, c32, hl), dof[ss], dp);
       }
-      const bool full = tile_full(g, qb, tile);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ks = tile * 32 + acc_row(r, hl);
-        const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - lq) : 0.f;
-        s[r] = p * (dp[r] - dl);
+      for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], LOG2E, -lq)) * (dp[r] - dl);
+      if (!tile_full(g, qb, tile)) {
+        const uint32_t mh = key_mask(g, qs, tile) >> (4 * hl);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = mask_bit(mh, r) ? s[r] : 0.f;
       }
       const bf16x8 d0 = cvt8(s, 0), d1 = cvt8(s, 8);
       dq0 = MFMA32(tr_operand(Ks, 0, 0, lane), d0, dq0);
@@ -349,9 +421,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
       dq1 = MFMA32(tr_operand(Ks, 1, 1, lane), d1, dq1);
     }
     if (more) {
-      __bf16* Kn = smem + ((t + 1) & 1) * (64 * RS);
-      *reinterpret_cast<s16x8*>(Kn + st_row * RS + st_col) = kreg;
-      *reinterpret_cast<s16x8*>(Kn + 32 * RS + st_row * RS + st_col) = vreg;
+      __bf16* Kn = smem + ((t + 1) & 1) * (2 * TILE);
+      *reinterpret_cast<s16x8*>(Kn + st_off) = kreg;
+      *reinterpret_cast<s16x8*>(Kn + TILE + st_off) = vreg;
     }
     __syncthreads();
   }
@@ -377,7 +449,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
                                                                const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                const float* __restrict__ lse, const float* __restrict__ delta,
                                                                __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 32 * RS];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
   __shared__ float stats[2][2][32];
   const int bh = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
@@ -408,14 +480,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
   }
 
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
+  const int st_off = lds_idx(st_row, st_col);
   s16x8 qreg, doreg;
   float lreg = 0.f, dreg = 0.f;
   {
     const size_t off = base + (size_t)(q_lo * 32 + st_row) * 64 + st_col;
     qreg = *reinterpret_cast<const s16x8*>(Q + off);
     doreg = *reinterpret_cast<const s16x8*>(dO + off);
-    *reinterpret_cast<s16x8*>(smem + st_row * RS + st_col) = qreg;
-    *reinterpret_cast<s16x8*>(smem + 32 * RS + st_row * RS + st_col) = doreg;
+    *reinterpret_cast<s16x8*>(smem + st_off) = qreg;
+    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = doreg;
     if (tid < 32) stats[0][0][tid] = lse[(size_t)bh * g.Np + q_lo * 32 + tid];
     else if (tid < 64) stats[0][1][tid - 32] = delta[(size_t)bh * g.Np + q_lo * 32 + tid - 32];
   }
@@ -433,25 +506,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
       else if (tid < 64) dreg = delta[(size_t)bh * g.Np + (qt + 1) * 32 + tid - 32];
     }
     const int buf = t & 1;
-    const __bf16* Qs = smem + buf * (64 * RS);
-    const __bf16* Ds = Qs + 32 * RS;
+    const __bf16* Qs = smem + buf * (2 * TILE);
+    const __bf16* Ds = Qs + TILE;
     const bool need = active && qt >= kb && qt <= my_hi;
     if (need) {
       f32x16 s = {}, dp = {};
 #pragma unroll
       for (int ss = 0; ss < 4; ++ss) {
-        s = MFMA32(ld16(Qs + c32 * RS + 16 * ss + 8 * hl), kf[ss], s);
-        dp = MFMA32(ld16(Ds + c32 * RS + 16 * ss + 8 * hl), vf[ss], dp);
+        s = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], s);
+        dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
       }
       f32x16 ds;
-      const bool full = tile_full(g, qt, kb);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = acc_row(r, hl);
-        const int qs = qt * 32 + ql;
-        const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - stats[buf][0][ql]) : 0.f;
+        const float p = fast_exp2(fmaf(s[r], LOG2E, -stats[buf][0][ql]));
         s[r] = p;
         ds[r] = p * (dp[r] - stats[buf][1][ql]);
+      }
+      if (!tile_full(g, qt, kb)) {
+        const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool on = mask_bit(mh, r);
+          s[r] = on ? s[r] : 0.f;
+          ds[r] = on ? ds[r] : 0.f;
+        }
       }
       const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
       const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
@@ -466,9 +546,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
     }
     if (more) {
       const int nb = (t + 1) & 1;
-      __bf16* Qn = smem + nb * (64 * RS);
-      *reinterpret_cast<s16x8*>(Qn + st_row * RS + st_col) = qreg;
-      *reinterpret_cast<s16x8*>(Qn + 32 * RS + st_row * RS + st_col) = doreg;
+      __bf16* Qn = smem + nb * (2 * TILE);
+      *reinterpret_cast<s16x8*>(Qn + st_off) = qreg;
+      *reinterpret_cast<s16x8*>(Qn + TILE + st_off) = doreg;
       if (tid < 32) stats[nb][0][tid] = lreg;
       else if (tid < 64) stats[nb][1][tid - 32] = dreg;
     }
@@ -503,8 +583,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
                                                                     const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                                     __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
-  // per wave: 2 buffers x {Q, dO} x 32 rows x RS   +  2 buffers x {lse, delta} x 32
-  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * 2 * 32 * RS];
+  // per wave: 2 buffers x {Q, dO} tile images   +  2 buffers x {lse, delta} x 32
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * 2 * TILE];
   __shared__ float stats[4][2][2][32];
   const int bh = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
@@ -519,7 +599,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
 #pragma unroll
     for (int s = 0; s < 4; ++s) { kf[s] = ld16(kp + 16 * s); vf[s] = ld16(vp + 16 * s); }
   }
-  __bf16* wsm = smem + wave * (2 * 2 * 32 * RS);
+  __bf16* wsm = smem + wave * (2 * 2 * TILE);
   const int first = kb + wave;
   const int ntiles = first < nqb ? (nqb - first + 3) / 4 : 0;
   // lane-private staging: 4 chunks of Q and 4 of dO per tile (32 rows x 8 chunks of 16 B)
@@ -539,12 +619,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
     }
   };
   auto store_tile = [&](int buf) {
-    __bf16* Qs = wsm + buf * (2 * 32 * RS);
+    __bf16* Qs = wsm + buf * (2 * TILE);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-      *reinterpret_cast<s16x8*>(Qs + row * RS + col) = qreg[j];
-      *reinterpret_cast<s16x8*>(Qs + 32 * RS + row * RS + col) = dreg[j];
+      *reinterpret_cast<s16x8*>(Qs + lds_idx(row, col)) = qreg[j];
+      *reinterpret_cast<s16x8*>(Qs + TILE + lds_idx(row, col)) = dreg[j];
     }
     if (lane < 32) { stats[wave][buf][0][lane] = lreg; stats[wave][buf][1][lane] = dlreg; }
   };
@@ -560,23 +640,30 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores of the current tile landed
     __builtin_amdgcn_wave_barrier();
     const int buf = i & 1;
-    const __bf16* Qs = wsm + buf * (2 * 32 * RS);
-    const __bf16* Ds = Qs + 32 * RS;
+    const __bf16* Qs = wsm + buf * (2 * TILE);
+    const __bf16* Ds = Qs + TILE;
     f32x16 s = {}, dp = {};
 #pragma unroll
     for (int ss = 0; ss < 4; ++ss) {
-      s = MFMA32(ld16(Qs + c32 * RS + 16 * ss + 8 * hl), kf[ss], s);
-      dp = MFMA32(ld16(Ds + c32 * RS + 16 * ss + 8 * hl), vf[ss], dp);
+      s = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], s);
+      dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
     }
     f32x16 ds;
-    const bool full = tile_full(g, qt, kb);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ql = acc_row(r, hl);
-      const int qs = qt * 32 + ql;
-      const float p = (full || allowed_st(g, qs, ks)) ? exp2f(s[r] * LOG2E - stats[wave][buf][0][ql]) : 0.f;
+      const float p = fast_exp2(fmaf(s[r], LOG2E, -stats[wave][buf][0][ql]));
       s[r] = p;
       ds[r] = p * (dp[r] - stats[wave][buf][1][ql]);
+    }
+    if (!tile_full(g, qt, kb)) {
+      const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool on = mask_bit(mh, r);
+        s[r] = on ? s[r] : 0.f;
+        ds[r] = on ? ds[r] : 0.f;
+      }
     }
     const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
     const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
@@ -593,15 +680,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
       store_tile(buf ^ 1);
     }
   }
-  // reduce the 4 waves' partial dK^T / dV^T through LDS (reuse the staging area: 4 x 64 x 64 floats)
+  // reduce the 4 waves' partial dK^T / dV^T through LDS (reuse the staging area: 4 waves x 64 values
+  // x 64 lanes floats = 64 KB), laid out value-major so consecutive lanes hit consecutive banks
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // 4 waves x 64 lanes x 64 values (16 KB... x4 = 64 KB)
+  float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    red[(wave * 64 + lane) * 64 + r] = dk0[r];
-    red[(wave * 64 + lane) * 64 + 16 + r] = dk1[r];
-    red[(wave * 64 + lane) * 64 + 32 + r] = dv0[r];
-    red[(wave * 64 + lane) * 64 + 48 + r] = dv1[r];
+    red[(wave * 64 + r) * 64 + lane] = dk0[r];
+    red[(wave * 64 + 16 + r) * 64 + lane] = dk1[r];
+    red[(wave * 64 + 32 + r) * 64 + lane] = dv0[r];
+    red[(wave * 64 + 48 + r) * 64 + lane] = dv1[r];
   }
   __syncthreads();
   if (wave == 0) {
@@ -618,8 +706,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
           fa[i] = fc[i] = 0.f;
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            fa[i] += red[(w * 64 + lane) * 64 + dt * 16 + r];
-            fc[i] += red[(w * 64 + lane) * 64 + 32 + dt * 16 + r];
+            fa[i] += red[(w * 64 + dt * 16 + r) * 64 + lane];
+            fc[i] += red[(w * 64 + 32 + dt * 16 + r) * 64 + lane];
           }
         }
         *reinterpret_cast<s16x4*>(kp + 32 * dt + 8 * gq + 4 * hl) = pack4(fa);

@@ -51,7 +51,42 @@ __global__ __launch_bounds__(256) void geglu_bwd_bias_kernel(const __bf16* __res
   const int j = (blockIdx.y * 256 + threadIdx.x) * 8;
   if (j >= F) return;
   float sa[8] = {}, sg[8] = {};
-  for (long r = blockIdx.x; r < M; r += gridDim.x) {
+  // U rows per iteration: all 3*U 16-byte loads are issued before any math (memory-level parallelism)
+  constexpr int U = 4;
+  const long step = gridDim.x;
+  long r = blockIdx.x;
+  for (; r + (U - 1) * step < M; r += U * step) {
+    s16x8 va[U], vg[U], vd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long rr = r + u * step;
+      va[u] = *reinterpret_cast<const s16x8*>(h + rr * 2 * F + j);
+      vg[u] = *reinterpret_cast<const s16x8*>(h + rr * 2 * F + F + j);
+      vd[u] = *reinterpret_cast<const s16x8*>(dout + rr * F + j);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long rr = r + u * step;
+      float a[8], gg[8], d[8], da[8], dg[8];
+      unpack8(va[u], a);
+      unpack8(vg[u], gg);
+      unpack8(vd[u], d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        da[i] = d[i] * gelu_erf(gg[i]);
+        dg[i] = d[i] * a[i] * gelu_erf_grad(gg[i]);
+      }
+      const s16x8 pa = pack8(da), pg = pack8(dg);
+      *reinterpret_cast<s16x8*>(dh + rr * 2 * F + j) = pa;
+      *reinterpret_cast<s16x8*>(dh + rr * 2 * F + F + j) = pg;
+      float ra[8], rg[8];
+      unpack8(pa, ra);  // bias grad of the values actually propagated (bf16), as a GEMM epilogue would
+      unpack8(pg, rg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sa[i] += ra[i]; sg[i] += rg[i]; }
+    }
+  }
+  for (; r < M; r += step) {
     float a[8], gg[8], d[8], da[8], dg[8];
     unpack8(*reinterpret_cast<const s16x8*>(h + r * 2 * F + j), a);
     unpack8(*reinterpret_cast<const s16x8*>(h + r * 2 * F + F + j), gg);
@@ -65,7 +100,7 @@ __global__ __launch_bounds__(256) void geglu_bwd_bias_kernel(const __bf16* __res
     *reinterpret_cast<s16x8*>(dh + r * 2 * F + j) = pa;
     *reinterpret_cast<s16x8*>(dh + r * 2 * F + F + j) = pg;
     float ra[8], rg[8];
-    unpack8(pa, ra);  // bias grad of the values actually propagated (bf16), as a GEMM epilogue would
+    unpack8(pa, ra);
     unpack8(pg, rg);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { sa[i] += ra[i]; sg[i] += rg[i]; }
@@ -182,7 +217,7 @@ void geglu_bwd(const void* h, const void* dout, void* dh, long M, int F, hipStre
   hipLaunchKernelGGL(geglu_bwd_kernel, dim3((t + 255) / 256), dim3(256), 0, st, (const __bf16*)h, (const __bf16*)dout,
                      (__bf16*)dh, M, F);
 }
-constexpr int GEGLU_ROW_BLOCKS = 256;
+constexpr int GEGLU_ROW_BLOCKS = 512;  // must match the partial buffer rows allocated in binding.cpp
 void geglu_bwd_bias(const void* h, const void* dout, void* dh, float* part, const GradSink& dbias, long M, int F,
                     hipStream_t st) {
   dim3 grid(GEGLU_ROW_BLOCKS, (F / 8 + 255) / 256);
