@@ -106,6 +106,18 @@ __device__ __forceinline__ bool tile_full(const AttnGeom& g, int qt, int kt) {
   return g.pattern == 0 && qt >= ntext && kt < qt;
 }
 
+// XCD-aware workgroup order (guide §1 "Workgroups, grid, and XCD partitioning"): the dispatcher
+// deals linear workgroup ids round-robin over the 8 XCDs, each with its own L2. Remap so every
+// workgroup of one (b, h) runs on the same XCD, consecutively: its K/V (or Q/dO) stay L2-resident.
+__device__ __forceinline__ void xcd_remap(int& grp, int& bh) {
+  const int ng = gridDim.x, BH = gridDim.y;
+  if (BH & 7) { grp = blockIdx.x; bh = blockIdx.y; return; }
+  const int L = blockIdx.x + blockIdx.y * ng;
+  const int x = L & 7, j = L >> 3;
+  bh = x + 8 * (j / ng);
+  grp = j - (j / ng) * ng;
+}
+
 // first local (image) key tile needed by image query block qb
 __device__ __forceinline__ int local_lo_tile(const AttnGeom& g, int qb) {
   const int kq0 = qb * 32 - g.Tp;
@@ -173,33 +185,101 @@ __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r 
 // it by more than this, so P <= 2^8 (exact in bf16's relative precision; fp32 sums have headroom).
 constexpr float RESCALE_THR = 8.0f;
 
+// max of x over the lane and its partner in the other 32-lane half (v_permlane32_swap, no LDS)
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Online-softmax state of one wave (32 queries on the lanes, keys on the accumulator rows).
+struct SoftmaxState {
+  float m = NEG_BIG;  // running max of RAW scores (q carries 1/sqrt(d))
+  float lsum = 0.f;   // this lane half's partial row sum
+  f32x16 o0 = {}, o1 = {};
+};
+
+// S^T tile(s) of one wave -> masked -> online update -> P^T (bf16) -> O^T += V^T P^T.
+// NT key tiles at once (independent MFMA chains and one rescale decision for all of them).
+template <int NT>
+__device__ __forceinline__ void fwd_tiles(SoftmaxState& st, const __bf16* const (&Ks)[NT], const __bf16* const (&Vs)[NT],
+                                          const int (&kt)[NT], const bf16x8 (&qf)[4], const AttnGeom& g, int qb, int qs,
+                                          int lane) {
+  const int hl = lane >> 5, c32 = lane & 31;
+  constexpr float THR_RAW = RESCALE_THR / LOG2E;
+  f32x16 s[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    s[j] = f32x16{};
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) s[j] = MFMA32(row_operand(Ks[j], ss, c32, hl), qf[ss], s[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    if (!tile_full(g, qb, kt[j])) {
+      const uint32_t mh = key_mask(g, qs, kt[j]) >> (4 * hl);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[j][r] = mask_bit(mh, r) ? s[j][r] : NEG_BIG;
+    }
+  }
+  float mt = NEG_BIG;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) mt = fmaxf(fmaxf(mt, s[j][r]), s[j][r + 1]);
+  mt = half_max(mt);
+  if (!__all(mt <= st.m + THR_RAW)) {
+    const float mnew = fmaxf(st.m, mt);
+    const float alpha = fast_exp2((st.m - mnew) * LOG2E);
+    st.m = mnew;
+    st.lsum *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { st.o0[r] *= alpha; st.o1[r] *= alpha; }
+  }
+  const float mc = st.m * LOG2E;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fast_exp2(fmaf(s[j][r], LOG2E, -mc));
+      s[j][r] = p;
+      ps += p;
+    }
+    st.lsum += ps;
+    const bf16x8 p0 = cvt8(s[j], 0), p1 = cvt8(s[j], 8);
+    st.o0 = MFMA32(tr_operand(Vs[j], 0, 0, lane), p0, st.o0);
+    st.o0 = MFMA32(tr_operand(Vs[j], 1, 0, lane), p1, st.o0);
+    st.o1 = MFMA32(tr_operand(Vs[j], 0, 1, lane), p0, st.o1);
+    st.o1 = MFMA32(tr_operand(Vs[j], 1, 1, lane), p1, st.o1);
+  }
+}
+
+// Forward. Workgroup = 4 waves = 4 consecutive 32-query blocks of one (b, h).
+// Phase A (shared): the text key tiles every block needs, staged cooperatively two tiles per step
+//   (double-buffered 2 x {Ka, Kb, Va, Vb}, register-staged loads issued before compute, T14).
+// Phase B (wave-private): each image query block streams ITS OWN local key tiles through a private
+//   LDS slot (reusing phase A's buffers) -- no workgroup barrier, no wave idling on other blocks' tiles.
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                           const __bf16* __restrict__ V, __bf16* __restrict__ out,
                                                           float* __restrict__ lse, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
-  const int bh = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
+  int grp, bh;
+  xcd_remap(grp, bh);
   const int b = bh / g.H, h = bh - b * g.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
-  const int qb0 = blockIdx.x * 4;
+  const int qb0 = grp * 4;
   const int qb = qb0 + wave;
   const int qb_last = min(qb0 + 3, nqb - 1);
   const bool active = qb < nqb;
   const size_t base = (size_t)bh * g.Np * 64;
 
-  // union of key tiles of the workgroup
-  const int u_text_end = qb_last < ntext ? qb_last + 1 : ntext;
-  const int first_img_qb = max(qb0, ntext);
-  const int u_loc_lo = (qb_last >= ntext) ? local_lo_tile(g, first_img_qb) : 0;
-  const int n_loc = (qb_last >= ntext) ? (qb_last - u_loc_lo + 1) : 0;
-  const int ntiles = u_text_end + n_loc;
-  // this wave's ranges
-  int my_text_end = 0, my_lo = 1, my_hi = 0;
-  if (active) {
-    if (qb < ntext) my_text_end = qb + 1;
-    else { my_text_end = ntext; my_lo = local_lo_tile(g, qb); my_hi = qb; }
-  }
-
+  const int n_text = qb_last < ntext ? qb_last + 1 : ntext;  // text tiles of the workgroup union
+  const int my_text_end = active ? min(qb + 1, ntext) : 0;
   const int qs = qb * 32 + c32;
   bf16x8 qf[4];
   {
@@ -207,93 +287,94 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restri
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = ld16(qp + 16 * s);
   }
+  SoftmaxState st;
 
-  // staging: each thread moves one 16-B chunk of K and of V per tile (swizzled image)
+  // ---- phase A: shared text tiles, two per step ----
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
   const int st_off = lds_idx(st_row, st_col);
-  auto tile_id = [&](int t) { return t < u_text_end ? t : u_loc_lo + (t - u_text_end); };
-  s16x8 kreg, vreg;
-  {
-    const int t0 = tile_id(0);
-    const size_t off = base + (size_t)(t0 * 32 + st_row) * 64 + st_col;
-    kreg = *reinterpret_cast<const s16x8*>(Kt + off);
-    vreg = *reinterpret_cast<const s16x8*>(V + off);
-    *reinterpret_cast<s16x8*>(smem + st_off) = kreg;
-    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = vreg;
-  }
+  const int npairs = (n_text + 1) >> 1;
+  s16x8 sreg[4];  // Ka, Kb, Va, Vb chunks of this thread
+  auto load_pair = [&](int pi) {
+    const int ta = 2 * pi, tb = min(2 * pi + 1, n_text - 1);
+    const size_t oa = base + (size_t)(ta * 32 + st_row) * 64 + st_col;
+    const size_t ob = base + (size_t)(tb * 32 + st_row) * 64 + st_col;
+    sreg[0] = *reinterpret_cast<const s16x8*>(Kt + oa);
+    sreg[1] = *reinterpret_cast<const s16x8*>(Kt + ob);
+    sreg[2] = *reinterpret_cast<const s16x8*>(V + oa);
+    sreg[3] = *reinterpret_cast<const s16x8*>(V + ob);
+  };
+  auto store_pair = [&](int buf) {
+    __bf16* S0 = smem + buf * (4 * TILE);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<s16x8*>(S0 + i * TILE + st_off) = sreg[i];
+  };
+  load_pair(0);
+  store_pair(0);
   __syncthreads();
-
-  // m: running max of the RAW scores (q carries 1/sqrt(d)); p = 2^(s*log2e - m*log2e) via one fma
-  float m = NEG_BIG, lsum = 0.f;
-  f32x16 o0 = {}, o1 = {};
-  constexpr float THR_RAW = RESCALE_THR / LOG2E;
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int tile = tile_id(t);
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      const size_t off = base + (size_t)(tile_id(t + 1) * 32 + st_row) * 64 + st_col;
-      kreg = *reinterpret_cast<const s16x8*>(Kt + off);
-      vreg = *reinterpret_cast<const s16x8*>(V + off);
+  for (int pi = 0; pi < npairs; ++pi) {
+    const bool more = pi + 1 < npairs;
+    if (more) load_pair(pi + 1);
+    const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
+    const int ta = 2 * pi, tb = 2 * pi + 1;
+    if (tb < my_text_end) {
+      const __bf16* const Ks[2] = {S0, S0 + TILE};
+      const __bf16* const Vs[2] = {S0 + 2 * TILE, S0 + 3 * TILE};
+      const int kt[2] = {ta, tb};
+      fwd_tiles<2>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
+    } else if (ta < my_text_end) {
+      const __bf16* const Ks[1] = {S0};
+      const __bf16* const Vs[1] = {S0 + 2 * TILE};
+      const int kt[1] = {ta};
+      fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
-    const __bf16* Ks = smem + (t & 1) * (2 * TILE);
-    const __bf16* Vs = Ks + TILE;
-    const bool need = (tile < my_text_end) || (tile >= my_lo && tile <= my_hi);
-    if (need) {
-      f32x16 s = {};
-#pragma unroll
-      for (int ss = 0; ss < 4; ++ss) s = MFMA32(row_operand(Ks, ss, c32, hl), qf[ss], s);
-      if (!tile_full(g, qb, tile)) {
-        const uint32_t mh = key_mask(g, qs, tile) >> (4 * hl);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = mask_bit(mh, r) ? s[r] : NEG_BIG;
-      }
-      float mt = fmaxf(fmaxf(s[0], s[1]), s[2]);
-#pragma unroll
-      for (int r = 3; r < 15; r += 2) mt = fmaxf(fmaxf(mt, s[r]), s[r + 1]);
-      mt = fmaxf(mt, s[15]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      if (!__all(mt <= m + THR_RAW)) {
-        const float mnew = fmaxf(m, mt);
-        const float alpha = fast_exp2((m - mnew) * LOG2E);
-        m = mnew;
-        lsum *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-      }
-      const float mc = m * LOG2E;
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(fmaf(s[r], LOG2E, -mc));
-        s[r] = p;
-        ps += p;
-      }
-      lsum += ps;
-      const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
-      o0 = MFMA32(tr_operand(Vs, 0, 0, lane), p0, o0);
-      o0 = MFMA32(tr_operand(Vs, 1, 0, lane), p1, o0);
-      o1 = MFMA32(tr_operand(Vs, 0, 1, lane), p0, o1);
-      o1 = MFMA32(tr_operand(Vs, 1, 1, lane), p1, o1);
-    }
-    if (more) {
-      __bf16* Kn = smem + ((t + 1) & 1) * (2 * TILE);
-      *reinterpret_cast<s16x8*>(Kn + st_off) = kreg;
-      *reinterpret_cast<s16x8*>(Kn + TILE + st_off) = vreg;
-    }
+    if (more) store_pair((pi + 1) & 1);
     __syncthreads();
   }
 
+  // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
+  if (active && qb >= ntext) {
+    __bf16* P = smem + wave * (2 * TILE);
+    const int lo = local_lo_tile(g, qb);
+    s16x8 kr[4], vr[4];
+    auto load_loc = [&](int t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+        const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
+        kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
+        vr[j] = *reinterpret_cast<const s16x8*>(V + off);
+      }
+    };
+    load_loc(lo);
+    for (int t = lo; t <= qb; ++t) {
+      // the previous tile's LDS reads were consumed by its MFMAs (in program order before these stores)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+        *reinterpret_cast<s16x8*>(P + lds_idx(row, col)) = kr[j];
+        *reinterpret_cast<s16x8*>(P + TILE + lds_idx(row, col)) = vr[j];
+      }
+      if (t < qb) load_loc(t + 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stores landed before any lane reads them
+      __builtin_amdgcn_wave_barrier();
+      const __bf16* const Ks[1] = {P};
+      const __bf16* const Vs[1] = {P + TILE};
+      const int kt[1] = {t};
+      fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+
   if (!active) return;
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float ltot = half_sum(st.lsum);
   const float inv = 1.0f / ltot;
-  lse[(size_t)bh * g.Np + qs] = m * LOG2E + log2f(ltot);
+  lse[(size_t)bh * g.Np + qs] = st.m * LOG2E + log2f(ltot);
   const int p = st2seq(g, qs);
   if (p < 0) return;
   __bf16* op = out + ((size_t)b * g.n + p) * (g.H * 64) + h * 64;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
-    const f32x16& o = dt ? o1 : o0;
+    const f32x16& o = dt ? st.o1 : st.o0;
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
       float f[4];
@@ -343,10 +424,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
                                                              __bf16* __restrict__ dQ, AttnGeom g) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
-  const int bh = blockIdx.y;
+  int grp, bh;
+  xcd_remap(grp, bh);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
-  const int qb0 = blockIdx.x * 4;
+  const int qb0 = grp * 4;
   const int qb = qb0 + wave;
   const int qb_last = min(qb0 + 3, nqb - 1);
   const bool active = qb < nqb;
@@ -443,118 +525,97 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
 }
 
 // ------------------------------------------------------------------------------------------------
-// Backward dK / dV (key-centric)
+// Backward dK / dV for the IMAGE key blocks (key-centric, no float atomics). Image keys are seen only
+// by the few query tiles of their local pattern (axial: the key's own row tile; conv_like: the next
+// K row tiles; full: every later tile), so each wave owns one 32-key block and streams ITS OWN query
+// tiles {Q, dO, lse, delta} through a private LDS slot (register prefetch one tile ahead): no
+// workgroup barrier and no wave idling on the other blocks' tiles.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                                const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                const float* __restrict__ lse, const float* __restrict__ delta,
                                                                __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
-  __shared__ float stats[2][2][32];
-  const int bh = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * TILE];  // per wave {Q, dO}
+  __shared__ float stats[4][2][32];                                   // per wave {lse, delta}
+  int grp, bh;
+  xcd_remap(grp, bh);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nkb = g.Np >> 5, ntext = g.Tp >> 5;
-  // image (local) key blocks only: text key blocks go to attn_bwd_dkdv_text_kernel
-  const int kb0 = ntext + blockIdx.x * 4;
-  const int kb = kb0 + wave;
-  const int kb_last = min(kb0 + 3, nkb - 1);
-  const bool active = kb < nkb;
+  const int kb = ntext + grp * 4 + wave;
+  if (kb >= nkb) return;  // wave-uniform; no workgroup barrier below
   const size_t base = (size_t)bh * g.Np * 64;
-
-  auto hi_of = [&](int k) { return k < ntext ? nkb - 1 : local_hi_qtile(g, k); };
-  const int q_lo = kb0;
-  const int q_hi = hi_of(kb_last) > hi_of(kb0) ? hi_of(kb_last) : hi_of(kb0);
-  int u_hi = q_hi;
-  for (int k = kb0; k <= kb_last; ++k) u_hi = max(u_hi, hi_of(k));
-  const int ntiles = u_hi - q_lo + 1;
-  const int my_hi = active ? hi_of(kb) : -1;
-
   const int ks = kb * 32 + c32;
-  const int krow = active ? ks : 0;
+  const int q_hi = local_hi_qtile(g, kb);
   bf16x8 kf[4], vf[4];
   {
-    const __bf16* kp = Kt + base + (size_t)krow * 64 + 8 * hl;
-    const __bf16* vp = V + base + (size_t)krow * 64 + 8 * hl;
+    const __bf16* kp = Kt + base + (size_t)ks * 64 + 8 * hl;
+    const __bf16* vp = V + base + (size_t)ks * 64 + 8 * hl;
 #pragma unroll
     for (int s = 0; s < 4; ++s) { kf[s] = ld16(kp + 16 * s); vf[s] = ld16(vp + 16 * s); }
   }
-
-  const int st_row = tid >> 3, st_col = (tid & 7) * 8;
-  const int st_off = lds_idx(st_row, st_col);
-  s16x8 qreg, doreg;
-  float lreg = 0.f, dreg = 0.f;
-  {
-    const size_t off = base + (size_t)(q_lo * 32 + st_row) * 64 + st_col;
-    qreg = *reinterpret_cast<const s16x8*>(Q + off);
-    doreg = *reinterpret_cast<const s16x8*>(dO + off);
-    *reinterpret_cast<s16x8*>(smem + st_off) = qreg;
-    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = doreg;
-    if (tid < 32) stats[0][0][tid] = lse[(size_t)bh * g.Np + q_lo * 32 + tid];
-    else if (tid < 64) stats[0][1][tid - 32] = delta[(size_t)bh * g.Np + q_lo * 32 + tid - 32];
-  }
-  __syncthreads();
-
-  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
-  for (int t = 0; t < ntiles; ++t) {
-    const int qt = q_lo + t;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      const size_t off = base + (size_t)((qt + 1) * 32 + st_row) * 64 + st_col;
-      qreg = *reinterpret_cast<const s16x8*>(Q + off);
-      doreg = *reinterpret_cast<const s16x8*>(dO + off);
-      if (tid < 32) lreg = lse[(size_t)bh * g.Np + (qt + 1) * 32 + tid];
-      else if (tid < 64) dreg = delta[(size_t)bh * g.Np + (qt + 1) * 32 + tid - 32];
-    }
-    const int buf = t & 1;
-    const __bf16* Qs = smem + buf * (2 * TILE);
-    const __bf16* Ds = Qs + TILE;
-    const bool need = active && qt >= kb && qt <= my_hi;
-    if (need) {
-      f32x16 s = {}, dp = {};
+  __bf16* Qs = smem + wave * (2 * TILE);
+  __bf16* Ds = Qs + TILE;
+  s16x8 qr[4], dr[4];
+  float sv = 0.f;
+  auto load_tile = [&](int qt) {
 #pragma unroll
-      for (int ss = 0; ss < 4; ++ss) {
-        s = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], s);
-        dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
-      }
-      f32x16 ds;
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      const size_t off = base + (size_t)(qt * 32 + row) * 64 + col;
+      qr[j] = *reinterpret_cast<const s16x8*>(Q + off);
+      dr[j] = *reinterpret_cast<const s16x8*>(dO + off);
+    }
+    sv = (hl ? delta : lse)[(size_t)bh * g.Np + qt * 32 + c32];
+  };
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  load_tile(kb);
+  for (int qt = kb; qt <= q_hi; ++qt) {
+    // this tile's LDS image (the previous tile's reads were consumed by its MFMAs, earlier in order)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<s16x8*>(Qs + lds_idx(row, col)) = qr[j];
+      *reinterpret_cast<s16x8*>(Ds + lds_idx(row, col)) = dr[j];
+    }
+    stats[wave][hl][c32] = sv;
+    if (qt < q_hi) load_tile(qt + 1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    f32x16 sc = {}, dp = {};
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) {
+      sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
+      dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
+    }
+    f32x16 ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = acc_row(r, hl);
+      const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[wave][0][ql]));
+      sc[r] = pr;
+      ds[r] = pr * (dp[r] - stats[wave][1][ql]);
+    }
+    if (!tile_full(g, qt, kb)) {
+      const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int ql = acc_row(r, hl);
-        const float p = fast_exp2(fmaf(s[r], LOG2E, -stats[buf][0][ql]));
-        s[r] = p;
-        ds[r] = p * (dp[r] - stats[buf][1][ql]);
+        const bool on = mask_bit(mh, r);
+        sc[r] = on ? sc[r] : 0.f;
+        ds[r] = on ? ds[r] : 0.f;
       }
-      if (!tile_full(g, qt, kb)) {
-        const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool on = mask_bit(mh, r);
-          s[r] = on ? s[r] : 0.f;
-          ds[r] = on ? ds[r] : 0.f;
-        }
-      }
-      const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
-      const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
-      dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
-      dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
-      dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
-      dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
-      dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
-      dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
-      dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
-      dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
     }
-    if (more) {
-      const int nb = (t + 1) & 1;
-      __bf16* Qn = smem + nb * (2 * TILE);
-      *reinterpret_cast<s16x8*>(Qn + st_off) = qreg;
-      *reinterpret_cast<s16x8*>(Qn + TILE + st_off) = doreg;
-      if (tid < 32) stats[nb][0][tid] = lreg;
-      else if (tid < 64) stats[nb][1][tid - 32] = dreg;
-    }
-    __syncthreads();
+    const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
+    const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
+    dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
+    dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
+    dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
+    dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
+    dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
+    dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
+    dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
+    dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
+    __builtin_amdgcn_wave_barrier();
   }
-  if (!active) return;
   __bf16* kp = dK + base + (size_t)ks * 64;
   __bf16* vp = dV + base + (size_t)ks * 64;
 #pragma unroll
@@ -573,142 +634,148 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
 }
 
 // ------------------------------------------------------------------------------------------------
-// Backward dK / dV for the TEXT key blocks: every later query tile (all image queries see all
-// text keys) attends to them, so one workgroup owns ONE 32-key block and its 4 waves split the
-// query tiles round-robin (balanced; 4x shorter critical path than one wave per key block). Each
-// wave stages its own Q/dO tile (wave-private double buffer, register prefetch one tile ahead);
-// the four partial dK/dV accumulators are summed through LDS at the end.
+// Backward dK / dV for the TEXT key blocks: every later query tile (all image queries see all text
+// keys) attends to them. One workgroup owns TWO 32-key blocks; wave w handles key block kb0 + (w&1)
+// over the query tiles of parity (w>>1). Each step stages two query tiles {Q, dO} (one per parity)
+// cooperatively, so every staged tile serves two key blocks (half the Q/dO traffic of one block per
+// workgroup) while the critical path stays at half the query tiles. The two parity partials of each
+// key block are summed through LDS at the end (fixed order, deterministic).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                                     const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                                     __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
-  // per wave: 2 buffers x {Q, dO} tile images   +  2 buffers x {lse, delta} x 32
-  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * 2 * TILE];
-  __shared__ float stats[4][2][2][32];
-  const int bh = blockIdx.y;
+  // 2 stages x 2 parities x {Q, dO} tile images (32 KB) + the per-query stats
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 2 * TILE];
+  __shared__ float stats[2][2][2][32];  // [stage][parity][lse | delta][row]
+  int grp, bh;
+  xcd_remap(grp, bh);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
-  const int nqb = g.Np >> 5;
-  const int kb = blockIdx.x;
+  const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
+  const int kb0 = grp * 2;
+  const int kb = kb0 + (wave & 1), par = wave >> 1;
+  const bool active = kb < ntext;
   const size_t base = (size_t)bh * g.Np * 64;
   const int ks = kb * 32 + c32;
   bf16x8 kf[4], vf[4];
   {
-    const __bf16* kp = Kt + base + (size_t)ks * 64 + 8 * hl;
-    const __bf16* vp = V + base + (size_t)ks * 64 + 8 * hl;
+    const int krow = active ? ks : 0;
+    const __bf16* kp = Kt + base + (size_t)krow * 64 + 8 * hl;
+    const __bf16* vp = V + base + (size_t)krow * 64 + 8 * hl;
 #pragma unroll
     for (int s = 0; s < 4; ++s) { kf[s] = ld16(kp + 16 * s); vf[s] = ld16(vp + 16 * s); }
   }
-  __bf16* wsm = smem + wave * (2 * 2 * TILE);
-  const int first = kb + wave;
-  const int ntiles = first < nqb ? (nqb - first + 3) / 4 : 0;
-  // lane-private staging: 4 chunks of Q and 4 of dO per tile (32 rows x 8 chunks of 16 B)
-  s16x8 qreg[4], dreg[4];
-  float lreg = 0.f, dlreg = 0.f;
-  auto load_tile = [&](int qt) {
+  // query tiles kb0 .. nqb-1, two per step (parity 0: kb0 + 2i, parity 1: kb0 + 2i + 1)
+  const int nsteps = (nqb - kb0 + 1) >> 1;
+  // staging: thread tid moves chunk (row, col) of Q and dO of both parity tiles
+  const int st_row = (tid & 255) >> 3, st_col = (tid & 7) * 8;
+  const int st_off = lds_idx(st_row, st_col);
+  s16x8 sreg[4];  // Q0, dO0, Q1, dO1
+  float sl = 0.f, sd = 0.f;
+  auto load_step = [&](int i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-      const size_t off = base + (size_t)(qt * 32 + row) * 64 + col;
-      qreg[j] = *reinterpret_cast<const s16x8*>(Q + off);
-      dreg[j] = *reinterpret_cast<const s16x8*>(dO + off);
+    for (int pp = 0; pp < 2; ++pp) {
+      const int qt = min(kb0 + 2 * i + pp, nqb - 1);
+      const size_t off = base + (size_t)(qt * 32 + st_row) * 64 + st_col;
+      sreg[2 * pp] = *reinterpret_cast<const s16x8*>(Q + off);
+      sreg[2 * pp + 1] = *reinterpret_cast<const s16x8*>(dO + off);
     }
-    if (lane < 32) {
-      lreg = lse[(size_t)bh * g.Np + qt * 32 + lane];
-      dlreg = delta[(size_t)bh * g.Np + qt * 32 + lane];
+    if (tid < 128) {  // lse / delta rows of both tiles: 2 parities x 2 stats x 32
+      const int pp = tid >> 6, which = (tid >> 5) & 1, r = tid & 31;
+      const int qt = min(kb0 + 2 * i + pp, nqb - 1);
+      const float* src = which ? delta : lse;
+      sl = src[(size_t)bh * g.Np + qt * 32 + r];
     }
   };
-  auto store_tile = [&](int buf) {
-    __bf16* Qs = wsm + buf * (2 * TILE);
+  auto store_step = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-      *reinterpret_cast<s16x8*>(Qs + lds_idx(row, col)) = qreg[j];
-      *reinterpret_cast<s16x8*>(Qs + TILE + lds_idx(row, col)) = dreg[j];
+    for (int pp = 0; pp < 2; ++pp) {
+      __bf16* T0 = smem + (buf * 2 + pp) * (2 * TILE);
+      *reinterpret_cast<s16x8*>(T0 + st_off) = sreg[2 * pp];
+      *reinterpret_cast<s16x8*>(T0 + TILE + st_off) = sreg[2 * pp + 1];
     }
-    if (lane < 32) { stats[wave][buf][0][lane] = lreg; stats[wave][buf][1][lane] = dlreg; }
+    if (tid < 128) stats[buf][tid >> 6][(tid >> 5) & 1][tid & 31] = sl;
   };
+  (void)sd;
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
-  if (ntiles > 0) {
-    load_tile(first);
-    store_tile(0);
+  if (nsteps > 0) {
+    load_step(0);
+    store_step(0);
   }
-  for (int i = 0; i < ntiles; ++i) {
-    const int qt = first + 4 * i;
-    const bool more = i + 1 < ntiles;
-    if (more) load_tile(qt + 4);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores of the current tile landed
-    __builtin_amdgcn_wave_barrier();
+  __syncthreads();
+  for (int i = 0; i < nsteps; ++i) {
+    const bool more = i + 1 < nsteps;
+    if (more) load_step(i + 1);
     const int buf = i & 1;
-    const __bf16* Qs = wsm + buf * (2 * TILE);
-    const __bf16* Ds = Qs + TILE;
-    f32x16 s = {}, dp = {};
+    const int qt = kb0 + 2 * i + par;
+    if (active && qt < nqb && qt >= kb) {
+      const __bf16* Qs = smem + (buf * 2 + par) * (2 * TILE);
+      const __bf16* Ds = Qs + TILE;
+      f32x16 sc = {}, dp = {};
 #pragma unroll
-    for (int ss = 0; ss < 4; ++ss) {
-      s = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], s);
-      dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
-    }
-    f32x16 ds;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ql = acc_row(r, hl);
-      const float p = fast_exp2(fmaf(s[r], LOG2E, -stats[wave][buf][0][ql]));
-      s[r] = p;
-      ds[r] = p * (dp[r] - stats[wave][buf][1][ql]);
-    }
-    if (!tile_full(g, qt, kb)) {
-      const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+      for (int ss = 0; ss < 4; ++ss) {
+        sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
+        dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
+      }
+      f32x16 ds;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const bool on = mask_bit(mh, r);
-        s[r] = on ? s[r] : 0.f;
-        ds[r] = on ? ds[r] : 0.f;
+        const int ql = acc_row(r, hl);
+        const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[buf][par][0][ql]));
+        sc[r] = pr;
+        ds[r] = pr * (dp[r] - stats[buf][par][1][ql]);
       }
-    }
-    const bf16x8 p0 = cvt8(s, 0), p1 = cvt8(s, 8);
-    const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
-    dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
-    dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
-    dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
-    dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
-    dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
-    dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
-    dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
-    dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
-    if (more) {
-      __builtin_amdgcn_wave_barrier();  // every lane finished reading the other buffer (tile i-1)
-      store_tile(buf ^ 1);
-    }
-  }
-  // reduce the 4 waves' partial dK^T / dV^T through LDS (reuse the staging area: 4 waves x 64 values
-  // x 64 lanes floats = 64 KB), laid out value-major so consecutive lanes hit consecutive banks
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);
+      if (!tile_full(g, qt, kb)) {
+        const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    red[(wave * 64 + r) * 64 + lane] = dk0[r];
-    red[(wave * 64 + 16 + r) * 64 + lane] = dk1[r];
-    red[(wave * 64 + 32 + r) * 64 + lane] = dv0[r];
-    red[(wave * 64 + 48 + r) * 64 + lane] = dv1[r];
+        for (int r = 0; r < 16; ++r) {
+          const bool on = mask_bit(mh, r);
+          sc[r] = on ? sc[r] : 0.f;
+          ds[r] = on ? ds[r] : 0.f;
+        }
+      }
+      const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
+      const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
+      dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
+      dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
+      dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
+      dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
+      dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
+      dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
+      dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
+      dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
+    }
+    if (more) store_step((i + 1) & 1);
+    __syncthreads();
+  }
+  // parity 1 waves hand their partials to the parity 0 wave of the same key block through LDS
+  // (value-major layout: consecutive lanes on consecutive banks), which sums and stores
+  float* red = reinterpret_cast<float*>(smem);  // 2 key blocks x 64 values x 64 lanes floats = 32 KB
+  if (par == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      red[((wave & 1) * 64 + r) * 64 + lane] = dk0[r];
+      red[((wave & 1) * 64 + 16 + r) * 64 + lane] = dk1[r];
+      red[((wave & 1) * 64 + 32 + r) * 64 + lane] = dv0[r];
+      red[((wave & 1) * 64 + 48 + r) * 64 + lane] = dv1[r];
+    }
   }
   __syncthreads();
-  if (wave == 0) {
+  if (par == 0 && active) {
     __bf16* kp = dK + base + (size_t)ks * 64;
     __bf16* vp = dV + base + (size_t)ks * 64;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
+      const f32x16& a = dt ? dk1 : dk0;
+      const f32x16& c = dt ? dv1 : dv0;
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         float fa[4], fc[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * gq + i;
-          fa[i] = fc[i] = 0.f;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            fa[i] += red[(w * 64 + dt * 16 + r) * 64 + lane];
-            fc[i] += red[(w * 64 + 32 + dt * 16 + r) * 64 + lane];
-          }
+          fa[i] = a[r] + red[((wave & 1) * 64 + dt * 16 + r) * 64 + lane];
+          fc[i] = c[r] + red[((wave & 1) * 64 + 32 + dt * 16 + r) * 64 + lane];
         }
         *reinterpret_cast<s16x4*>(kp + 32 * dt + 8 * gq + 4 * hl) = pack4(fa);
         *reinterpret_cast<s16x4*>(vp + 32 * dt + 8 * gq + 4 * hl) = pack4(fc);
@@ -736,7 +803,7 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
                      (const __bf16*)do_st, lse, delta, (__bf16*)dq, g);
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
   // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
-  hipLaunchKernelGGL(attn_bwd_dkdv_text_kernel, dim3(ntext, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+  hipLaunchKernelGGL(attn_bwd_dkdv_text_kernel, dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
                      (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
   // image key blocks (short, local patterns): four blocks per workgroup
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((nimg + 3) / 4, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
