@@ -133,6 +133,12 @@ class BasePeerArguments:
         metadata={"help": "Visible multiaddrs the host announces for external connections"},
     )
     identity_path: Optional[str] = field(default=None, metadata={"help": "File holding this peer's persistent id"})
+    elastic_coordinator: Optional[str] = field(
+        default=None,
+        metadata={"help": "host:port of the elastic coordinator store (hosted by run_aux_peer.py "
+                          "--host_elastic_coordinator True). When set, trainers form their communicator through "
+                          "it and survive peer death / admit late joiners (SURVEY 5.3)"},
+    )
 
 
 @dataclass
@@ -171,6 +177,8 @@ class AuxiliaryPeerArguments(BasePeerArguments):
         default=None, metadata={"help": "Frequency (in seconds) of uploading the model to Hub"}
     )
     store_checkpoints: bool = field(default=True, metadata={"help": "If True, enables CheckpointHandler"})
+    host_elastic_coordinator: bool = field(
+        default=False, metadata={"help": "Host the elastic coordinator store at --elastic_coordinator host:port"})
     assist_in_averaging: bool = field(
         default=False, metadata={"help": "If True, this peer will facilitate averaging for other (training) peers"})
     assist_refresh: float = field(default=1.0, metadata={"help": "Period (in seconds) for tryin to assist averaging"})

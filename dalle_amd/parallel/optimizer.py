@@ -233,7 +233,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                  state_averaging_compression: Optional[CompressionBase] = None, average_state_every: int = 1,
                  client_mode: bool = False, auxiliary: bool = False, verbose: bool = False, process_group=None,
                  arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "collective",
-                 device=None, **kwargs):
+                 device=None, elastic=None, **kwargs):
         self.dht, self.run_id = dht, run_id
         self.target_batch_size = target_batch_size
         self.batch_size_per_step = batch_size_per_step
@@ -243,6 +243,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         self.client_mode, self.auxiliary, self.verbose = client_mode, auxiliary, verbose
         self.group = process_group
         self.arena = arena
+        self.elastic = elastic  # ElasticGroup: survive peer death / admit joiners
 
         param_groups = list(params)
         if param_groups and isinstance(param_groups[0], dict):
@@ -325,19 +326,52 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if bs is None:
             raise ValueError("batch_size_per_step (ctor) or batch_size (step) is required")
         self.grad_averager.accumulate_grads_(bs)
+        if self.elastic is None:
+            self._collective_part(grad_scaler)
+            return loss
+        try:
+            self._collective_part(grad_scaler)
+            if not self.grad_averager.last_averaging_ok:
+                raise RuntimeError("gradient averaging failed")
+        except Exception as e:  # noqa: BLE001 - a member died / timed out: re-form the group and go on
+            logger.warning(f"{self.run_id}: collective failure ({e!r}); regrouping")
+            self._regroup()
+        return loss
+
+    def _collective_part(self, grad_scaler):
         self.tracker.report_local_progress(self.local_epoch, self.grad_averager.local_samples_accumulated)
         if self.tracker.max_epoch_seen > self.local_epoch + 1:
             logger.info(f"local epoch {self.local_epoch} lags the collaboration ({self.tracker.max_epoch_seen}); loading state")
             self.load_state_from_peers()
             self.grad_averager.reset_accumulated_grads_()
-            return loss
+            return
         if self.tracker.ready_to_update_epoch:
-            self._update_global_epoch()
-        return loss
+            self._update_global_epoch(grad_scaler)
+            if self.elastic is not None and self.elastic.poll_join():
+                logger.info(f"{self.run_id}: a peer asked to join; regrouping at epoch {self.local_epoch}")
+                self._regroup()
 
-    def _update_global_epoch(self):
+    def _regroup(self):
+        """New communicator over the live members, then one donor brings everyone (joiners, or
+        survivors whose last step fell back to local gradients) to the same state."""
+        self.elastic.regroup()
+        self.grad_averager._shards = None
+        self.grad_averager.last_averaging_ok = True
+        self.load_state_from_peers()
+
+    def _update_global_epoch(self, grad_scaler=None):
         t0 = time.perf_counter()
         total = self.tracker.global_progress.samples_accumulated
+        if grad_scaler is not None and grad_scaler.is_enabled():
+            # deferred AMP unscale + collaboration-wide overflow check (D28): skip the whole update
+            # (and the averaging round) if any peer's accumulated grads overflowed
+            flat = self.arena.grad if (self.arena is not None and self.grad_averager.reuse_grad_buffers) else None
+            if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group):
+                logger.warning(f"{self.run_id}: non-finite scaled gradients at epoch {self.local_epoch}; skipping update")
+                self.grad_averager.reset_accumulated_grads_()
+                self.tracker.update_epoch(self.local_epoch + 1)
+                self.local_epoch = self.local_epoch + 1
+                return
         self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
         self.state_averager.step(optimizer_step=True, averaging_round=True)
         faults.after_update(self.local_epoch, self._params)

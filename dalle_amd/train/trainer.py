@@ -127,8 +127,13 @@ class CollaborativeHFTrainer:
         self.model = IgnoreGradManipulations(model, override_zero_grad=reuse)
         self.state = TrainerState()
         self.control = TrainerControl()
+        self.grad_scaler = None
         if getattr(args, "fp16", False):
-            logger.warning("--fp16 requested: the MI355X engine computes in bf16 (no loss scaler needed)")
+            # reference: HivemindGradScaler under --fp16 (D28). The MI355X engine computes in bf16, but the
+            # deferred collaborative scaler keeps the flag's semantics (scale, global-step unscale/skip).
+            from ..optim.grad_scaler import CollaborativeGradScaler
+            self.grad_scaler = CollaborativeGradScaler()
+            logger.info("--fp16: loss scaling with the collaborative (global-step deferred) grad scaler")
 
     def remove_callback(self, cb_type):
         self.callbacks = [c for c in self.callbacks if not (isinstance(c, cb_type) if isinstance(cb_type, type) else c is cb_type)]
@@ -175,10 +180,14 @@ class CollaborativeHFTrainer:
                 batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
                 out = self.model(**batch)
                 loss = out["loss"] / accum
-                loss.backward()
+                (self.grad_scaler.scale(loss) if self.grad_scaler is not None else loss).backward()
                 total += float(loss.detach())
             self.model.clip_grad_norm_(args.max_grad_norm)
-            self.collaborative_optimizer.step()
+            if self.grad_scaler is not None:
+                self.grad_scaler.step(self.collaborative_optimizer)
+                self.grad_scaler.update()
+            else:
+                self.collaborative_optimizer.step()
             self.lr_scheduler.step()
             self.model.zero_grad()
             self.state.global_step += 1

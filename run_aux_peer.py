@@ -102,6 +102,16 @@ def main(argv=None):
     parser = HfArgumentParser((AuxiliaryPeerArguments, HFTrainerArguments, CollaborativeArguments))
     peer_args, trainer_args, collab_args = parser.parse_args_into_dataclasses(argv)
 
+    coordinator = None
+    if peer_args.host_elastic_coordinator and peer_args.elastic_coordinator:
+        # the long-lived store elastic trainers rendezvous on: it must outlive every trainer
+        from dalle_amd.parallel.elastic import coordinator_store
+
+        host, port = peer_args.elastic_coordinator.rsplit(":", 1)
+        coordinator = coordinator_store(host, int(port), is_master=True)
+        logger.info(f"hosting the elastic coordinator at {peer_args.elastic_coordinator}")
+        peer_args.elastic_coordinator = None  # the aux peer itself is not a trainer / group member
+
     task = TrainingTask(peer_args, trainer_args, collab_args)
     dht = task.dht
 

@@ -7,6 +7,7 @@ process per MI355X, RCCL over xGMI; gloo for CPU peers) launched with torchrun; 
 replaces the public DHT for metrics / progress records.
 """
 import os
+import socket
 from datetime import timedelta
 from pathlib import Path
 
@@ -64,7 +65,7 @@ def make_averaging_compression(kind: str):
 
 class TrainingTask:
     """A container that defines the training config, model, tokenizer, optimizer and other local training utilities"""
-    _authorizer = _dht = _collaborative_optimizer = _training_dataset = _process_group = _arena = None
+    _authorizer = _dht = _collaborative_optimizer = _training_dataset = _process_group = _arena = _elastic = None
 
     def __init__(self, peer_args: BasePeerArguments, trainer_args: HFTrainerArguments, collab_args: CollaborativeArguments):
         self.peer_args, self.trainer_args, self.collab_args = peer_args, trainer_args, collab_args
@@ -103,7 +104,21 @@ class TrainingTask:
 
     @property
     def process_group(self):
-        """torch.distributed default group (torchrun launch), or None for a single peer."""
+        """torch.distributed default group (torchrun launch, or an elastic generation formed through the
+        coordinator store), or None for a single peer."""
+        coord = getattr(self.peer_args, "elastic_coordinator", None)
+        if coord and self._elastic is None:
+            from dalle_amd.parallel.elastic import ElasticGroup, coordinator_store
+            host, port = coord.rsplit(":", 1)
+            backend = self.trainer_args.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            if backend == "nccl":
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+            store = coordinator_store(host, int(port), is_master=False, timeout=self.collab_args.averaging_timeout)
+            peer_id = f"{socket.gethostname()}-{os.getpid()}"
+            self._elastic = ElasticGroup(store, peer_id, backend=backend, matchmaking_time=self.collab_args.matchmaking_time,
+                                         allreduce_timeout=self.collab_args.allreduce_timeout,
+                                         device=torch.device("cuda") if backend == "nccl" else torch.device("cpu"))
+            self._elastic.join()
         if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not dist.is_initialized():
             backend = self.trainer_args.backend or ("nccl" if torch.cuda.is_available() else "gloo")
             if backend == "nccl":
@@ -157,7 +172,7 @@ class TrainingTask:
                 batch_size_per_step=ta.batch_size_per_step,
                 grad_compression=averaging_compression, state_averaging_compression=averaging_compression,
                 client_mode=self.peer_args.client_mode, verbose=True, process_group=group, arena=self._arena,
-                powersgd_rank=ta.powersgd_rank if ta.grad_averaging == "powersgd" else None,
+                powersgd_rank=ta.powersgd_rank if ta.grad_averaging == "powersgd" else None, elastic=self._elastic,
                 **{k: v for k, v in vars(self.collab_args).items()})
         return self._collaborative_optimizer
 
