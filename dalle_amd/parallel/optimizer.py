@@ -355,6 +355,11 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         """New communicator over the live members, then one donor brings everyone (joiners, or
         survivors whose last step fell back to local gradients) to the same state."""
         self.elastic.regroup()
+        if self.group is not None:  # the old group object died with its communicator: rebind to the new WORLD
+            self.group = dist.group.WORLD
+            self.grad_averager.group = self.state_averager.group = self.tracker.group = self.group
+            if self.grad_averager.powersgd is not None:
+                self.grad_averager.powersgd.group = self.group
         self.grad_averager._shards = None
         self.grad_averager.last_averaging_ok = True
         self.load_state_from_peers()
