@@ -3,8 +3,10 @@
 
 For every query: 16 x 8 = 128 images (temperature / top-k / top-p sampling with the KV-cache decoder,
 one hipGraph-captured step replayed per image token on MI355X), decoded by the VQGAN, optionally
-re-ranked with CLIP (only when the ``clip`` package and weights are available locally), and saved
-as ``{output_dir}/{query}.pickle`` with keys ``query, temperature, images, clip_scores``.
+re-ranked with the native CLIP ViT-B/32 (``dalle_amd.models.clip``; weights from ``--clip`` -- a
+safetensors / state-dict file in OpenAI key layout -- or random-init with ``--clip random``; without
+``--clip`` the scores are uniform), and saved as ``{output_dir}/{query}.pickle`` with keys
+``query, temperature, images, clip_scores``.
 
 Checkpoints in the training layout are accepted (the reference's CachedAs rename
 ``net.fn.fn -> net.fn.fn.fn`` / ``to_qkv -> fn.to_qkv`` / ``to_out -> fn.to_out`` is undone when present).
@@ -81,6 +83,8 @@ def main(argv=None):
     parser.add_argument('--model-preset', type=str, default='reference', help='[new] dalle_amd.config preset')
     parser.add_argument('--batch-size', type=int, default=16, help='[new] images per generate call (reference: 16)')
     parser.add_argument('--n-iters', type=int, default=8, help='[new] generate calls per query (reference: 8)')
+    parser.add_argument('--clip', type=str, default=None, help='[new] CLIP ViT-B/32 weights (safetensors/state dict) or "random"')
+    parser.add_argument('--clip-tokenizer', type=str, default=None, help='[new] CLIP BPE tokenizer.json (tokenizers format)')
     args = parser.parse_args(argv)
 
     with open(args.queries) as f:
@@ -102,13 +106,15 @@ def main(argv=None):
     model.model.vae = gan.eval()
     model = model.to(device).eval()
 
-    clip_model = None
-    try:
-        import clip  # noqa: F401
+    clip_model = clip_tok = None
+    if args.clip:
+        from dalle_amd.models.clip import ClipTokenizer, load_clip
 
-        clip_model, clip_preprocess = clip.load("ViT-B/32", device=device)
-    except Exception:  # noqa: BLE001 - CLIP weights are not available offline
-        print('[*] CLIP unavailable: clip_scores will be uniform')
+        clip_model = load_clip(None if args.clip == "random" else args.clip, device=device)
+        clip_tok = ClipTokenizer(args.clip_tokenizer)
+        print(f"[*] CLIP ViT-B/32 {'random-init (scores are not meaningful)' if args.clip == 'random' else 'from ' + args.clip}")
+    else:
+        print('[*] No --clip weights: clip_scores will be uniform')
 
     os.makedirs(args.output_dir, exist_ok=True)
     print(f'[*] Saving results to `{args.output_dir}`')
@@ -117,13 +123,9 @@ def main(argv=None):
                           temperature=args.temperature, top_k=args.top_k, top_p=args.top_p,
                           text_seq_len=model.model.text_seq_len, device=device)
         if clip_model is not None:
-            from PIL import Image
+            from dalle_amd.models.clip import clip_scores as score_images
 
-            images_for_clip = torch.cat([clip_preprocess(Image.fromarray((img * 255).astype(np.uint8))).unsqueeze(0).to(device)
-                                         for img in images])
-            text = clip.tokenize([query]).to(device)
-            _, logits_per_text = clip_model(images_for_clip, text)
-            clip_scores = logits_per_text[0].softmax(dim=-1).cpu().numpy()
+            clip_scores = score_images(clip_model, clip_tok, torch.from_numpy(np.stack(images)), query).cpu().numpy()
         else:
             clip_scores = np.full(len(images), 1.0 / len(images), dtype=np.float32)
         with open(os.path.join(args.output_dir, f'{query}.pickle'), 'wb') as f:
