@@ -88,7 +88,7 @@ class ElasticGroup:
             self.store.set(f"elastic/g{g}/m{ticket}", self.peer_id)
             if ticket == 1:
                 self._lead(g)
-            self.store.wait([f"elastic/g{g}/frozen"], datetime.timedelta(seconds=self.matchmaking_time + self.timeout))
+            self.store.wait([f"elastic/g{g}/frozen"], datetime.timedelta(seconds=self.matchmaking_time + 2 * self.timeout + 10))
             n = int(self.store.get(f"elastic/g{g}/frozen"))
             if ticket <= n:
                 self.members = [self.store.get(f"elastic/g{g}/m{i}").decode() for i in range(1, n + 1)]
@@ -110,9 +110,11 @@ class ElasticGroup:
             if time.time() >= deadline:
                 if g == 0:
                     done = n >= self.min_peers
-                else:  # wait for every previous member that is still alive (fresh heartbeat)
+                else:  # wait for every previous member that is still alive (fresh heartbeat), but not for a
+                    # straggler past allreduce_timeout: it is dropped from this generation and rejoins later
                     arrived = {self.store.get(f"elastic/g{g}/m{i}").decode() for i in range(1, n + 1)}
-                    done = all(m in arrived or not self._alive(m) for m in previous)
+                    done = all(m in arrived or not self._alive(m) for m in previous) or \
+                        time.time() >= deadline + self.timeout
                 if done:
                     break
             time.sleep(0.05)

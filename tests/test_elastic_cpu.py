@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, port, q, die_after, start_delay, min_peers, epochs, want_world):
+def _worker(rank, port, q, die_after, start_delay, min_peers, epochs, want_world, stall_at=0, timeout=20.0):
     try:
         torch.set_num_threads(1)
         time.sleep(start_delay)
@@ -26,7 +26,7 @@ def _worker(rank, port, q, die_after, start_delay, min_peers, epochs, want_world
         from dalle_amd.parallel.optimizer import CollaborativeOptimizer
 
         store = coordinator_store("127.0.0.1", port, is_master=False, timeout=60)
-        eg = ElasticGroup(store, peer_id=f"p{rank}", matchmaking_time=1.0, allreduce_timeout=20, min_peers=min_peers)
+        eg = ElasticGroup(store, peer_id=f"p{rank}", matchmaking_time=1.0, allreduce_timeout=timeout, min_peers=min_peers)
         eg.join()
         p = torch.nn.Parameter(torch.zeros(32))
         opt = CollaborativeOptimizer(run_id="el", params=[p], optimizer=lambda ps: torch.optim.SGD(ps, lr=0.1),
@@ -42,6 +42,8 @@ def _worker(rank, port, q, die_after, start_delay, min_peers, epochs, want_world
             steps += 1
             if die_after and steps == die_after:
                 os._exit(0)  # abrupt death: no goodbye to the group
+            if stall_at and steps == stall_at:
+                time.sleep(3 * timeout)  # a straggler far past allreduce_timeout
             if steps > 1500:
                 raise RuntimeError("no progress")
         q.put(pickle.dumps((rank, eg.world_size, eg.generation, eg.regroups, opt.local_epoch, p.detach().clone())))
@@ -96,5 +98,16 @@ def test_late_joiner_is_admitted_and_synced():
     res = _run(specs, expect=3)
     worlds = {r[1] for r in res}
     assert worlds == {3}
+    ps = [r[5] for r in res]
+    assert torch.allclose(ps[0], ps[1]) and torch.allclose(ps[0], ps[2])
+
+
+@pytest.mark.slow
+def test_straggler_past_timeout_is_dropped_then_readmitted():
+    # (die_after, start_delay, min_peers, epochs, want_world, stall_at, timeout)
+    specs = [(0, 0.0, 3, 6, 3, 0, 3.0), (0, 0.0, 3, 6, 3, 0, 3.0), (0, 0.0, 3, 6, 3, 3, 3.0)]
+    res = _run(specs, expect=3)
+    assert {r[1] for r in res} == {3}
+    assert all(r[3] >= 1 for r in res)  # everybody regrouped at least once
     ps = [r[5] for r in res]
     assert torch.allclose(ps[0], ps[1]) and torch.allclose(ps[0], ps[2])
