@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--optim-bits", type=int, default=32, choices=[8, 32])
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--tunable", default="off", choices=["auto", "use", "tune", "off"],
+                    help="hipBLASLt solution selection for the library GEMMs (dalle_amd/utils/tuning.py)")
     return ap.parse_args()
 
 
@@ -55,6 +57,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.backends.cuda.matmul.allow_tf32 = False
+    from dalle_amd.utils.tuning import setup_gemm_tuning
+    tuning = setup_gemm_tuning(args.tunable if (args.tunable != "tune" or rank == 0) else "use")
 
     cfg = get_config(args.model)
     torch.manual_seed(1234)
@@ -127,7 +131,7 @@ def main():
                        "preset": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": cfg.seq_len, "parallelism": f"dp{world}",
                        "optimizer": f"LAMB ({args.optim_bits}-bit moments) + global clip 4.0",
-                       "grad_allreduce_dtype": args.grad_dtype},
+                       "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning},
             "model_tflops_per_gpu": round(tflops, 1),
             "loss": round(final_loss, 4),
         }), flush=True)
