@@ -23,6 +23,7 @@ void geglu_bwd_bias(const void*, const void*, void*, float*, const GradSink&, lo
 void scale_residual(const float*, const void*, const float*, float*, long, int, hipStream_t);
 void scale_residual_bwd(const float*, const void*, const float*, void*, float*, const GradSink&, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
+bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
@@ -299,6 +300,23 @@ void splitk_accum_(Tensor acc, Tensor part, bool accumulate) {
   dalle::splitk_accum(part.data_ptr<float>(), acc.data_ptr<float>(), n, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
 }
 
+// C = A . B^T (+ bias): A (M, K), B (N, K) bf16, both K-contiguous; M, N multiples of 256, K of 64
+Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) {
+  CHECK_IN(A, torch::kBFloat16); CHECK_IN(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A (M, K) and B (N, K)");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0, "gemm_nt: M, N multiples of 256 and K of 64");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN((*bias), torch::kBFloat16);
+    TORCH_CHECK(bias->numel() == N);
+    bp = bias->data_ptr();
+  }
+  auto C = torch::empty({M, N}, A.options());
+  TORCH_CHECK(dalle::gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, (int)variant, cur_stream()));
+  return C;
+}
+
 Tensor nonfinite(Tensor x) {
   CHECK_IN(x, torch::kFloat32);
   auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
@@ -416,6 +434,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
+  m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);
   m.def("decode_rope_", &decode_rope_);

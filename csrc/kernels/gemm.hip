@@ -1,0 +1,341 @@
+// bf16 GEMM on CDNA4 MFMA with fused epilogues (SURVEY K9/K10 epilogue targets).
+//
+//   C[M, N] = A[M, K] . B[N, K]^T     (both operands K-contiguous: "NT"; fp32 accumulate)
+//
+// Workgroup tile 256 x 256 x 64, 8 waves (2 along M x 4 along N, 128 x 64 outputs per wave, 32
+// v_mfma_f32_16x16x32_bf16 accumulators). Operands stream global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: one 1 KiB piece = 8 rows x 128 B per wave-instruction), double
+// buffered. The LDS image is lane-linear (the DMA writes base + 16*lane), so the XOR swizzle that
+// makes the fragment reads bank-conflict-free is applied to the per-lane SOURCE address:
+// physical 16-byte chunk c of row r holds logical chunk c ^ swz(r), swz(r) = (r >> 1) & 7 -- the 16
+// rows x 1 chunk read by each ds_read_b128 lane group then land on 16 distinct bank slots.
+// Workgroups walk the output tiles in an XCD-aware, column-grouped order (B column panels stay in
+// one XCD's L2 while its A row panels stream).
+//
+// Epilogues (template EPI): 0 = bf16 store (+bias); further epilogues fuse the GEGLU forward /
+// backward into the FF GEMMs (see gemm_epilogue).
+#include "common.h"
+
+namespace dalle {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+constexpr int GBM = 256, GBN = 256, GBK = 64;
+constexpr int G_THREADS = 512;
+
+__device__ __forceinline__ int gswz(int r) { return (r >> 1) & 7; }
+
+// one operand tile (256 rows x 64 k) of buffer `buf` into LDS via 4 DMA pieces per wave
+__device__ __forceinline__ void gemm_stage(const __bf16* __restrict__ src, int ld, int row0, int k0, __bf16* lds_tile,
+                                           int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;           // 0..31, rows 8*piece .. 8*piece+7
+    const int row = piece * 8 + (lane >> 3);  // this lane's row in the tile
+    const int lchunk = (lane & 7) ^ gswz(row);  // logical chunk that lands in physical chunk (lane & 7)
+    const __bf16* g = src + (size_t)(row0 + row) * ld + k0 + lchunk * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                     (void __attribute__((address_space(3)))*)(lds_tile + piece * 512), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 gemm_frag(const __bf16* tile, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(tile + row * 64 + ((chunk ^ gswz(row)) << 3));
+}
+
+// XCD-aware tile order: linear id -> XCD slot; within an XCD, tiles sweep M inside column groups
+__device__ __forceinline__ void gemm_tile_of(int& tm, int& tn, int tiles_m, int tiles_n) {
+  const int nwg = tiles_m * tiles_n;
+  int id = blockIdx.x;
+  if ((nwg & 7) == 0) id = (id & 7) * (nwg >> 3) + (id >> 3);  // bijective when nwg % 8 == 0
+  constexpr int GROUP_N = 4;                                    // column panels per group
+  const int group = id / (GROUP_N * tiles_m);
+  const int first_n = group * GROUP_N;
+  const int gn = min(tiles_n - first_n, GROUP_N);
+  const int in_group = id - group * GROUP_N * tiles_m;
+  tn = first_n + in_group % gn;
+  tm = in_group / gn;
+}
+
+template <int EPI, int VAR>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                               __bf16* __restrict__ C, const __bf16* __restrict__ bias,
+                                                               int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * GBM * GBK];  // [buf][A | B] 128 KiB
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(tm, tn, M / GBM, N / GBN);
+  const int row0 = tm * GBM, col0 = tn * GBN;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / GBK;
+  gemm_stage(A, K, row0, 0, smem, wave, lane);
+  gemm_stage(B, K, col0, 0, smem + GBM * GBK, wave, lane);
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0)
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) {
+      __bf16* nb = smem + (buf ^ 1) * (2 * GBM * GBK);
+      gemm_stage(A, K, row0, (t + 1) * GBK, nb, wave, lane);
+      gemm_stage(B, K, col0, (t + 1) * GBK, nb + GBM * GBK, wave, lane);
+    }
+    const __bf16* As = smem + buf * (2 * GBM * GBK);
+    const __bf16* Bs = As + GBM * GBK;
+    if (VAR == 0) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 a[8], b[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = gemm_frag(As, wm * 128 + i * 16 + fr, kk * 4 + fq);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = gemm_frag(Bs, wn * 64 + j * 16 + fr, kk * 4 + fq);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // all fragments of the K-step first (24 ds_read_b128 in flight), then 64 MFMAs at raised priority
+      bf16x8 a[2][8], b[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[kk][j] = gemm_frag(Bs, wn * 64 + j * 16 + fr, kk * 4 + fq);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[kk][i] = gemm_frag(As, wm * 128 + i * 16 + fr, kk * 4 + fq);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage the wave's 128 x 64 tile (bf16) through LDS, then 16-byte row stores ----
+  __bf16* ep = smem + wave * (128 * 64);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + fr;  // column within the wave tile
+    float bv = 0.f;
+    if (bias != nullptr) bv = (float)bias[col0 + wn * 64 + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        // row-major [128][64] image with the 16-byte chunk XOR-swizzled by row (conflict-free reads below)
+        ep[row * 64 + (((c >> 3) ^ (row & 7)) << 3) + (c & 7)] = (__bf16)(acc[i][j][r] + bv);
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 64 + lane;  // 128 rows x 8 chunks
+    const int row = idx >> 3, ch = idx & 7;
+    const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
+    *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Phase-pipelined variant (cdna_hip_programming.md, "256^2 8-phase template", re-derived here):
+// each K-tile runs as 4 phases, one per 64 x 32 quadrant of the wave's 128 x 64 output (16 MFMAs
+// each). The tile buffers are split into half-tiles (A rows 0-127 / 128-255, B rows 0-127 / 128-255:
+// a wave only ever reads ITS A half and B half), and every phase issues the LDS-DMA of one half-tile
+// of the NEXT K-tile into the other buffer, in consumption order (A0, B0, B1, A1). A counted
+// vmcnt(4) before each phase's barrier keeps two half-tiles in flight across barriers while retiring
+// exactly the half the next phase reads; a restaged half was last read >= 4 phases earlier (WAR).
+//   phase 0: read A[q rows 0-63] + B[cols 0-31] -> MFMA quadrant (0,0)
+//   phase 1: read B[cols 32-63]                 -> MFMA quadrant (0,1)
+//   phase 2: read A[q rows 64-127]              -> MFMA quadrant (1,1)
+//   phase 3: (registers only)                   -> MFMA quadrant (1,0)
+// ------------------------------------------------------------------------------------------------
+constexpr int HALF = 128 * GBK;  // elements of one half-tile image
+
+// Half-tile image of 128 operand rows: the rows one PHASE reads across all 8 waves. For A (blk = 64)
+// the "lo" half holds tile rows 0-63 and 128-191 (rows 0-63 of both wave rows), "hi" the other 128;
+// for B (blk = 32) "lo" holds columns {0-31, 64-95, 128-159, 192-223} (the first 32 of each wave's
+// 64), "hi" the rest. Image row hr <-> tile row (hr / blk) * 2 blk + off + hr % blk.
+__device__ __forceinline__ void stage_half(const __bf16* __restrict__ src, int ld, int row0, int k0, __bf16* lds_half,
+                                           int wave, int lane, int blk, int off) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;           // 0..15: image rows 8*piece .. 8*piece+7
+    const int hr = piece * 8 + (lane >> 3);
+    const int row = (hr / blk) * 2 * blk + off + (hr % blk);
+    const int lchunk = (lane & 7) ^ gswz(hr);
+    const __bf16* g = src + (size_t)(row0 + row) * ld + k0 + lchunk * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                     (void __attribute__((address_space(3)))*)(lds_half + piece * 512), 16, 0, 0);
+  }
+}
+
+template <int EPI, int OPT>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                                      __bf16* __restrict__ C, const __bf16* __restrict__ bias,
+                                                                      int M, int N, int K) {
+  // [buf][A0 | A1 | B0 | B1] half-tile images, 128 KiB in ONE array (a second __shared__ object can
+  // make hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(tm, tn, M / GBM, N / GBN);
+  const int row0 = tm * GBM, col0 = tn * GBN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile images per buffer, in consumption order: 0 A-lo (phase 0), 1 B-lo (phase 0),
+  // 2 B-hi (phase 1), 3 A-hi (phase 2)
+  auto slot = [&](int buf, int which) { return smem + (buf * 4 + which) * HALF; };
+  auto stage = [&](int t, int p) {
+    const int buf = t & 1, k0 = t * GBK;
+    if (p == 0) stage_half(A, K, row0, k0, slot(buf, 0), wave, lane, 64, 0);
+    else if (p == 1) stage_half(B, K, col0, k0, slot(buf, 1), wave, lane, 32, 0);
+    else if (p == 2) stage_half(B, K, col0, k0, slot(buf, 2), wave, lane, 32, 32);
+    else stage_half(A, K, row0, k0, slot(buf, 3), wave, lane, 64, 64);
+  };
+
+  const int nk = K / GBK;
+  for (int p = 0; p < 4; ++p) stage(0, p);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];  // [m-tile][kk], [n-tile][kk]
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const __bf16* Alo = slot(buf, 0);
+    const __bf16* Blo = slot(buf, 1);
+    const __bf16* Bhi = slot(buf, 2);
+    const __bf16* Ahi = slot(buf, 3);
+    const bool more = t + 1 < nk;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // 1) fragment reads of this phase (data retired one phase earlier)
+      if (p == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0[j][kk] = gemm_frag(Blo, wn * 32 + j * 16 + fr, kk * 4 + fq);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Alo, wm * 64 + i * 16 + fr, kk * 4 + fq);
+      } else if (p == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b1[j][kk] = gemm_frag(Bhi, wn * 32 + j * 16 + fr, kk * 4 + fq);
+      } else if (p == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Ahi, wm * 64 + i * 16 + fr, kk * 4 + fq);
+      }
+      // 2) LDS-DMA of one half-tile of the next K-tile, then retire all but the two youngest halves
+      if (more) {
+        stage(t + 1, p);
+        // phase 3 reads nothing from LDS, so phase 2 need not retire anything (OPT & 1)
+        if (!((OPT & 1) && p == 2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // a compiler-visible barrier: the builtin s_barrier does not order memory operations, and a
+      // ds_read of the next phase hoisted above it would race with other waves' DMA retirement
+      asm volatile("s_barrier" ::: "memory");
+      // 3) the quadrant's 16 MFMAs
+      if (!(OPT & 2)) __builtin_amdgcn_s_setprio(1);
+      const int mi0 = (p >= 2) ? 4 : 0;
+      const bool right = (p == 1 || p == 2);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4_t& c = acc[mi0 + i][(right ? 2 : 0) + j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], right ? b1[j][kk] : b0[j][kk], c, 0, 0, 0);
+          }
+      if (!(OPT & 2)) __builtin_amdgcn_s_setprio(0);
+      if (OPT & 4) asm volatile("s_barrier" ::: "memory");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue (as in gemm_nt_kernel) ----
+  __bf16* ep = smem + wave * (128 * 64);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + fr;
+    float bv = 0.f;
+    if (bias != nullptr) bv = (float)bias[col0 + wn * 64 + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        ep[row * 64 + (((c >> 3) ^ (row & 7)) << 3) + (c & 7)] = (__bf16)(acc[i][j][r] + bv);
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 64 + lane;
+    const int row = idx >> 3, ch = idx & 7;
+    const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
+    *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+  }
+}
+
+bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int epi, hipStream_t st) {
+  if (M % GBM || N % GBN || K % GBK) return false;
+  const int nwg = (M / GBM) * (N / GBN);
+  switch (epi) {
+    case 0:
+      hipLaunchKernelGGL((gemm_nt_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                         (__bf16*)C, (const __bf16*)bias, M, N, K);
+      return true;
+#define PHASED_CASE(o)                                                                                          \
+  case 200 + o:                                                                                                \
+    hipLaunchKernelGGL((gemm_nt_phased_kernel<0, o>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A,      \
+                       (const __bf16*)B, (__bf16*)C, (const __bf16*)bias, M, N, K);                             \
+    return true;
+    PHASED_CASE(0) PHASED_CASE(1) PHASED_CASE(2) PHASED_CASE(3) PHASED_CASE(4) PHASED_CASE(5) PHASED_CASE(6) PHASED_CASE(7)
+#undef PHASED_CASE
+    case 100:
+      hipLaunchKernelGGL((gemm_nt_kernel<0, 1>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                         (__bf16*)C, (const __bf16*)bias, M, N, K);
+      return true;
+    default:
+      return false;
+  }
+}
+
+}  // namespace dalle

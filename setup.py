@@ -21,6 +21,7 @@ hip_sources = [
     "csrc/kernels/elementwise.hip",
     "csrc/kernels/xent.hip",
     "csrc/kernels/decode.hip",
+    "csrc/kernels/gemm.hip",
     "csrc/optim/lamb.hip",
 ]
 

@@ -125,3 +125,19 @@ def test_splitk_accum(cuda):
     assert torch.allclose(acc, want, atol=1e-5)
     C().splitk_accum_(acc, part, False)
     assert torch.allclose(acc, part.sum(0), atol=1e-5)
+
+
+@pytest.mark.parametrize("variant", [0, 202])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 320), (1024, 256, 1024)])
+def test_gemm_nt(cuda, variant, M, N, K):
+    from dalle_amd.ops.hip_ops import C
+
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).bfloat16()
+    B = torch.randn(N, K, device=cuda).bfloat16()
+    bias = torch.randn(N, device=cuda).bfloat16()
+    want = A.float() @ B.float().t() + bias.float()
+    got = C().gemm_nt(A, B, bias, variant).float()
+    assert _rel(got, want) < 1e-2
+    got = C().gemm_nt(A, B, None, variant).float()
+    assert _rel(got, A.float() @ B.float().t()) < 1e-2
