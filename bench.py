@@ -52,10 +52,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a 1-GPU box, with
+    # BENCH_BACKEND=gloo) share devices round-robin
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", dev_index)
     torch.backends.cuda.matmul.allow_tf32 = False
     from dalle_amd.utils.tuning import setup_gemm_tuning
     tuning = setup_gemm_tuning(args.tunable if (args.tunable != "tune" or rank == 0) else "use")
