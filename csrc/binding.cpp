@@ -24,6 +24,8 @@ void scale_residual(const float*, const void*, const float*, float*, long, int, 
 void scale_residual_bwd(const float*, const void*, const float*, void*, float*, const GradSink&, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
 bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
+bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
+                   float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
@@ -317,6 +319,26 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
   return C;
 }
 
+// QKV projection with the rotary fused into the GEMM epilogue: h (B*n, K) . Wqkv (3*H*64, K)^T ->
+// q (pre-scaled), k, v in the padded attention storage layout (B*H, Np, 64); padding rows zeroed.
+std::vector<Tensor> qkv_rope(Tensor h, Tensor w, Tensor cosT, Tensor sinT, int64_t T, int64_t S, int64_t H, int64_t n,
+                             bool col_major, double qscale) {
+  CHECK_IN(h, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  TORCH_CHECK(h.dim() == 2 && w.dim() == 2 && w.size(0) == 3 * H * 64 && w.size(1) == h.size(1), "qkv_rope: shapes");
+  const int M = h.size(0), K = h.size(1);
+  TORCH_CHECK(M % n == 0 && M % 256 == 0 && (3 * H * 64) % 256 == 0 && K % 64 == 0, "qkv_rope: tile multiples");
+  TORCH_CHECK(cosT.size(0) >= n && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes());
+  auto g = make_attn_geom(T, S, n, 1, H, 0);
+  const int B = M / n;
+  auto opts = h.options();
+  auto q = torch::empty({B * H, g.Np, 64}, opts);
+  auto k = torch::empty({B * H, g.Np, 64}, opts);
+  auto v = torch::empty({B * H, g.Np, 64}, opts);
+  TORCH_CHECK(dalle::gemm_qkv_rope(h.data_ptr(), w.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cosT.data_ptr<float>(),
+                                   sinT.data_ptr<float>(), M, K, H, T, S, n, col_major ? 1 : 0, (float)qscale, cur_stream()));
+  return {q, k, v};
+}
+
 Tensor nonfinite(Tensor x) {
   CHECK_IN(x, torch::kFloat32);
   auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
@@ -434,6 +456,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
+  m.def("qkv_rope", &qkv_rope);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);

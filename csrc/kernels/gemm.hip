@@ -155,6 +155,26 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_kernel(const __bf16* __r
 }
 
 
+// Epilogue parameters of the QKV projection with the 3-axis rotary fused in (EPI 1): the GEMM writes
+// q (rotated, pre-scaled), k, v (rotated) straight into the padded attention storage layout
+// (B*H, Np, 64) instead of a (M, 3*H*64) tensor -- the separate rotary pass disappears.
+struct RopeEpi {
+  __bf16* q;
+  __bf16* k;
+  __bf16* v;
+  const float* cosT;
+  const float* sinT;
+  int T, Tp, S, logS, n, Np, H, col_major;
+  float qscale;
+};
+
+__device__ __forceinline__ int rope_epi_seq2st(const RopeEpi& e, int p) {
+  if (p < e.T) return p;
+  const int kk = p - e.T;
+  const int kst = e.col_major ? ((kk & (e.S - 1)) << e.logS) + (kk >> e.logS) : kk;
+  return e.Tp + kst;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Phase-pipelined variant (cdna_hip_programming.md, "256^2 8-phase template", re-derived here):
 // each K-tile runs as 4 phases, one per 64 x 32 quadrant of the wave's 128 x 64 output (16 MFMAs
@@ -191,7 +211,7 @@ __device__ __forceinline__ void stage_half(const __bf16* __restrict__ src, int l
 template <int EPI, int OPT>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                       __bf16* __restrict__ C, const __bf16* __restrict__ bias,
-                                                                      int M, int N, int K) {
+                                                                      int M, int N, int K, RopeEpi rope) {
   // [buf][A0 | A1 | B0 | B1] half-tile images, 128 KiB in ONE array (a second __shared__ object can
   // make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];
@@ -304,14 +324,61 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_s_waitcnt(0xC07F);
-  __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
+  if (EPI == 0) {
+    __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int idx = it * 64 + lane;
-    const int row = idx >> 3, ch = idx & 7;
-    const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
-    *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, ch = idx & 7;
+      const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
+      *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+    }
+  } else {
+    // the wave's 64 columns are exactly one (part, head): rotate each 8-column chunk of each row and
+    // scatter the row to its storage slot
+    const int HD = rope.H * 64;
+    const int c0 = col0 + wn * 64;
+    const int part = c0 / HD, h = (c0 - part * HD) >> 6;
+    __bf16* dstT = part == 0 ? rope.q : (part == 1 ? rope.k : rope.v);
+    const float sc = part == 0 ? rope.qscale : 1.0f;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, ch = idx & 7;
+      const int r = row0 + wm * 128 + row;
+      const int b = r / rope.n, p = r - b * rope.n;
+      float x[8], cs[8], sn[8];
+      unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), x);
+      const float* cp = rope.cosT + (size_t)p * 64 + ch * 8;
+      const float* sp = rope.sinT + (size_t)p * 64 + ch * 8;
+      *reinterpret_cast<f32x4*>(cs) = *reinterpret_cast<const f32x4*>(cp);
+      *reinterpret_cast<f32x4*>(cs + 4) = *reinterpret_cast<const f32x4*>(cp + 4);
+      *reinterpret_cast<f32x4*>(sn) = *reinterpret_cast<const f32x4*>(sp);
+      *reinterpret_cast<f32x4*>(sn + 4) = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const float a0 = x[i], a1 = x[i + 1];
+        x[i] = (a0 * cs[i] + a1 * sn[i]) * sc;
+        x[i + 1] = (a1 * cs[i + 1] + a0 * sn[i + 1]) * sc;
+      }
+      const int srow = rope_epi_seq2st(rope, p);
+      *reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8) = pack8(x);
+    }
   }
+}
+
+// zero the storage rows that have no sequence position (text padding [T, Tp) and the last image slot)
+__global__ void rope_pad_zero_kernel(__bf16* q, __bf16* k, __bf16* v, int Tp, int T, int Np, int BH) {
+  const int bh = blockIdx.x, t = threadIdx.x;  // 256 threads: (pad row, 8-chunk)
+  const int npad = Tp - T + 1;
+  const int pr = t >> 3, ch = t & 7;
+  if (pr >= npad) return;
+  const int srow = pr < Tp - T ? T + pr : Np - 1;
+  const size_t off = ((size_t)bh * Np + srow) * 64 + ch * 8;
+  const s16x8 z = {};
+  *reinterpret_cast<s16x8*>(q + off) = z;
+  *reinterpret_cast<s16x8*>(k + off) = z;
+  *reinterpret_cast<s16x8*>(v + off) = z;
 }
 
 bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int epi, hipStream_t st) {
@@ -325,7 +392,7 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
 #define PHASED_CASE(o)                                                                                          \
   case 200 + o:                                                                                                \
     hipLaunchKernelGGL((gemm_nt_phased_kernel<0, o>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A,      \
-                       (const __bf16*)B, (__bf16*)C, (const __bf16*)bias, M, N, K);                             \
+                       (const __bf16*)B, (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{});                  \
     return true;
     PHASED_CASE(0) PHASED_CASE(1) PHASED_CASE(2) PHASED_CASE(3) PHASED_CASE(4) PHASED_CASE(5) PHASED_CASE(6) PHASED_CASE(7)
 #undef PHASED_CASE
@@ -338,4 +405,22 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
   }
 }
 
+// QKV projection + rotary into the attention storage layout (q pre-scaled); M = B*n rows
+bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, const float* cosT, const float* sinT, int M, int K,
+                   int H, int T, int S, int n, int col_major, float qscale, hipStream_t st) {
+  const int N = 3 * H * 64;
+  if (M % GBM || N % GBN || K % GBK || M % n) return false;
+  int logS = 0;
+  while ((1 << logS) < S) ++logS;
+  const int Tp = (T + 31) / 32 * 32;
+  RopeEpi e{(__bf16*)q, (__bf16*)k, (__bf16*)v, cosT, sinT, T, Tp, S, logS, n, Tp + S * S, H, col_major, qscale};
+  const int nwg = (M / GBM) * (N / GBN);
+  hipLaunchKernelGGL((gemm_nt_phased_kernel<1, 2>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)W,
+                     (__bf16*)nullptr, (const __bf16*)nullptr, M, N, K, e);
+  const int BH = (M / n) * H;
+  hipLaunchKernelGGL(rope_pad_zero_kernel, dim3(BH), dim3(256), 0, st, (__bf16*)q, (__bf16*)k, (__bf16*)v, Tp, T, Tp + S * S, BH);
+  return true;
+}
+
 }  // namespace dalle
+

@@ -84,6 +84,8 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
 
 
 SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
+# QKV projection through the hand-written GEMM with the rotary in its epilogue (csrc/kernels/gemm.hip)
+FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "1"))
 
 
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
@@ -312,10 +314,14 @@ class _AttnSublayer(torch.autograd.Function):
         h, mean, rstd = C().ln_shift_fwd(x, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
         h2 = h.view(-1, d)
         wq = bf16_weight(w_qkv)
-        qkv = torch.mm(h2, wq.t()).view(B, n, -1)
         col = pattern == PATTERN_IDS["axial_col"]
-        q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
-        del qkv
+        if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
+            # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
+            q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
+        else:
+            qkv = torch.mm(h2, wq.t()).view(B, n, -1)
+            q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+            del qkv
         out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
         wo = bf16_weight(w_out)
         y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())

@@ -141,3 +141,23 @@ def test_gemm_nt(cuda, variant, M, N, K):
     assert _rel(got, want) < 1e-2
     got = C().gemm_nt(A, B, None, variant).float()
     assert _rel(got, A.float() @ B.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
+def test_qkv_rope_gemm_matches_unfused(cuda, attn_type):
+    from dalle_amd.ops.hip_ops import C, _rope_tables
+
+    torch.manual_seed(0)
+    T, S, H, D = 65, 16, 4, 256
+    geom = AttnGeometry(T, S, 5)
+    n, B = T + S * S - 1, 4  # M = 1280: a multiple of 256
+    h = torch.randn(B * n, D, device=cuda).bfloat16()
+    w = (0.05 * torch.randn(3 * H * 64, D, device=cuda)).bfloat16()
+    cos, sin = _rope_tables(geom, 64, cuda)
+    col = attn_type == "axial_col"
+    q, k, v = C().qkv_rope(h, w, cos, sin, T, S, H, n, col, 0.125)
+    qkv = torch.mm(h, w.t()).view(B, n, -1)
+    q2, k2, v2 = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+    for a, b_ in [(q, q2), (k, k2), (v, v2)]:
+        assert a.shape == b_.shape
+        assert _rel(a, b_) < 1e-2
