@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--model", default="bench24")
     ap.add_argument("--optim-bits", type=int, default=32, choices=[8, 32])
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="after the timed run: K more steps with per-phase timing (+ torch.profiler trace)")
+    ap.add_argument("--trace", default="", help="chrome trace path for the --profile-steps pass")
     ap.add_argument("--tunable", default="off", choices=["auto", "use", "tune", "off"],
                     help="hipBLASLt solution selection for the library GEMMs (dalle_amd/utils/tuning.py)")
     return ap.parse_args()
@@ -87,13 +89,20 @@ def main():
     batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
                                cfg.num_image_tokens, gen, device=device) for _ in range(4)]
 
-    def step(i):
+    from dalle_amd.utils.profiling import StepTimer, prof_range
+
+    def step(i, timer=None):
+        phase = timer if timer is not None else (lambda name: prof_range(name))
         b = batches[i % len(batches)]
         arena.zero_grad()
-        loss = model(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
-        loss.backward()
-        sync.all_reduce()
-        opt.step()
+        with phase("forward"):
+            loss = model(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
+        with phase("backward"):
+            loss.backward()
+        with phase("grad_allreduce"):
+            sync.all_reduce()
+        with phase("optimizer"):
+            opt.step()
         return loss
 
     for i in range(args.warmup):
@@ -143,6 +152,22 @@ def main():
             "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1),
             "loss": round(final_loss, 4),
         }), flush=True)
+    if args.profile_steps:
+        # untimed diagnostic pass: per-phase wall times (synchronised) and an optional trace
+        timer = StepTimer()
+        prof = None
+        if args.trace:
+            prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                      torch.profiler.ProfilerActivity.CUDA])
+            prof.__enter__()
+        for i in range(args.profile_steps):
+            step(i, timer)
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            if rank == 0:
+                prof.export_chrome_trace(args.trace)
+        if rank == 0:
+            print("# phase ms/step: " + json.dumps(timer.summary()), file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

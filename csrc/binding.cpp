@@ -24,6 +24,9 @@ void scale_residual(const float*, const void*, const float*, float*, long, int, 
 void scale_residual_bwd(const float*, const void*, const float*, void*, float*, const GradSink&, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
 bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
+void uq8_compress(const float*, long, uint8_t*, float*, void*, hipStream_t);
+size_t uq8_workspace_bytes();
+void uq8_dequant(const uint8_t*, const float*, float*, long, float, int, hipStream_t);
 bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
                    float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
@@ -339,6 +342,26 @@ std::vector<Tensor> qkv_rope(Tensor h, Tensor w, Tensor cosT, Tensor sinT, int64
   return {q, k, v};
 }
 
+// Uniform 8-bit quantisation (collaborative averaging compression): x fp32 -> (q uint8, codebook[256] fp32)
+std::vector<Tensor> uq8_compress(Tensor x) {
+  CHECK_IN(x, torch::kFloat32);
+  const long n = x.numel();
+  TORCH_CHECK(n > 0, "uq8_compress: empty tensor");
+  auto q = torch::empty({n}, x.options().dtype(torch::kUInt8));
+  auto cb = torch::empty({256}, x.options());
+  auto ws = torch::empty({(long)dalle::uq8_workspace_bytes()}, x.options().dtype(torch::kUInt8));
+  dalle::uq8_compress(x.data_ptr<float>(), n, q.data_ptr<uint8_t>(), cb.data_ptr<float>(), ws.data_ptr(), cur_stream());
+  return {q, cb};
+}
+
+// out [+]= weight * codebook[q]
+void uq8_dequant_(Tensor q, Tensor codebook, Tensor out, double weight, bool accumulate) {
+  CHECK_IN(q, torch::kUInt8); CHECK_IN(codebook, torch::kFloat32); CHECK_IN(out, torch::kFloat32);
+  TORCH_CHECK(codebook.numel() == 256 && out.numel() == q.numel());
+  dalle::uq8_dequant(q.data_ptr<uint8_t>(), codebook.data_ptr<float>(), out.data_ptr<float>(), q.numel(), (float)weight,
+                     accumulate ? 1 : 0, cur_stream());
+}
+
 Tensor nonfinite(Tensor x) {
   CHECK_IN(x, torch::kFloat32);
   auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
@@ -457,6 +480,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
   m.def("qkv_rope", &qkv_rope);
+  m.def("uq8_compress", &uq8_compress);
+  m.def("uq8_dequant_", &uq8_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);

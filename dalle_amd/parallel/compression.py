@@ -77,6 +77,12 @@ class Uniform8BitQuantization(CompressionBase):
 
     def compress(self, x):
         x = x.reshape(-1).float()
+        if x.is_cuda:
+            # fused HIP passes with an integer (deterministic) codebook reduction: csrc/kernels/quant.hip
+            from ..ops.ext import load_extension
+
+            q, cb = load_extension(required=True).uq8_compress(x.contiguous())
+            return {"idx": q, "codebook": cb}
         n = x.numel()
         shift = x.mean()
         centered = x - shift
@@ -86,6 +92,12 @@ class Uniform8BitQuantization(CompressionBase):
         return {"idx": q, "codebook": average_buckets(x, q, self.n_bins)}
 
     def extract(self, c, numel):
+        if c["idx"].is_cuda:
+            from ..ops.ext import load_extension
+
+            out = torch.empty(c["idx"].numel(), dtype=torch.float32, device=c["idx"].device)
+            load_extension(required=True).uq8_dequant_(c["idx"].contiguous(), c["codebook"].float().contiguous(), out, 1.0, False)
+            return out
         return c["codebook"][c["idx"].long()]
 
     def bytes_per_element(self):

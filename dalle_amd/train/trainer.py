@@ -24,6 +24,7 @@ import torch
 from torch.utils.data import DataLoader
 
 from ..utils.logging import get_logger
+from ..utils.profiling import prof_range
 
 logger = get_logger(__name__)
 
@@ -178,16 +179,19 @@ class CollaborativeHFTrainer:
             for _ in range(accum):
                 batch = next(loader)
                 batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
-                out = self.model(**batch)
-                loss = out["loss"] / accum
-                (self.grad_scaler.scale(loss) if self.grad_scaler is not None else loss).backward()
+                with prof_range("forward"):
+                    out = self.model(**batch)
+                    loss = out["loss"] / accum
+                with prof_range("backward"):
+                    (self.grad_scaler.scale(loss) if self.grad_scaler is not None else loss).backward()
                 total += float(loss.detach())
             self.model.clip_grad_norm_(args.max_grad_norm)
-            if self.grad_scaler is not None:
-                self.grad_scaler.step(self.collaborative_optimizer)
-                self.grad_scaler.update()
-            else:
-                self.collaborative_optimizer.step()
+            with prof_range("collaborative_step"):
+                if self.grad_scaler is not None:
+                    self.grad_scaler.step(self.collaborative_optimizer)
+                    self.grad_scaler.update()
+                else:
+                    self.collaborative_optimizer.step()
             self.lr_scheduler.step()
             self.model.zero_grad()
             self.state.global_step += 1

@@ -22,6 +22,7 @@ hip_sources = [
     "csrc/kernels/xent.hip",
     "csrc/kernels/decode.hip",
     "csrc/kernels/gemm.hip",
+    "csrc/kernels/quant.hip",
     "csrc/optim/lamb.hip",
 ]
 
