@@ -27,6 +27,10 @@ bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, h
 void uq8_compress(const float*, long, uint8_t*, float*, void*, hipStream_t);
 size_t uq8_workspace_bytes();
 void uq8_dequant(const uint8_t*, const float*, float*, long, float, int, hipStream_t);
+bool skinny_gemm(int, SkinnyArgs, hipStream_t);
+int skinny_ks(int, int, int, int);
+void skinny_force_config(int, int, int, int);
+std::vector<int> skinny_shape_info(int, int, int, int);
 bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
                    float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
@@ -322,6 +326,84 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
   return C;
 }
 
+// ---- decode-step skinny GEMMs (M <= 64): one launch each, epilogue fused ----
+static dalle::SkinnyArgs skinny_prep(const Tensor& X, const Tensor& W, const c10::optional<Tensor>& bias, int64_t nout,
+                                     int nb, const Tensor& cnt, Tensor& ws) {
+  CHECK_CUDA(X); CHECK_DT(X, torch::kBFloat16); CHECK_IN(W, torch::kBFloat16); CHECK_IN(cnt, torch::kInt32);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && W.dim() == 2 && X.size(1) == W.size(1), "skinny: X (M, K), W (N, K)");
+  const int M = X.size(0), K = X.size(1);
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny: 1 <= M <= 64");
+  TORCH_CHECK(nout % 16 == 0 && W.size(0) == nout * nb && K % 128 == 0, "skinny: N % 16, K % 128");
+  TORCH_CHECK(cnt.numel() >= nout / 16, "skinny: counter buffer too small");
+  TORCH_CHECK(X.stride(0) % 8 == 0, "skinny: X rows must be 16-byte aligned");
+  dalle::SkinnyArgs a{};
+  a.X = X.data_ptr();
+  a.W = W.data_ptr();
+  a.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN((*bias), torch::kBFloat16);
+    TORCH_CHECK(bias->numel() == nout * nb, "skinny: bias size");
+    a.bias = bias->data_ptr();
+  }
+  a.M = M; a.N = nout; a.K = K; a.ldx = X.stride(0);
+  a.KS = dalle::skinny_ks(M, nout, K, nb);
+  const int mpad = M <= 16 ? 16 : (M <= 32 ? 32 : 64);
+  if (a.KS > 1) ws = torch::empty({(int64_t)a.KS * nout * mpad * nb}, X.options().dtype(torch::kFloat32));
+  a.ws = a.KS > 1 ? ws.data_ptr<float>() : nullptr;
+  a.cnt = cnt.data_ptr<int>();
+  return a;
+}
+
+Tensor skinny_linear(Tensor X, Tensor W, c10::optional<Tensor> bias, bool out_f32, Tensor cnt) {
+  Tensor ws;
+  auto a = skinny_prep(X, W, bias, W.size(0), 1, cnt, ws);
+  auto out = torch::empty({X.size(0), W.size(0)}, X.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  a.out = out.data_ptr();
+  a.out_f32 = out_f32;
+  TORCH_CHECK(dalle::skinny_gemm(0, a, cur_stream()), "skinny_linear: unsupported shape");
+  return out;
+}
+
+Tensor skinny_geglu(Tensor X, Tensor W, c10::optional<Tensor> bias, Tensor cnt) {
+  TORCH_CHECK(W.size(0) % 2 == 0, "skinny_geglu: W holds the value and gate halves");
+  Tensor ws;
+  auto a = skinny_prep(X, W, bias, W.size(0) / 2, 2, cnt, ws);
+  auto out = torch::empty({X.size(0), W.size(0) / 2}, X.options().dtype(torch::kBFloat16));
+  a.out = out.data_ptr();
+  TORCH_CHECK(dalle::skinny_gemm(1, a, cur_stream()), "skinny_geglu: unsupported shape");
+  return out;
+}
+
+void skinny_residual_(Tensor resid, Tensor X, Tensor W, c10::optional<Tensor> bias, Tensor scale, Tensor cnt) {
+  CHECK_IN(resid, torch::kFloat32); CHECK_IN(scale, torch::kFloat32);
+  Tensor ws;
+  auto a = skinny_prep(X, W, bias, W.size(0), 1, cnt, ws);
+  TORCH_CHECK(resid.dim() == 2 && resid.size(0) == X.size(0) && resid.size(1) == W.size(0), "skinny_residual_: resid (M, N)");
+  TORCH_CHECK(scale.numel() == W.size(0), "skinny_residual_: scale (N,)");
+  a.resid = resid.data_ptr<float>();
+  a.scale = scale.data_ptr<float>();
+  TORCH_CHECK(dalle::skinny_gemm(2, a, cur_stream()), "skinny_residual_: unsupported shape");
+}
+
+void skinny_qkv_rope_(Tensor X, Tensor W, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, Tensor pos, int64_t H,
+                      double qscale, Tensor cnt) {
+  CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32); CHECK_IN(q, torch::kBFloat16);
+  CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  TORCH_CHECK(W.size(0) == 3 * H * 64, "skinny_qkv_rope_: W (3*H*64, K)");
+  const int M = X.size(0);
+  TORCH_CHECK(q.numel() == (int64_t)M * H * 64, "skinny_qkv_rope_: q (M*H, 64)");
+  TORCH_CHECK(kc.dim() == 3 && kc.size(0) == M * H && kc.size(2) == 64 && vc.sizes() == kc.sizes(),
+              "skinny_qkv_rope_: caches (M*H, n, 64)");
+  TORCH_CHECK(cosT.size(0) >= kc.size(1) && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes(), "skinny_qkv_rope_: tables");
+  Tensor ws;
+  auto a = skinny_prep(X, W, c10::nullopt, W.size(0), 1, cnt, ws);
+  a.q = q.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr();
+  a.cosT = cosT.data_ptr<float>(); a.sinT = sinT.data_ptr<float>();
+  a.pos = pos.data_ptr<int>();
+  a.H = H; a.n = kc.size(1); a.qscale = (float)qscale;
+  TORCH_CHECK(dalle::skinny_gemm(3, a, cur_stream()), "skinny_qkv_rope_: unsupported shape");
+}
+
 // QKV projection with the rotary fused into the GEMM epilogue: h (B*n, K) . Wqkv (3*H*64, K)^T ->
 // q (pre-scaled), k, v in the padded attention storage layout (B*H, Np, 64); padding rows zeroed.
 std::vector<Tensor> qkv_rope(Tensor h, Tensor w, Tensor cosT, Tensor sinT, int64_t T, int64_t S, int64_t H, int64_t n,
@@ -487,6 +569,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_ln_shift_", &decode_ln_shift_);
   m.def("decode_rope_", &decode_rope_);
   m.def("decode_attn_", &decode_attn_);
+  m.def("skinny_linear", &skinny_linear);
+  m.def("skinny_force_config", &dalle::skinny_force_config);
+  m.def("skinny_shape_info", &dalle::skinny_shape_info);
+  m.def("skinny_geglu", &skinny_geglu);
+  m.def("skinny_residual_", &skinny_residual_);
+  m.def("skinny_qkv_rope_", &skinny_qkv_rope_);
   m.def("vq_embed", &vq_embed);
   m.def("lamb_grad_norm", &lamb_grad_norm);
   m.def("lamb_step", &lamb_step);

@@ -115,66 +115,160 @@ __device__ __forceinline__ int decode_key_at(const DecodeGeom& g, int i, int pos
   return g.T + rr * g.S + cc;
 }
 
-// ---- one query per (b, h) against its allowed cached keys; scores in LDS, PV over 4 key groups ----
+// ---- one query per (b, h) against its allowed cached keys ----
+// Bandwidth-bound: ~290 keys x (K + V) x 128 B per (b, h) at the reference config. Layout: 8 lanes
+// cover one 128-B key row (16 B each), so a wave reads 8 whole rows per instruction; key i of a
+// chunk sits at (round u, wave w, slot s) = i / 32, (i / 8) % 4, i % 8. In the common case (all keys
+// in one chunk of 32 * DA_U) every K AND V load of the lane is issued before the first score is
+// formed -- V does not depend on the softmax -- so the whole (b, h) is one memory round trip. Longer
+// key sets (full attention late in the sequence) take a chunked two-pass path with scores in LDS.
+constexpr int DA_U = 12;                 // rounds per chunk: 384 keys
+constexpr int DA_CHUNK = 32 * DA_U;
+constexpr int DA_MAXN = 2048;
+
+__device__ __forceinline__ float dot8(const float* q, const s16x8& k) {
+  float f[8];
+  unpack8(k, f);
+  float a = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a += q[e] * f[e];
+  return a;
+}
+
+__device__ __forceinline__ float slot_sum(float v) {  // over the 8 lanes of one key row
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ kc,
                                                           const __bf16* __restrict__ vc, __bf16* __restrict__ out,
                                                           const int* __restrict__ pos_ptr, DecodeGeom g) {
-  __shared__ float qs[64];
-  __shared__ float sc[2048];
-  __shared__ float red[8];
+  __shared__ float sc[DA_MAXN];
+  __shared__ float red[2][4];
   __shared__ float part[4][64];
-  const int bh = blockIdx.x, tid = threadIdx.x;
+  const int bh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sub = lane & 7, slot = lane >> 3;
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
-  if (tid < 64) qs[tid] = bf2f(reinterpret_cast<const bf16_raw*>(q)[(size_t)bh * 64 + tid]);
-  __syncthreads();
+  float qd[8];
+  unpack8(*reinterpret_cast<const s16x8*>(q + (size_t)bh * 64 + sub * 8), qd);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
   int nloc, r0 = 0, c0 = 0, nr = 0, nc = 1;
   const int nkeys = decode_num_keys(g, pos, nloc, r0, c0, nr, nc);
-  const __bf16* kb = kc + (size_t)bh * g.n * 64;
-  const __bf16* vb = vc + (size_t)bh * g.n * 64;
-  float mloc = NEG_BIG;
-  for (int i = tid; i < nkeys; i += 256) {
-    const int j = decode_key_at(g, i, pos, r0, c0, nc);
-    const __bf16* kr = kb + (size_t)j * 64;
-    float acc = 0.f;
+  const __bf16* kb = kc + (size_t)bh * g.n * 64 + sub * 8;
+  const __bf16* vb = vc + (size_t)bh * g.n * 64 + sub * 8;
+  float acc[8];
 #pragma unroll
-    for (int d8 = 0; d8 < 8; ++d8) {
-      float f[8];
-      unpack8(*reinterpret_cast<const s16x8*>(kr + 8 * d8), f);
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  float m, inv;
+
+  if (nkeys <= DA_CHUNK) {
+    // ---- single chunk: K and V of every key in flight at once ----
+    s16x8 kf[DA_U], vf[DA_U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc += f[e] * qs[8 * d8 + e];
+    for (int u = 0; u < DA_U; ++u) {
+      const int i = u * 32 + wave * 8 + slot;
+      if (i < nkeys) {
+        const size_t j = (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64;
+        kf[u] = *reinterpret_cast<const s16x8*>(kb + j);
+        vf[u] = *reinterpret_cast<const s16x8*>(vb + j);
+      } else {
+        kf[u] = s16x8{};
+        vf[u] = s16x8{};
+      }
     }
-    acc *= LOG2E;
-    sc[i] = acc;
-    mloc = fmaxf(mloc, acc);
+    float sv[DA_U];
+    float mloc = NEG_BIG;
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) {
+      const int i = u * 32 + wave * 8 + slot;
+      sv[u] = i < nkeys ? slot_sum(dot8(qd, kf[u])) : NEG_BIG;
+      mloc = fmaxf(mloc, sv[u]);
+    }
+    mloc = wave_max(mloc);
+    if (lane == 0) red[0][wave] = mloc;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float ssum = 0.f;
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) {
+      const float p = exp2f(sv[u] - m);  // 0 for invalid slots
+      ssum += p;
+      float f[8];
+      unpack8(vf[u], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * f[e];
+    }
+    ssum = wave_sum(ssum) * 0.125f;  // each key counted once per lane of its row
+    if (lane == 0) red[1][wave] = ssum;
+  } else {
+    // ---- chunked: scores of every key into LDS, then softmax, then P.V ----
+    float mloc = NEG_BIG;
+    for (int c = 0; c < nkeys; c += DA_CHUNK) {
+      s16x8 kf[DA_U];
+#pragma unroll
+      for (int u = 0; u < DA_U; ++u) {
+        const int i = c + u * 32 + wave * 8 + slot;
+        kf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(kb + (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64) : s16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < DA_U; ++u) {
+        const int i = c + u * 32 + wave * 8 + slot;
+        if (i < nkeys) {
+          const float sv = slot_sum(dot8(qd, kf[u]));
+          mloc = fmaxf(mloc, sv);
+          if (sub == 0) sc[i] = sv;
+        }
+      }
+    }
+    mloc = wave_max(mloc);
+    if (lane == 0) red[0][wave] = mloc;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float ssum = 0.f;
+    for (int c = 0; c < nkeys; c += DA_CHUNK) {
+      s16x8 vf[DA_U];
+#pragma unroll
+      for (int u = 0; u < DA_U; ++u) {
+        const int i = c + u * 32 + wave * 8 + slot;
+        vf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(vb + (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64) : s16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < DA_U; ++u) {
+        const int i = c + u * 32 + wave * 8 + slot;
+        const float p = i < nkeys ? exp2f(sc[i] - m) : 0.f;
+        ssum += p;
+        float f[8];
+        unpack8(vf[u], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * f[e];
+      }
+    }
+    ssum = wave_sum(ssum) * 0.125f;
+    if (lane == 0) red[1][wave] = ssum;
   }
-  mloc = wave_max(mloc);
-  if ((tid & 63) == 0) red[tid >> 6] = mloc;
-  __syncthreads();
-  const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
-  float ssum = 0.f;
-  for (int i = tid; i < nkeys; i += 256) {
-    const float p = exp2f(sc[i] - m);
-    sc[i] = p;
-    ssum += p;
+  // ---- reduce acc over the 8 row slots of the wave, then over the 4 waves ----
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = acc[e];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    acc[e] = v;
   }
-  ssum = wave_sum(ssum);
-  if ((tid & 63) == 0) red[4 + (tid >> 6)] = ssum;
-  __syncthreads();
-  const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
-  const int d = tid & 63, grp = tid >> 6;
-  float acc = 0.f;
-  for (int i = grp; i < nkeys; i += 4) {
-    const int j = decode_key_at(g, i, pos, r0, c0, nc);
-    acc += sc[i] * bf2f(reinterpret_cast<const bf16_raw*>(vb)[(size_t)j * 64 + d]);
+  if (slot == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[wave][sub * 8 + e] = acc[e];
   }
-  part[grp][d] = acc;
   __syncthreads();
-  if (grp == 0) {
+  inv = 1.0f / (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  if (tid < 64) {
     const int b = bh / g.H, h = bh - b * g.H;
-    const float o = (part[0][d] + part[1][d] + part[2][d] + part[3][d]) * inv;
-    reinterpret_cast<bf16_raw*>(out)[(size_t)b * g.H * 64 + h * 64 + d] = f2bf(o);
+    const float o = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv;
+    reinterpret_cast<bf16_raw*>(out)[(size_t)b * g.H * 64 + h * 64 + tid] = f2bf(o);
   }
 }
 

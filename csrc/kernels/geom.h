@@ -38,4 +38,31 @@ struct GradSink {
   int split;
   int accumulate;     // 1: dst += v (the fp32 grad arena), 0: dst = v
 };
+
+// Decode-step skinny GEMM (skinny.hip): Y (M <= 64, N) = X (M, K) . W (N, K)^T + fused epilogue.
+// bf16 operands are passed as void pointers (this header is also compiled by the host compiler).
+struct SkinnyArgs {
+  const void* X;
+  const void* W;
+  const void* bias;  // bf16, may be null
+  int M, N, K, ldx;  // N: output columns (F for GEGLU: W holds 2F rows)
+  int KS;            // cross-workgroup split-K factor (must equal skinny_ks(M, N, K, G))
+  int steps;         // 128-wide K chunks per wave (set by skinny_gemm)
+  float* ws;         // KS * (N / 16) * ceil16(M) * 16 * (1 or 2) floats
+  int* cnt;          // >= N / 16 zero-initialised counters (self-resetting)
+  void* out;         // EPI 0 (bf16 or fp32), EPI 1 (bf16)
+  int out_f32;
+  float* resid;        // EPI 2: resid += scale * (y + bias), fp32 (M, N)
+  const float* scale;
+  void* q;           // EPI 3: rotary q (pre-scaled) -> q (M*H, 64); k, v -> caches (M*H, n, 64) at *pos
+  void* kc;
+  void* vc;
+  const float* cosT;
+  const float* sinT;
+  const int* pos;
+  int H, n;
+  float qscale;
+  int dbg;  // benchmark-only: bit 0 skips the X loads, bit 1 the W loads
+};
+
 }  // namespace dalle

@@ -73,6 +73,12 @@ class DecodeEngine:
         self.graph = None
         self._static_logits = None
         self._w = {}
+        # decode-step projections through the skinny MFMA GEMM (csrc/kernels/skinny.hip) with the
+        # rotary / GEGLU / LayerScale-residual epilogues fused: M = batch <= 64 rows
+        import os
+        self.skinny = (use_hip and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0
+                       and os.environ.get("DALLE_AMD_SKINNY", "1") != "0")
+        self.sk_cnt = torch.zeros(8192, dtype=torch.int32, device=dev) if self.skinny else None
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
     def _wt(self, p):
@@ -87,7 +93,7 @@ class DecodeEngine:
         keeps pointing at the same buffers, so weight updates between calls are still seen)."""
         self.pos.zero_()
         for p, w in self._w.values():
-            w.copy_(p.detach())
+            w.copy_(p.detach().reshape(w.shape))
         for k in self.kc + self.vc:
             k.zero_()
 
@@ -113,6 +119,40 @@ class DecodeEngine:
             out[:, :q] = hist[:, p - self.S, :q] if k >= self.S else 0.0
             out[:, q:h2] = hist[:, p - 1, q:h2] if k % self.S else 0.0
         return out
+
+    def _attn_res(self, li, ls, x_in, x_res):
+        """x_res += LayerScale * Attention(LN-shift(x_in)); one skinny GEMM each for QKV (+rotary into
+        the KV cache) and the output projection (+bias, LayerScale, residual) on the fused path."""
+        if not self.skinny:
+            return self._residual(x_res, self._attn(li, ls, x_in), ls)
+        from ..ops.hip_ops import C
+        attn = ls.fn.fn.fn
+        h = self._ln_shift(ls, self.hist[li][0], x_in)
+        C().skinny_qkv_rope_(h, self._wt(attn.to_qkv.weight), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li],
+                             self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
+        C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
+                         self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+        C().skinny_residual_(x_res, self.obuf, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias),
+                             self._scale(ls), self.sk_cnt)
+        return x_res
+
+    def _ff_res(self, li, ls, x_in, x_res):
+        """x_res += LayerScale * FF(LN-shift(x_in)): FF1 with GEGLU and FF2 with the residual fused."""
+        if not self.skinny:
+            return self._residual(x_res, self._ff(li, ls, x_in), ls)
+        from ..ops.hip_ops import C
+        ff = ls.fn.fn.fn
+        h = self._ln_shift(ls, self.hist[li][1], x_in)
+        a = C().skinny_geglu(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias), self.sk_cnt)
+        C().skinny_residual_(x_res, a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias), self._scale(ls), self.sk_cnt)
+        return x_res
+
+    def _scale(self, ls):
+        ent = self._w.get(("scale", id(ls.scale)))
+        if ent is None:
+            ent = (ls.scale, ls.scale.detach().reshape(-1).float().contiguous())
+            self._w[("scale", id(ls.scale))] = ent
+        return ent[1]
 
     def _attn(self, li, ls, x):
         attn = ls.fn.fn.fn
@@ -174,16 +214,20 @@ class DecodeEngine:
         if self.cfg.reversible:
             x1, x2 = x, x.clone()
             for li, (f, g) in enumerate(self.pairs):
-                x1 = self._residual(x1, self._attn(li, f, x2), f)
-                x2 = self._residual(x2, self._ff(li, g, x1), g)
+                x1 = self._attn_res(li, f, x2, x1)
+                x2 = self._ff_res(li, g, x1, x2)
             out = (x1 + x2) * 0.5
         else:
             for li, (f, g) in enumerate(self.pairs):
-                x = self._residual(x, self._attn(li, f, x), f)
-                x = self._residual(x, self._ff(li, g, x), g)
+                x = self._attn_res(li, f, x, x)
+                x = self._ff_res(li, g, x, x)
             out = x
         norm, head = self.model.to_logits[0], self.model.to_logits[1]
         h = F.layer_norm(out, (self.d,), norm.weight.detach(), norm.bias.detach())
+        if self.skinny:
+            from ..ops.hip_ops import C
+            return C().skinny_linear(h.to(self.cdt), self._wt(head.weight)[self.Vt:], self._wt(head.bias)[self.Vt:], True,
+                                     self.sk_cnt)
         return F.linear(h.to(self.cdt), self._wt(head.weight)[self.Vt:], self._wt(head.bias)[self.Vt:]).float()
 
     def _step(self):

@@ -23,6 +23,7 @@ hip_sources = [
     "csrc/kernels/decode.hip",
     "csrc/kernels/gemm.hip",
     "csrc/kernels/quant.hip",
+    "csrc/kernels/skinny.hip",
     "csrc/optim/lamb.hip",
 ]
 

@@ -16,8 +16,10 @@ def _cfg(reversible):
                           "shared_attn_ids": [0, 1, 2, 3], "shared_ff_ids": [0, 1, 0, 1]})
 
 
+@pytest.mark.parametrize("skinny", ["1", "0"])
 @pytest.mark.parametrize("reversible", [False, True])
-def test_hip_decode_matches_reference_decode(cuda, reversible):
+def test_hip_decode_matches_reference_decode(cuda, reversible, skinny, monkeypatch):
+    monkeypatch.setenv("DALLE_AMD_SKINNY", skinny)
     torch.manual_seed(0)
     cfg = _cfg(reversible)
     m = DALLE(cfg).eval()
@@ -27,6 +29,7 @@ def test_hip_decode_matches_reference_decode(cuda, reversible):
     ref = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False).teacher_forced_logits(m.prepare_text(text), img)
     mg = m.to(cuda)
     eng = DecodeEngine(mg, B, device=cuda, use_hip=True)
+    assert eng.skinny == (skinny == "1")
     out = eng.teacher_forced_logits(mg.prepare_text(text.to(cuda)), img.to(cuda)).cpu()
     rel = ((out - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
