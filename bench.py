@@ -29,6 +29,12 @@ from dalle_amd.models.dalle import DALLE  # noqa: E402
 from dalle_amd.optim import FlatArena, LAMB8bit  # noqa: E402
 from dalle_amd.parallel.dp import GradSync  # noqa: E402
 
+MODEL_NAMES = {
+    "bench24": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
+    "dalle-1024-24l": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
+    "reference": "DALL-E d_model=1024, 64 layers (5 shared blocks), reversible, 256 text + 32x32 image tokens",
+    "dalle-1.3b": "DALL-E ~1.3B, reversible, 256 text + 32x32 image tokens",
+}
 BASELINE_VALUE = None  # the reference publishes no throughput numbers
 
 
@@ -41,6 +47,10 @@ def parse():
     ap.add_argument("--model", default="bench24")
     ap.add_argument("--optim-bits", type=int, default=32, choices=[8, 32])
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--compression", default="none", choices=["none", "powersgd", "uniform8bit"],
+                    help="gradient averaging: plain bucketed all-reduce, PowerSGD rank-4 with error feedback "
+                         "(BASELINE config 3) or the hivemind size-adaptive fp16 / uniform-8-bit butterfly")
+    ap.add_argument("--powersgd-rank", type=int, default=4)
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: K more steps with per-phase timing (+ torch.profiler trace)")
     ap.add_argument("--trace", default="", help="chrome trace path for the --profile-steps pass")
@@ -84,6 +94,20 @@ def main():
     opt = LAMB8bit(groups, lr=0.0025, betas=(0.9, 0.96), eps=1e-6, weight_decay=0.045, clamp_value=10000.0,
                    max_grad_norm=4.0, reuse_grad_buffers=True, optim_bits=args.optim_bits, arena=arena)
     sync = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype)
+    if args.compression == "powersgd":
+        # compression work runs at every world size (the all-reduces are skipped only when world == 1)
+        from dalle_amd.parallel.powersgd import PowerSGD
+        psgd = PowerSGD([p for _, p in named], rank=args.powersgd_rank, seed=0)
+        reduce_grads = psgd.allreduce_
+    elif args.compression == "uniform8bit":
+        from dalle_amd.parallel.averaging import allreduce_weighted
+        from dalle_amd.parallel.compression import reference_averaging_compression
+        comp = reference_averaging_compression()
+
+        def reduce_grads():
+            allreduce_weighted(arena.grad, 1.0, compression=comp)  # a no-op on one GPU
+    else:
+        reduce_grads = sync.all_reduce
 
     gen = torch.Generator().manual_seed(1000 + rank)
     batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
@@ -100,7 +124,7 @@ def main():
         with phase("backward"):
             loss.backward()
         with phase("grad_allreduce"):
-            sync.all_reduce()
+            reduce_grads()
         with phase("optimizer"):
             opt.step()
         return loss
@@ -143,11 +167,13 @@ def main():
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
             "dtype": "bf16",
             "data": "synthetic LAION-shaped pairs (256 caption ids + 32x32 VQGAN codes), random-init weights",
-            "config": {"model": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
+            "config": {"model": MODEL_NAMES.get(args.model, args.model),
                        "preset": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": cfg.seq_len, "parallelism": f"dp{world}",
                        "optimizer": f"LAMB ({args.optim_bits}-bit moments) + global clip 4.0",
-                       "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning},
+                       "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning,
+                       "grad_compression": args.compression if args.compression != "powersgd"
+                       else f"powersgd-rank{args.powersgd_rank}"},
             "model_tflops_per_gpu": round(tflops, 1),
             "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1),
             "loss": round(final_loss, 4),

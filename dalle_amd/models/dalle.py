@@ -170,6 +170,17 @@ class Transformer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         pairs = self.layers.pairs()
+        if self.cfg.reversible and ops.fused_reversible_available(x):
+            cfg = self.cfg
+            layers = []
+            for f, g in pairs:
+                pre, attn = f.fn, f.fn.fn.fn
+                gpre, ff = g.fn, g.fn.fn.fn
+                layers.append(((pre.norm.weight, pre.norm.bias, attn.to_qkv.weight, attn.to_out[0].weight, attn.to_out[0].bias,
+                                f.scale, attn.heads, attn.attn_type, pre.fn.enabled),
+                               (gpre.norm.weight, gpre.norm.bias, ff.net[0].weight, ff.net[0].bias, ff.net[3].weight,
+                                ff.net[3].bias, g.scale, gpre.fn.enabled)))
+            return ops.reversible_stack(x, layers, self.geom, cfg.text_len, cfg.image_fmap_size)
         if self.cfg.reversible:
             fns = [(lambda t, f=f: ops.scale_rows(self._attn_out(f, t), f.scale),
                     lambda t, g=g: ops.scale_rows(self._ff_out(g, t), g.scale)) for f, g in pairs]

@@ -116,6 +116,16 @@ def ff_sublayer(x, ln_w, ln_b, w1, b1, w2, b2, scale, text_len: int, image_size:
     return proj_residual(x, ff_hidden(h, w1, b1), w2, b2, scale)
 
 
+def fused_reversible_available(x) -> bool:
+    """True when the reversible stack can run on the fused HIP sublayers (``hip_ops.reversible_stack``)."""
+    return x.is_cuda and backend_for(x) == "hip" and os.environ.get("DALLE_AMD_FUSED_REVERSIBLE", "1") != "0"
+
+
+def reversible_stack(x, layers, geom, text_len: int, image_size: int):
+    """Reversible residual stack over the fused attention / FF sublayers (HIP only)."""
+    return _hip().reversible_stack(x, layers, geom, text_len, image_size)
+
+
 def begin_forward():
     """Start of a model forward: drops the per-forward bf16 weight casts of the HIP path."""
     if hip_available():

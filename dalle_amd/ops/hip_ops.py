@@ -305,109 +305,219 @@ def _sinks(params, needs):
     return None
 
 
+def _attn_fwd(res, inp, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta, save: bool, sign: float = 1.0):
+    """res + sign * scale * to_out(attn(rope(to_qkv(LN_shift(inp))))); returns (out, saved-or-None)."""
+    T, S, K, H, pattern, shift = meta
+    inp = inp.contiguous()
+    B, n, d = inp.shape
+    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    h2 = h.view(-1, d)
+    wq = bf16_weight(w_qkv)
+    col = pattern == PATTERN_IDS["axial_col"]
+    if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
+        # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
+        q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
+    else:
+        qkv = torch.mm(h2, wq.t()).view(B, n, -1)
+        q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+        del qkv
+    out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
+    wo = bf16_weight(w_out)
+    y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())
+    s = scale.reshape(-1).contiguous()
+    xo = torch.empty_like(res)
+    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
+    if not save:
+        return xo, None
+    return xo, (inp, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, (B, n, T, S, K, H, pattern, shift, col))
+
+
+def _attn_bwd(saved, params, needs, g, resid):
+    """Backward of ``_attn_fwd`` for the branch upstream grad ``g`` (fp32): returns (d inp + resid,
+    dln_w, dln_b, dw_qkv, dw_out, db_out, dscale); the parameter grads are None when they went to the
+    arena sinks. ``resid`` (fp32, may be None) is added to d inp inside the LayerNorm-backward kernel."""
+    x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, geo = saved
+    ln_w, ln_b, w_qkv, w_out, b_out, scale = params
+    B, n, T, S, K, H, pattern, shift, col = geo
+    g = g.contiguous()
+    sk = _sinks(params, needs)
+    if sk is not None:
+        dy, _, _ = C().scale_residual_bwd(g, y, s, sk[5], sk[4])
+        db = dscale = None
+    else:
+        dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
+        db, dscale = gsum * s, dscale.view(scale.shape)
+    dy = dy.view(-1, dy.shape[-1])
+    o2 = out.view(-1, out.shape[-1])
+    do = torch.mm(dy, wo).view(out.shape)
+    dwo = weight_grad(w_out, dy, o2)
+    dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
+    del do
+    dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
+    del dq, dk, dv
+    dh = torch.mm(dqkv, wq).view(x.shape)
+    dwq = weight_grad(w_qkv, dqkv, h2)
+    resid = resid.contiguous() if resid is not None else None
+    if sk is not None:
+        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid, sk[0], sk[1])
+    else:
+        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid)
+    return dx, dlw, dlb, dwq, dwo, db, dscale
+
+
+def _ff_fwd(res, inp, ln_w, ln_b, w1, b1, w2, b2, scale, meta, save: bool, sign: float = 1.0):
+    """res + sign * scale * (W2 GEGLU(W1 LN_shift(inp) + b1) + b2); returns (out, saved-or-None)."""
+    T, S, shift = meta
+    inp = inp.contiguous()
+    d = inp.shape[-1]
+    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    h2 = h.view(-1, d)
+    w1b, w2b = bf16_weight(w1), bf16_weight(w2)
+    a = torch.addmm(bf16_weight(b1), h2, w1b.t())
+    u = C().geglu_fwd(a)
+    if not save:
+        del a
+    y = torch.addmm(bf16_weight(b2), u, w2b.t())
+    s = scale.reshape(-1).contiguous()
+    xo = torch.empty_like(res)
+    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
+    if not save:
+        return xo, None
+    return xo, (inp, mean, rstd, h2, w1b, a, u, w2b, y, s, meta)
+
+
+def _ff_bwd(saved, params, needs, g, resid):
+    """Backward of ``_ff_fwd`` (same contract as ``_attn_bwd``)."""
+    x, mean, rstd, h2, w1b, a, u, w2b, y, s, meta = saved
+    ln_w, ln_b, w1, b1, w2, b2, scale = params
+    T, S, shift = meta
+    g = g.contiguous()
+    sk = _sinks(params, needs)
+    if sk is not None:
+        dy, _, _ = C().scale_residual_bwd(g, y, s, sk[6], sk[5])
+        db2 = dscale = None
+    else:
+        dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
+        db2, dscale = gsum * s, dscale.view(scale.shape)
+    dy = dy.view(-1, dy.shape[-1])
+    du = torch.mm(dy, w2b)
+    dw2 = weight_grad(w2, dy, u)
+    da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
+    del du
+    dh = torch.mm(da, w1b).view(x.shape)
+    dw1 = weight_grad(w1, da, h2)
+    resid = resid.contiguous() if resid is not None else None
+    if sk is not None:
+        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid, sk[0], sk[1])
+    else:
+        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid)
+    return dx, dlw, dlb, dw1, db1, dw2, db2, dscale
+
+
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta):
-        T, S, K, H, pattern, shift = meta
-        x = x.contiguous()
-        B, n, d = x.shape
-        h, mean, rstd = C().ln_shift_fwd(x, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
-        h2 = h.view(-1, d)
-        wq = bf16_weight(w_qkv)
-        col = pattern == PATTERN_IDS["axial_col"]
-        if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
-            # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
-            q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
-        else:
-            qkv = torch.mm(h2, wq.t()).view(B, n, -1)
-            q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
-            del qkv
-        out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
-        wo = bf16_weight(w_out)
-        y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())
-        s = scale.reshape(-1).contiguous()
-        xo = torch.empty_like(x)
-        C().scale_residual_out(x, y, s, xo)
-        ctx.save_for_backward(x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin)
+        xo, saved = _attn_fwd(x, x, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta, save=True)
+        ctx.saved = saved
         ctx.params = (ln_w, ln_b, w_qkv, w_out, b_out, scale)
-        ctx.meta = (B, n, T, S, K, H, pattern, shift, col)
         return xo
 
     @staticmethod
     def backward(ctx, g):
-        x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin = ctx.saved_tensors
-        ln_w, ln_b, w_qkv, w_out, b_out, scale = ctx.params
-        B, n, T, S, K, H, pattern, shift, col = ctx.meta
+        saved, ctx.saved = ctx.saved, None
         g = g.contiguous()
-        sk = _sinks(ctx.params, ctx.needs_input_grad[1:7])
-        if sk is not None:
-            dy, _, _ = C().scale_residual_bwd(g, y, s, sk[5], sk[4])
-            db = dscale = None
-        else:
-            dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
-            db, dscale = gsum * s, dscale.view(scale.shape)
-        dy = dy.view(-1, dy.shape[-1])
-        o2 = out.view(-1, out.shape[-1])
-        do = torch.mm(dy, wo).view(out.shape)
-        dwo = weight_grad(w_out, dy, o2)
-        dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
-        del do
-        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
-        del dq, dk, dv
-        dh = torch.mm(dqkv, wq).view(x.shape)
-        dwq = weight_grad(w_qkv, dqkv, h2)
-        if sk is not None:
-            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
-        else:
-            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g)
-        return dx, dlw, dlb, dwq, dwo, db, dscale, None, None, None
+        grads = _attn_bwd(saved, ctx.params, ctx.needs_input_grad[1:7], g, g)
+        return (*grads, None, None, None)
 
 
 class _FFSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, w1, b1, w2, b2, scale, meta):
-        T, S, shift = meta
-        x = x.contiguous()
-        d = x.shape[-1]
-        h, mean, rstd = C().ln_shift_fwd(x, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
-        h2 = h.view(-1, d)
-        w1b, w2b = bf16_weight(w1), bf16_weight(w2)
-        a = torch.addmm(bf16_weight(b1), h2, w1b.t())
-        u = C().geglu_fwd(a)
-        y = torch.addmm(bf16_weight(b2), u, w2b.t())
-        s = scale.reshape(-1).contiguous()
-        xo = torch.empty_like(x)
-        C().scale_residual_out(x, y, s, xo)
-        ctx.save_for_backward(x, mean, rstd, h2, w1b, a, u, w2b, y, s)
+        xo, saved = _ff_fwd(x, x, ln_w, ln_b, w1, b1, w2, b2, scale, meta, save=True)
+        ctx.saved = saved
         ctx.params = (ln_w, ln_b, w1, b1, w2, b2, scale)
-        ctx.meta = meta
         return xo
 
     @staticmethod
     def backward(ctx, g):
-        x, mean, rstd, h2, w1b, a, u, w2b, y, s = ctx.saved_tensors
-        ln_w, ln_b, w1, b1, w2, b2, scale = ctx.params
-        T, S, shift = ctx.meta
+        saved, ctx.saved = ctx.saved, None
         g = g.contiguous()
-        sk = _sinks(ctx.params, ctx.needs_input_grad[1:8])
-        if sk is not None:
-            dy, _, _ = C().scale_residual_bwd(g, y, s, sk[6], sk[5])
-            db2 = dscale = None
-        else:
-            dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
-            db2, dscale = gsum * s, dscale.view(scale.shape)
-        dy = dy.view(-1, dy.shape[-1])
-        du = torch.mm(dy, w2b)
-        dw2 = weight_grad(w2, dy, u)
-        da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
-        del du
-        dh = torch.mm(da, w1b).view(x.shape)
-        dw1 = weight_grad(w1, da, h2)
-        if sk is not None:
-            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
-        else:
-            dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, g)
-        return dx, dlw, dlb, dw1, db1, dw2, db2, dscale, None
+        grads = _ff_bwd(saved, ctx.params, ctx.needs_input_grad[1:8], g, g)
+        return (*grads, None)
+
+
+# ---------------------------------------------------------------------------------------------
+# Reversible stack over the fused sublayers (SURVEY D3 / K11). Forward: y1 = x1 + f(x2),
+# y2 = x2 + g(y1) with nothing saved but the final (y1, y2). Backward per block, newest first:
+#   x2 = y2 - g(y1)  (the fused FF sublayer run with sign -1, saving its activations)
+#   dy1 += g'(y1)^T dy2   (its hand-written backward; the residual add happens inside the LN-bwd kernel)
+#   x1 = y1 - f(x2); dy2 += f'(x2)^T dy1   (same with the attention sublayer)
+# so the recompute costs exactly one forward per block and no autograd graph is built.
+# ---------------------------------------------------------------------------------------------
+class _ReversibleFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blocks, *params):
+        x1 = x2 = x.contiguous()
+        with torch.no_grad():
+            for fa, ga in blocks:
+                x1, _ = _attn_fwd(x1, x2, *fa[0], save=False)
+                x2, _ = _ff_fwd(x2, x1, *ga[0], save=False)
+        ctx.blocks = blocks
+        ctx.params = params
+        ctx.save_for_backward(x1, x2)
+        return (x1 + x2) * 0.5
+
+    @staticmethod
+    def backward(ctx, gout):
+        y1, y2 = ctx.saved_tensors
+        blocks = ctx.blocks
+        dy1 = dy2 = (gout.float() * 0.5).contiguous()
+        pending: Dict[int, torch.Tensor] = {}  # grads that found no arena sink, keyed by id(param)
+
+        def collect(plist, grads):
+            for p, gr in zip(plist, grads):
+                if gr is None:
+                    continue
+                k = id(p)
+                pending[k] = gr if k not in pending else pending[k] + gr
+
+        with torch.no_grad():
+            for fa, ga in reversed(blocks):
+                g_args, g_params = ga
+                x2, saved = _ff_fwd(y2, y1, *g_args, save=True, sign=-1.0)
+                res = _ff_bwd(saved, g_params, [p.requires_grad for p in g_params], dy2, dy1)
+                del saved
+                dy1 = res[0]
+                collect(g_params, res[1:])
+                f_args, f_params = fa
+                x1, saved = _attn_fwd(y1, x2, *f_args, save=True, sign=-1.0)
+                res = _attn_bwd(saved, f_params, [p.requires_grad for p in f_params], dy1, dy2)
+                del saved
+                dy2 = res[0]
+                collect(f_params, res[1:])
+                y1, y2 = x1, x2
+        dx = dy1 + dy2
+        return (dx, None, *[pending.get(id(p)) for p in ctx.params])
+
+
+def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int):
+    """``layers``: per block ((ln_w, ln_b, w_qkv, w_out, b_out, scale, heads, attn_type, shift),
+    (ln_w, ln_b, w1, b1, w2, b2, scale, shift)). Returns mean(y1, y2) of the reversible stack."""
+    blocks, uniq, seen = [], [], set()
+    for (aln_w, aln_b, w_qkv, w_out, b_out, ascale, heads, attn_type, ashift), (fln_w, fln_b, w1, b1, w2, b2, fscale, fshift) in layers:
+        dim_head = w_qkv.shape[0] // 3 // heads
+        assert dim_head == 64, "the HIP attention kernels are specialised for dim_head = 64"
+        cos, sin = _rope_tables(geom, dim_head, x.device)
+        ameta = (geom.text_len, geom.image_size, geom.kernel_size, heads, PATTERN_IDS[attn_type], bool(ashift))
+        aparams = (aln_w, aln_b, w_qkv, w_out, b_out, ascale)
+        fparams = (fln_w, fln_b, w1, b1, w2, b2, fscale)
+        blocks.append((((*aparams, cos, sin, ameta), aparams),
+                       ((*fparams, (text_len, image_size, bool(fshift))), fparams)))
+        for p in aparams + fparams:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+    return _ReversibleFused.apply(x, blocks, *uniq)
 
 
 def attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):
