@@ -34,6 +34,8 @@ std::vector<int> skinny_shape_info(int, int, int, int);
 bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
                    float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
+void psgd_orthonormalize(float*, const long*, const int*, int, int, float, hipStream_t);
+bool psgd_reconstruct(float*, float*, const float*, const float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
                      hipStream_t);
@@ -542,6 +544,36 @@ void lamb_step(Tensor p, Tensor g, Tensor delta, Tensor q1, Tensor q2, Tensor ab
                    (float)eps, (float)clamp_value, use_clip ? 1 : 0, cur_stream());
 }
 
+// ---------------------------------------------------------------------------------------------
+// PowerSGD: in-place column orthonormalisation of every P factor (flat buffer, one launch) and the
+// fused rank-r reconstruction + error-feedback update
+void psgd_orthonormalize_(Tensor P, Tensor offsets, Tensor rows, int64_t r, double eps) {
+  CHECK_IN(P, torch::kFloat32); CHECK_IN(offsets, torch::kInt64); CHECK_IN(rows, torch::kInt32);
+  TORCH_CHECK(r >= 1 && r <= 8, "psgd: rank must be in [1, 8]");
+  TORCH_CHECK(offsets.numel() == rows.numel() && offsets.device() == P.device() && rows.device() == P.device());
+  const int nmat = rows.numel();
+  if (nmat == 0) return;
+  // host-side bounds check of the layout the kernel walks (tiny tensors)
+  auto oc = offsets.cpu(), rc = rows.cpu();
+  const long* o = oc.data_ptr<int64_t>();
+  const int* rr = rc.data_ptr<int>();
+  for (int i = 0; i < nmat; ++i)
+    TORCH_CHECK(o[i] >= 0 && rr[i] >= 0 && o[i] + (long)rr[i] * r <= P.numel(), "psgd_orthonormalize: matrix ", i, " out of bounds");
+  dalle::psgd_orthonormalize(P.data_ptr<float>(), offsets.data_ptr<int64_t>(), rows.data_ptr<int>(), nmat, (int)r, (float)eps,
+                             cur_stream());
+}
+
+void psgd_reconstruct_(Tensor grad, Tensor E, Tensor P, Tensor Q) {
+  CHECK_IN(grad, torch::kFloat32); CHECK_IN(E, torch::kFloat32); CHECK_IN(P, torch::kFloat32); CHECK_IN(Q, torch::kFloat32);
+  TORCH_CHECK(E.dim() == 2 && P.dim() == 2 && Q.dim() == 2, "psgd_reconstruct: E (n, m), P (n, r), Q (m, r)");
+  const long n = E.size(0);
+  const int m = E.size(1), r = P.size(1);
+  TORCH_CHECK(P.size(0) == n && Q.size(0) == m && Q.size(1) == r && grad.numel() == E.numel());
+  TORCH_CHECK(dalle::psgd_reconstruct(grad.data_ptr<float>(), E.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(), n, m, r,
+                                      cur_stream()),
+              "psgd_reconstruct: needs m % 4 == 0 and rank in {1, 2, 4, 8}");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dalle_amd HIP/CDNA4 kernels (gfx950)";
   m.def("ln_shift_fwd", &ln_shift_fwd);
@@ -561,6 +593,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
+  m.def("psgd_orthonormalize_", &psgd_orthonormalize_);
+  m.def("psgd_reconstruct_", &psgd_reconstruct_);
   m.def("qkv_rope", &qkv_rope);
   m.def("uq8_compress", &uq8_compress);
   m.def("uq8_dequant_", &uq8_dequant_);

@@ -52,40 +52,66 @@ class PowerSGD:
             dist.all_reduce(flat, group=self.group)
             flat.div_(world)
 
+    def _native(self) -> bool:
+        """HIP path: fused Gram-Schmidt + reconstruction kernels (csrc/kernels/powersgd.hip)."""
+        if not self.low_rank or not self.low_rank[0].is_cuda or self.rank not in (1, 2, 4, 8):
+            return False
+        from ..ops.ext import load_extension
+        self._C = load_extension(required=True)
+        return all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                   and (p.numel() // p.shape[0]) % 4 == 0 for p in self.low_rank)
+
     @torch.no_grad()
     def allreduce_(self, grads: Optional[List[torch.Tensor]] = None, scale: float = 1.0):
         """Average the ``.grad`` of the managed params in place (weighted by ``scale`` per peer:
         pass ``w_p * world / sum(w)`` for a sample-weighted mean)."""
         world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        Ms = [p.grad.reshape(p.shape[0], -1).float() * scale for p in self.low_rank]
-        if self.error_feedback:
-            Ms = [M + E for M, E in zip(Ms, self.E)]
-        # --- P = M Q, all-reduced in one flat buffer
-        Ps = [M @ Q for M, Q in zip(Ms, self.Q)]
-        if Ps:
-            flatP = torch.cat([P.reshape(-1) for P in Ps])
-            self._allreduce_mean(flatP, world)
-            off = 0
-            for i, P in enumerate(Ps):
-                k = P.numel()
-                Ps[i] = torch.linalg.qr(flatP[off:off + k].view_as(P), mode="reduced")[0]
-                off += k
-        # --- Q = M^T P, all-reduced
-        Qs = [M.t() @ P for M, P in zip(Ms, Ps)]
-        if Qs:
-            flatQ = torch.cat([Q.reshape(-1) for Q in Qs])
-            self._allreduce_mean(flatQ, world)
-            off = 0
-            for i, Q in enumerate(Qs):
-                k = Q.numel()
-                self.Q[i] = flatQ[off:off + k].view_as(Q).clone()
-                off += k
-        # --- reconstruct + error feedback
-        for i, (p, M, P) in enumerate(zip(self.low_rank, Ms, Ps)):
-            approx = P @ self.Q[i].t()
+        native = self._native()
+        r = self.rank
+        # M_e = scale * grad (+ E): accumulated in place into the error buffer
+        Ms = []
+        for i, p in enumerate(self.low_rank):
+            g = p.grad.reshape(p.shape[0], -1)
             if self.error_feedback:
-                self.E[i] = M - approx
-            p.grad.copy_(approx.view_as(p.grad))
+                Ms.append(self.E[i].add_(g.float(), alpha=scale))
+            else:
+                Ms.append(g.float() * scale)
+        if Ms:
+            dev = Ms[0].device
+            rows = [M.shape[0] for M in Ms]
+            cols = [M.shape[1] for M in Ms]
+            flatP = torch.empty(sum(rows) * r, dtype=torch.float32, device=dev)
+            Ps, off = [], 0
+            for M, Q, n in zip(Ms, self.Q, rows):
+                P = flatP[off:off + n * r].view(n, r)
+                torch.mm(M, Q, out=P)  # P = M Q
+                Ps.append(P)
+                off += n * r
+            self._allreduce_mean(flatP, world)
+            if native:
+                offs = torch.tensor([0] + [n * r for n in rows[:-1]], dtype=torch.int64).cumsum(0).to(dev)
+                self._C.psgd_orthonormalize_(flatP, offs, torch.tensor(rows, dtype=torch.int32, device=dev), r, 1e-8)
+            else:
+                for P in Ps:
+                    P.copy_(torch.linalg.qr(P, mode="reduced")[0])
+            flatQ = torch.empty(sum(cols) * r, dtype=torch.float32, device=dev)
+            Qs, off = [], 0
+            for M, P, m in zip(Ms, Ps, cols):
+                Qn = flatQ[off:off + m * r].view(m, r)
+                torch.mm(M.t(), P, out=Qn)  # Q = M^T P
+                Qs.append(Qn)
+                off += m * r
+            self._allreduce_mean(flatQ, world)
+            self.Q = Qs
+            # reconstruct M^ = P Q^T into .grad; error feedback E = M_e - M^
+            for p, M, P, Qn in zip(self.low_rank, Ms, Ps, Qs):
+                if native:
+                    self._C.psgd_reconstruct_(p.grad, M, P, Qn)
+                else:
+                    approx = P @ Qn.t()
+                    if self.error_feedback:
+                        M.sub_(approx)
+                    p.grad.copy_(approx.view_as(p.grad))
         # --- small / 1-D tensors uncompressed
         if self.plain:
             flat = torch.cat([p.grad.reshape(-1).float() * scale for p in self.plain])
