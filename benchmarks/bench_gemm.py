@@ -27,10 +27,33 @@ def timeit(fn, reps=20, warmup=3):
     return ts[len(ts) // 2]
 
 
+def wgrad_sweep(M):
+    """dW (N x K, fp32) = g^T x over M tokens: one GEMM with fp32 out (accumulate, beta=1) vs split-K
+    batched GEMMs (fp32 partials) + the deterministic fold, as dalle_amd.ops.hip_ops.weight_grad runs them."""
+    C = load_extension(required=True)
+    dev = torch.device("cuda")
+    for N, K in [(3072, 1024), (1024, 1024), (8192, 1024), (1024, 4096)]:
+        g = torch.randn(M, N, device=dev).bfloat16()
+        x = torch.randn(M, K, device=dev).bfloat16()
+        acc = torch.zeros(N, K, device=dev)
+        fl = 2 * M * N * K
+        res = {"shape": f"wgrad_M{M}_N{N}_K{K}"}
+        res["s1_TF"] = round(fl / timeit(lambda: torch.addmm(acc, g.t(), x, out_dtype=torch.float32, out=acc)) / 1e9)
+        for s in (2, 4, 8):
+            def f(s=s):
+                part = torch.bmm(g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
+                C.splitk_accum_(acc, part, True)
+            res[f"s{s}_TF"] = round(fl / timeit(f) / 1e9)
+        print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=61440)
+    ap.add_argument("--wgrad", action="store_true", help="weight-grad shapes: dW = g^T x, split-K sweep")
     args = ap.parse_args()
+    if args.wgrad:
+        return wgrad_sweep(args.m)
     C = load_extension(required=True)
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -56,12 +79,14 @@ def main():
         t_lt = timeit(lambda: torch.addmm(bias, A, B.t()))
         t_me = timeit(lambda: C.gemm_nt(A, B, bias))
         t_v1 = timeit(lambda: C.gemm_nt(A, B, bias, 200))
-        opts = {o: round(fl / timeit(lambda: C.gemm_nt(A, B, bias, 200 + o)) / 1e9) for o in range(8)}
+        opts = {o: round(fl / timeit(lambda: C.gemm_nt(A, B, bias, o)) / 1e9) for o in (202, 300, 301)}
+        opts["hipblaslt_again"] = round(fl / timeit(lambda: torch.addmm(bias, A, B.t())) / 1e9)
+        e8 = (C.gemm_nt(A, B, bias, 300).float() - torch.addmm(bias, A, B.t()).float()).abs().max().item()
         e2 = ((C.gemm_nt(A, B, bias, 200).float() - torch.addmm(bias, A, B.t()).float()).norm() /
               torch.addmm(bias, A, B.t()).float().norm()).item()
         e = ((C.gemm_nt(A, B, bias).float() - torch.addmm(bias, A, B.t()).float()).norm() /
              torch.addmm(bias, A, B.t()).float().norm()).item()
-        print(json.dumps({"shape": f"M{M}_N{N}_K{K}", "hipblaslt_TF": round(fl / t_lt / 1e9), "ours_TF": round(fl / t_me / 1e9), "ours_phased_TF": round(fl / t_v1 / 1e9), "phased_err": e2, "opts_TF": opts,
+        print(json.dumps({"shape": f"M{M}_N{N}_K{K}", "hipblaslt_TF": round(fl / t_lt / 1e9), "ours_TF": round(fl / t_me / 1e9), "ours_phased_TF": round(fl / t_v1 / 1e9), "phased_err": e2, "8ph_maxdiff": e8, "opts_TF": opts,
                           "hipblaslt_ms": round(t_lt, 4), "ours_ms": round(t_me, 4), "rel_err_vs_hipblaslt": e}), flush=True)
 
 

@@ -208,6 +208,74 @@ __device__ __forceinline__ void stage_half(const __bf16* __restrict__ src, int l
   }
 }
 
+// Shared epilogue of the phased kernels: stage each wave's 128 x 64 accumulator tile (bf16) through
+// LDS, then EPI 0 = 16-byte row stores (+bias), EPI 1 = rotary + scatter into the attention storage.
+// All LDS operand reads and DMA must be retired by the caller (the whole 128 KiB is reused).
+template <int EPI>
+__device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16* smem, __bf16* __restrict__ C,
+                                                    const __bf16* __restrict__ bias, int N, int row0, int col0, int wave,
+                                                    int lane, const RopeEpi& rope) {
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  __bf16* ep = smem + wave * (128 * 64);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + fr;
+    float bv = 0.f;
+    if (bias != nullptr) bv = (float)bias[col0 + wn * 64 + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + fq * 4 + r;
+        ep[row * 64 + (((c >> 3) ^ (row & 7)) << 3) + (c & 7)] = (__bf16)(acc[i][j][r] + bv);
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (EPI == 0) {
+    __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, ch = idx & 7;
+      const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
+      *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+    }
+  } else {
+    // the wave's 64 columns are exactly one (part, head): rotate each 8-column chunk of each row and
+    // scatter the row to its storage slot
+    const int HD = rope.H * 64;
+    const int c0 = col0 + wn * 64;
+    const int part = c0 / HD, h = (c0 - part * HD) >> 6;
+    __bf16* dstT = part == 0 ? rope.q : (part == 1 ? rope.k : rope.v);
+    const float sc = part == 0 ? rope.qscale : 1.0f;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, ch = idx & 7;
+      const int r = row0 + wm * 128 + row;
+      const int b = r / rope.n, p = r - b * rope.n;
+      float x[8], cs[8], sn[8];
+      unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), x);
+      const float* cp = rope.cosT + (size_t)p * 64 + ch * 8;
+      const float* sp = rope.sinT + (size_t)p * 64 + ch * 8;
+      *reinterpret_cast<f32x4*>(cs) = *reinterpret_cast<const f32x4*>(cp);
+      *reinterpret_cast<f32x4*>(cs + 4) = *reinterpret_cast<const f32x4*>(cp + 4);
+      *reinterpret_cast<f32x4*>(sn) = *reinterpret_cast<const f32x4*>(sp);
+      *reinterpret_cast<f32x4*>(sn + 4) = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const float a0 = x[i], a1 = x[i + 1];
+        x[i] = (a0 * cs[i] + a1 * sn[i]) * sc;
+        x[i + 1] = (a1 * cs[i + 1] + a0 * sn[i + 1]) * sc;
+      }
+      const int srow = rope_epi_seq2st(rope, p);
+      *reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8) = pack8(x);
+    }
+  }
+}
+
 template <int EPI, int OPT>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                       __bf16* __restrict__ C, const __bf16* __restrict__ bias,
@@ -307,64 +375,163 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- epilogue (as in gemm_nt_kernel) ----
-  __bf16* ep = smem + wave * (128 * 64);
+  gemm_store_epilogue<EPI>(acc, smem, C, bias, N, row0, col0, wave, lane, rope);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 8-phase template (cdna_hip_programming.md §5 "The 256^2 8-phase template", T3+T4+T5), re-derived:
+// the same 256x256x64 tile, half-tile images and quadrant order as gemm_nt_phased_kernel, but
+//   * each phase is {ds_read subtile ; 1 half-tile LDS-DMA ; s_barrier ; lgkmcnt(0) ; 16 MFMA ;
+//     s_barrier} and the two wave rows run STAGGERED by one barrier (wm == 1 enters one barrier
+//     late), so on every SIMD one wave issues MFMAs while its partner reads LDS / issues DMA;
+//   * three half-tiles stay in flight: the counted vmcnt(6) runs once per K-tile (phase 4), never 0
+//     in the steady state. Staging order per K-tile t (consumption order is A-lo B-lo | B-hi | A-hi):
+//       phase 1: A-hi(t+1) -> buf^1   (A-hi of buf^1 last read 2 phases ago)
+//       phase 2: B-lo(t+2) -> buf     (B-lo read in phase 1, retired by its lgkmcnt(8) before phase 1's
+//                                      first barrier, so 1 phase later is safe for both wave rows)
+//       phase 3: A-lo(t+2) -> buf     (read in phase 1, 2 phases ago)
+//       phase 4: B-hi(t+2) -> buf     (read in phase 2, 2 phases ago); then vmcnt(6) retires A-hi(t+1),
+//                                      the last half of K-tile t+1, before phase 4's first barrier
+//     so K-tile t+1 is complete for every wave before any wave's phase-5 reads (RAW), even for the
+//     lagging wave row.
+// ------------------------------------------------------------------------------------------------
+template <int EPI, int OPT>
+__global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                                   __bf16* __restrict__ C, const __bf16* __restrict__ bias,
+                                                                   int M, int N, int K, RopeEpi rope) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];  // [buf][A-lo | B-lo | B-hi | A-hi]
+  constexpr bool STAGGER = !(OPT & 1);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(tm, tn, M / GBM, N / GBN);
+  const int row0 = tm * GBM, col0 = tn * GBN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4_t acc[8][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = j * 16 + fr;
-    float bv = 0.f;
-    if (bias != nullptr) bv = (float)bias[col0 + wn * 64 + c];
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i * 16 + fq * 4 + r;
-        ep[row * 64 + (((c >> 3) ^ (row & 7)) << 3) + (c & 7)] = (__bf16)(acc[i][j][r] + bv);
-      }
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  if (EPI == 0) {
-    __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx >> 3, ch = idx & 7;
-      const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
-      *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
-    }
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto slot = [&](int buf, int which) { return smem + (buf * 4 + which) * HALF; };
+  // which: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
+  auto stage = [&](int t, int which) {
+    const int buf = t & 1, k0 = t * GBK;
+    if (which == 0) stage_half(A, K, row0, k0, slot(buf, 0), wave, lane, 64, 0);
+    else if (which == 1) stage_half(B, K, col0, k0, slot(buf, 1), wave, lane, 32, 0);
+    else if (which == 2) stage_half(B, K, col0, k0, slot(buf, 2), wave, lane, 32, 32);
+    else stage_half(A, K, row0, k0, slot(buf, 3), wave, lane, 64, 64);
+  };
+
+  const int nk = K / GBK;
+  stage(0, 1); stage(0, 0); stage(0, 2); stage(0, 3);
+  if (nk > 1) {
+    stage(1, 1); stage(1, 0); stage(1, 2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
-    // the wave's 64 columns are exactly one (part, head): rotate each 8-column chunk of each row and
-    // scatter the row to its storage slot
-    const int HD = rope.H * 64;
-    const int c0 = col0 + wn * 64;
-    const int part = c0 / HD, h = (c0 - part * HD) >> 6;
-    __bf16* dstT = part == 0 ? rope.q : (part == 1 ? rope.k : rope.v);
-    const float sc = part == 0 ? rope.qscale : 1.0f;
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx >> 3, ch = idx & 7;
-      const int r = row0 + wm * 128 + row;
-      const int b = r / rope.n, p = r - b * rope.n;
-      float x[8], cs[8], sn[8];
-      unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), x);
-      const float* cp = rope.cosT + (size_t)p * 64 + ch * 8;
-      const float* sp = rope.sinT + (size_t)p * 64 + ch * 8;
-      *reinterpret_cast<f32x4*>(cs) = *reinterpret_cast<const f32x4*>(cp);
-      *reinterpret_cast<f32x4*>(cs + 4) = *reinterpret_cast<const f32x4*>(cp + 4);
-      *reinterpret_cast<f32x4*>(sn) = *reinterpret_cast<const f32x4*>(sp);
-      *reinterpret_cast<f32x4*>(sn + 4) = *reinterpret_cast<const f32x4*>(sp + 4);
-#pragma unroll
-      for (int i = 0; i < 8; i += 2) {
-        const float a0 = x[i], a1 = x[i + 1];
-        x[i] = (a0 * cs[i] + a1 * sn[i]) * sc;
-        x[i + 1] = (a1 * cs[i + 1] + a0 * sn[i + 1]) * sc;
-      }
-      const int srow = rope_epi_seq2st(rope, p);
-      *reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8) = pack8(x);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  asm volatile("s_barrier" ::: "memory");
+  if (STAGGER && wm == 1) asm volatile("s_barrier" ::: "memory");
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];  // [m-tile][kk], [n-tile][kk]
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const __bf16* Alo = slot(buf, 0);
+    const __bf16* Blo = slot(buf, 1);
+    const __bf16* Bhi = slot(buf, 2);
+    const __bf16* Ahi = slot(buf, 3);
+    const bool s1 = t + 1 < nk, s2 = t + 2 < nk;
+
+    // ---- phase 1: B-lo then A-lo -> quadrant (lo, lo)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) b0[j][kk] = gemm_frag(Blo, wn * 32 + j * 16 + fr, kk * 4 + fq);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Alo, wm * 64 + i * 16 + fr, kk * 4 + fq);
+    if (s1) stage(t + 1, 3);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the 4 B reads (issued first) have retired
+    asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b0[j][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+
+    // ---- phase 2: B-hi -> quadrant (lo, hi)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) b1[j][kk] = gemm_frag(Bhi, wn * 32 + j * 16 + fr, kk * 4 + fq);
+    if (s2) stage(t + 2, 1);
+    asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b1[j][kk], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+
+    // ---- phase 3: A-hi -> quadrant (hi, hi)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Ahi, wm * 64 + i * 16 + fr, kk * 4 + fq);
+    if (s2) stage(t + 2, 0);
+    asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b1[j][kk], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+
+    // ---- phase 4: registers only -> quadrant (hi, lo); retire K-tile t+1
+    if (s2) {
+      stage(t + 2, 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b0[j][kk], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+  }
+  if (STAGGER && wm == 0) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  gemm_store_epilogue<EPI>(acc, smem, C, bias, N, row0, col0, wave, lane, rope);
 }
 
 // zero the storage rows that have no sequence position (text padding [T, Tp) and the last image slot)
@@ -396,6 +563,14 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
     return true;
     PHASED_CASE(0) PHASED_CASE(1) PHASED_CASE(2) PHASED_CASE(3) PHASED_CASE(4) PHASED_CASE(5) PHASED_CASE(6) PHASED_CASE(7)
 #undef PHASED_CASE
+    case 300:
+      hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                         (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{});
+      return true;
+    case 301:
+      hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 1>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                         (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{});
+      return true;
     case 100:
       hipLaunchKernelGGL((gemm_nt_kernel<0, 1>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
                          (__bf16*)C, (const __bf16*)bias, M, N, K);
@@ -415,7 +590,9 @@ bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, cons
   const int Tp = (T + 31) / 32 * 32;
   RopeEpi e{(__bf16*)q, (__bf16*)k, (__bf16*)v, cosT, sinT, T, Tp, S, logS, n, Tp + S * S, H, col_major, qscale};
   const int nwg = (M / GBM) * (N / GBN);
-  hipLaunchKernelGGL((gemm_nt_phased_kernel<1, 2>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)W,
+  // 8-phase staggered template: 1073 vs 1042 TF for the phased kernel at M=61440, N=3072, K=1024
+  // (profiles/r1_gemm_8phase.jsonl)
+  hipLaunchKernelGGL((gemm_nt_8ph_kernel<1, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)W,
                      (__bf16*)nullptr, (const __bf16*)nullptr, M, N, K, e);
   const int BH = (M / n) * H;
   hipLaunchKernelGGL(rope_pad_zero_kernel, dim3(BH), dim3(256), 0, st, (__bf16*)q, (__bf16*)k, (__bf16*)v, Tp, T, Tp + S * S, BH);

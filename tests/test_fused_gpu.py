@@ -127,8 +127,8 @@ def test_splitk_accum(cuda):
     assert torch.allclose(acc, part.sum(0), atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 202])
-@pytest.mark.parametrize("M,N,K", [(512, 768, 320), (1024, 256, 1024)])
+@pytest.mark.parametrize("variant", [0, 202, 300, 301])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 320), (1024, 256, 1024), (256, 256, 64), (768, 512, 128), (2048, 1024, 192)])
 def test_gemm_nt(cuda, variant, M, N, K):
     from dalle_amd.ops.hip_ops import C
 
@@ -141,6 +141,9 @@ def test_gemm_nt(cuda, variant, M, N, K):
     assert _rel(got, want) < 1e-2
     got = C().gemm_nt(A, B, None, variant).float()
     assert _rel(got, A.float() @ B.float().t()) < 1e-2
+    # the pipelined kernels must agree bitwise with the plain one (same MFMA order per output)
+    if variant:
+        assert torch.equal(C().gemm_nt(A, B, bias, variant), C().gemm_nt(A, B, bias, 0))
 
 
 @pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
