@@ -109,6 +109,8 @@ class LocalSwarm:
                "--host_maddrs", f"/ip4/127.0.0.1/tcp/{self.dht_port}",
                "--elastic_coordinator", f"127.0.0.1:{self.coordinator_port}", "--host_elastic_coordinator", "True",
                *self.aux_args]
+        if "--local_path" not in self.aux_args:  # checkpoints next to the logs, not in the source tree
+            cmd += ["--local_path", os.path.join(self.log_dir, "Repo")]
         return Peer("aux", cmd, self._env(None), os.path.join(self.log_dir, "aux.log"))
 
     def trainer(self, i: int) -> Peer:
