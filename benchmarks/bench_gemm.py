@@ -79,7 +79,8 @@ def main():
         t_lt = timeit(lambda: torch.addmm(bias, A, B.t()))
         t_me = timeit(lambda: C.gemm_nt(A, B, bias))
         t_v1 = timeit(lambda: C.gemm_nt(A, B, bias, 200))
-        opts = {o: round(fl / timeit(lambda: C.gemm_nt(A, B, bias, o)) / 1e9) for o in (202, 300, 301)}
+        opts = {o: round(fl / timeit(lambda: C.gemm_nt(A, B, bias, o)) / 1e9)
+                for o in (202, 300, 301, 302, 308, 316, 332, 401, 402, 404, 408, 416)}
         opts["hipblaslt_again"] = round(fl / timeit(lambda: torch.addmm(bias, A, B.t())) / 1e9)
         e8 = (C.gemm_nt(A, B, bias, 300).float() - torch.addmm(bias, A, B.t()).float()).abs().max().item()
         e2 = ((C.gemm_nt(A, B, bias, 200).float() - torch.addmm(bias, A, B.t()).float()).norm() /

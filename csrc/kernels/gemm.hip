@@ -43,18 +43,28 @@ __device__ __forceinline__ bf16x8 gemm_frag(const __bf16* tile, int row, int chu
   return *reinterpret_cast<const bf16x8*>(tile + row * 64 + ((chunk ^ gswz(row)) << 3));
 }
 
-// XCD-aware tile order: linear id -> XCD slot; within an XCD, tiles sweep M inside column groups
-__device__ __forceinline__ void gemm_tile_of(int& tm, int& tn, int tiles_m, int tiles_n) {
+// XCD-aware tile order: linear id -> XCD slot; within an XCD, tiles sweep M inside groups of
+// `group` column panels (group > 0), or sweep N inside groups of -group row panels (group < 0)
+__device__ __forceinline__ void gemm_tile_of(int& tm, int& tn, int tiles_m, int tiles_n, int group = 4) {
   const int nwg = tiles_m * tiles_n;
   int id = blockIdx.x;
   if ((nwg & 7) == 0) id = (id & 7) * (nwg >> 3) + (id >> 3);  // bijective when nwg % 8 == 0
-  constexpr int GROUP_N = 4;                                    // column panels per group
-  const int group = id / (GROUP_N * tiles_m);
-  const int first_n = group * GROUP_N;
-  const int gn = min(tiles_n - first_n, GROUP_N);
-  const int in_group = id - group * GROUP_N * tiles_m;
-  tn = first_n + in_group % gn;
-  tm = in_group / gn;
+  if (group > 0) {
+    const int g = id / (group * tiles_m);
+    const int first_n = g * group;
+    const int gn = min(tiles_n - first_n, group);
+    const int in_group = id - g * group * tiles_m;
+    tn = first_n + in_group % gn;
+    tm = in_group / gn;
+  } else {
+    const int gm_size = -group;
+    const int g = id / (gm_size * tiles_n);
+    const int first_m = g * gm_size;
+    const int gm = min(tiles_m - first_m, gm_size);
+    const int in_group = id - g * gm_size * tiles_n;
+    tm = first_m + in_group % gm;
+    tn = in_group / gm;
+  }
 }
 
 template <int EPI, int VAR>
@@ -398,13 +408,13 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf
 template <int EPI, int OPT>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                    __bf16* __restrict__ C, const __bf16* __restrict__ bias,
-                                                                   int M, int N, int K, RopeEpi rope) {
+                                                                   int M, int N, int K, RopeEpi rope, int group) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];  // [buf][A-lo | B-lo | B-hi | A-hi]
   constexpr bool STAGGER = !(OPT & 1);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   int tm, tn;
-  gemm_tile_of(tm, tn, M / GBM, N / GBN);
+  gemm_tile_of(tm, tn, M / GBM, N / GBN, group);
   const int row0 = tm * GBM, col0 = tn * GBN;
   const int fr = lane & 15, fq = lane >> 4;
 
@@ -563,19 +573,24 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
     return true;
     PHASED_CASE(0) PHASED_CASE(1) PHASED_CASE(2) PHASED_CASE(3) PHASED_CASE(4) PHASED_CASE(5) PHASED_CASE(6) PHASED_CASE(7)
 #undef PHASED_CASE
-    case 300:
-      hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
-                         (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{});
-      return true;
-    case 301:
-      hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 1>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
-                         (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{});
-      return true;
     case 100:
       hipLaunchKernelGGL((gemm_nt_kernel<0, 1>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
                          (__bf16*)C, (const __bf16*)bias, M, N, K);
       return true;
     default:
+      // 8-phase template; variant 3xx picks the tile order: 300 -> column groups of 4, 301..332 ->
+      // column groups of (variant - 300), 400 + g -> row groups of g
+      if (epi >= 300 && epi < 333) {
+        const int group = epi == 300 ? 4 : epi - 300;
+        hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                           (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, group);
+        return true;
+      }
+      if (epi > 400 && epi < 433) {
+        hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                           (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, -(epi - 400));
+        return true;
+      }
       return false;
   }
 }
@@ -593,7 +608,7 @@ bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, cons
   // 8-phase staggered template: 1073 vs 1042 TF for the phased kernel at M=61440, N=3072, K=1024
   // (profiles/r1_gemm_8phase.jsonl)
   hipLaunchKernelGGL((gemm_nt_8ph_kernel<1, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)W,
-                     (__bf16*)nullptr, (const __bf16*)nullptr, M, N, K, e);
+                     (__bf16*)nullptr, (const __bf16*)nullptr, M, N, K, e, 4);
   const int BH = (M / n) * H;
   hipLaunchKernelGGL(rope_pad_zero_kernel, dim3(BH), dim3(256), 0, st, (__bf16*)q, (__bf16*)k, (__bf16*)v, Tp, T, Tp + S * S, BH);
   return true;

@@ -127,7 +127,7 @@ def test_splitk_accum(cuda):
     assert torch.allclose(acc, part.sum(0), atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 202, 300, 301])
+@pytest.mark.parametrize("variant", [0, 202, 300, 301, 308, 404])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 320), (1024, 256, 1024), (256, 256, 64), (768, 512, 128), (2048, 1024, 192)])
 def test_gemm_nt(cuda, variant, M, N, K):
     from dalle_amd.ops.hip_ops import C
