@@ -148,8 +148,21 @@ class DHT:
             return False
         sub = b"" if subkey is None else (subkey if isinstance(subkey, bytes) else str(subkey).encode())
         payload = msgpack.packb(value, use_bin_type=True)
+        for v in self.record_validators:  # owner-protected records get signed (RSASignatureValidator)
+            if hasattr(v, "sign_value"):
+                payload = v.sign_value(str(key), subkey, payload, float(expiration_time))
         owner = self.owner if subkey is not None else b""
         return bool(self._client.store(str(key), sub, payload, float(expiration_time), owner))
+
+    def _decode(self, key: str, sub, payload: bytes, exp: float):
+        """Signature check + strip of one stored record; None when a validator rejects it."""
+        for v in self.record_validators:
+            if hasattr(v, "validate_signed"):
+                if not v.validate_signed(key, None if sub == b"" else sub, payload, exp):
+                    logger.warning(f"dropping record {key!r}/{sub[:24]!r}: bad or missing owner signature")
+                    return None
+                payload = v.strip_value(payload)
+        return msgpack.unpackb(payload, raw=False)
 
     def store(self, key: str, value: Any, expiration_time: float, subkey: Any = None, return_future: bool = False, **kw):
         if return_future:
@@ -162,15 +175,20 @@ class DHT:
         items = self._client.get(str(key))
         if not items:
             return None
+        key = str(key)
         if len(items) == 1 and items[0][0] == b"":
             _, payload, exp = items[0]
-            return ValueWithExpiration(msgpack.unpackb(payload, raw=False), exp)
+            val = self._decode(key, b"", payload, exp)
+            return None if val is None else ValueWithExpiration(val, exp)
         out: Dict[Any, ValueWithExpiration] = {}
         best = 0.0
         for sub, payload, exp in items:
-            out[sub] = ValueWithExpiration(msgpack.unpackb(payload, raw=False), exp)
+            val = self._decode(key, sub, payload, exp)
+            if val is None:
+                continue
+            out[sub] = ValueWithExpiration(val, exp)
             best = max(best, exp)
-        return ValueWithExpiration(out, best)
+        return ValueWithExpiration(out, best) if out else None
 
     def delete(self, key: str):
         self._client.delete(str(key))

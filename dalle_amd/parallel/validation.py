@@ -2,14 +2,17 @@
 
 * :class:`SchemaValidator` validates records whose key is ``{prefix}_{field}`` against the pydantic
   schema's field type (``MetricSchema{metrics: Dict[BytesWithPublicKey, LocalMetrics]}``).
-* :class:`RSASignatureValidator` gives every peer an owner identity (``local_public_key``). There is
-  no asymmetric-crypto library in this image, so ownership is enforced by the native store itself:
-  a live subkey can only be rewritten by the owner that created it (csrc/store/kvstore.cpp).
+* :class:`RSASignatureValidator` gives every peer an RSA owner identity (``local_public_key``) and
+  signs / verifies owner-protected records (``dalle_amd.parallel.crypto``). The native store also
+  refuses to let anyone but a live subkey's creator rewrite it (csrc/store/kvstore.cpp).
 """
 from __future__ import annotations
 
-import secrets
+import base64
+import re
 from typing import Any, Dict
+
+import msgpack
 
 BytesWithPublicKey = bytes
 
@@ -50,8 +53,61 @@ class SchemaValidator(RecordValidatorBase):
 
 
 class RSASignatureValidator(RecordValidatorBase):
-    def __init__(self, local_public_key: bytes = None):
-        self.local_public_key = local_public_key or (b"<rsa-pubkey:" + secrets.token_hex(16).encode() + b">")
+    """Owner-signed records (hivemind ``RSASignatureValidator`` semantics).
+
+    ``local_public_key`` is ``[owner:<ssh-rsa public key>]``. A record whose key or subkey contains an
+    owner marker must carry exactly one ``[signature:<base64>]`` suffix in its serialised value: an
+    RSASSA-PKCS1-v1_5 / SHA-256 signature by that owner over ``msgpack([key, subkey, value,
+    expiration_time])`` with the signature stripped. Unprotected records pass unchanged. The DHT
+    facade signs on store and validates + strips on every read, so a record forged by another peer
+    (or altered in the store) never reaches a consumer.
+    """
+
+    PUBLIC_KEY_FORMAT = b"[owner:_key_]"
+    SIGNATURE_FORMAT = b"[signature:_value_]"
+    _PUBLIC_KEY_RE = re.compile(rb"\[owner:(.+?)\]")
+    _SIGNATURE_RE = re.compile(rb"\[signature:(.+?)\]")
+
+    def __init__(self, private_key=None):
+        from .crypto import RSAPrivateKey
+
+        self._private_key = private_key or RSAPrivateKey.process_wide()
+        self.local_public_key = self.PUBLIC_KEY_FORMAT.replace(b"_key_", self._private_key.get_public_key().to_bytes())
+
+    @staticmethod
+    def _as_bytes(x) -> bytes:
+        if x is None:
+            return b""
+        return x if isinstance(x, bytes) else str(x).encode()
+
+    def _serialize(self, key, subkey, value: bytes, expiration_time: float) -> bytes:
+        return msgpack.packb([self._as_bytes(key), self._as_bytes(subkey), value, float(expiration_time)], use_bin_type=True)
+
+    def sign_value(self, key, subkey, value: bytes, expiration_time: float) -> bytes:
+        if self.local_public_key not in self._as_bytes(key) and self.local_public_key not in self._as_bytes(subkey):
+            return value
+        sig = self._private_key.sign(self._serialize(key, subkey, value, expiration_time))
+        return value + self.SIGNATURE_FORMAT.replace(b"_value_", base64.b64encode(sig))
+
+    def strip_value(self, value: bytes) -> bytes:
+        return self._SIGNATURE_RE.sub(b"", value)
+
+    def validate_signed(self, key, subkey, value: bytes, expiration_time: float) -> bool:
+        from .crypto import RSAPublicKey
+
+        keys = self._PUBLIC_KEY_RE.findall(self._as_bytes(key)) + self._PUBLIC_KEY_RE.findall(self._as_bytes(subkey))
+        if not keys:
+            return True  # not owner-protected
+        if len(set(keys)) > 1:
+            return False
+        sigs = self._SIGNATURE_RE.findall(value)
+        if len(sigs) != 1:
+            return False
+        try:
+            pub = RSAPublicKey.from_bytes(keys[0])
+            return pub.verify(self._serialize(key, subkey, self.strip_value(value), expiration_time), base64.b64decode(sigs[0]))
+        except Exception:  # malformed key / signature
+            return False
 
     def validate(self, key: str, subkey: Any, value: Any) -> bool:
-        return True
+        return True  # ownership is checked on the serialised record (validate_signed)

@@ -5,14 +5,15 @@ user's HF token) for an authority-signed access token (username, peer public key
 with exponential backoff, refreshed one minute before expiry, and validated by signature + expiry.
 
 Same protocol here, with two authorities:
-* a remote one when ``DALLE_AMD_AUTH_SERVER`` is set (HTTPS via ``requests``);
-* an offline local authority (HMAC-SHA256 with a shared secret from ``DALLE_AMD_AUTH_SECRET``) so
-  the peers of one node can still issue / verify tokens without network access.
+* a remote one when ``DALLE_AMD_AUTH_SERVER`` is set (HTTPS via ``requests``); its response carries
+  the token and the authority's RSA public key (``auth_server_public_key``);
+* an offline local authority whose RSA key lives in ``DALLE_AMD_AUTH_KEY`` (created on first use,
+  mode 0600) so the peers of one node can issue / verify tokens without network access.
+Tokens are RSASSA-PKCS1-v1_5 / SHA-256 signatures by the authority (``dalle_amd.parallel.crypto``),
+verified with the authority's public key plus the expiry.
 """
 import base64
 import getpass
-import hashlib
-import hmac
 import json
 import os
 import time
@@ -48,17 +49,32 @@ class AccessToken:
 
 
 class LocalAuthority:
-    def __init__(self, secret: Optional[bytes] = None):
-        self.secret = secret or os.environ.get("DALLE_AMD_AUTH_SECRET", "dalle-amd-local").encode()
+    """Offline token authority: an RSA key shared by the peers of one node through a key file."""
+
+    def __init__(self, key_path: Optional[str] = None, private_key=None):
+        from dalle_amd.parallel.crypto import RSAPrivateKey
+
+        self._key = private_key or RSAPrivateKey.load_or_create(key_path or os.environ.get("DALLE_AMD_AUTH_KEY"))
+
+    @property
+    def public_key(self):
+        return self._key.get_public_key()
 
     def issue(self, username: str, public_key: bytes, lifetime: float = 3600.0) -> AccessToken:
         tok = AccessToken(username, public_key, time.time() + lifetime)
-        tok.signature = hmac.new(self.secret, tok.payload(), hashlib.sha256).digest()
+        tok.signature = self._key.sign(tok.payload())
         return tok
 
     def verify(self, tok: AccessToken) -> bool:
-        good = hmac.new(self.secret, tok.payload(), hashlib.sha256).digest()
-        return hmac.compare_digest(good, tok.signature) and tok.expiration_time > time.time()
+        return verify_access_token(tok, self.public_key)
+
+
+def verify_access_token(tok: AccessToken, authority_public_key) -> bool:
+    """Authority signature over (username, peer public key, expiry) and not yet expired."""
+    try:
+        return authority_public_key.verify(tok.payload(), tok.signature) and tok.expiration_time > time.time()
+    except Exception:  # noqa: BLE001  (malformed token)
+        return False
 
 
 class HuggingFaceAuthorizer:
@@ -69,7 +85,8 @@ class HuggingFaceAuthorizer:
         self.organization_name, self.model_name = organization_name, model_name
         self.hf_user_access_token = hf_user_access_token
         self.local_public_key = local_public_key
-        self.authority = authority or LocalAuthority()
+        self.authority = authority
+        self._authority_public_key = None
         self.username: Optional[str] = None
         self.coordinator_ip, self.coordinator_port = None, None
         self._token: Optional[AccessToken] = None
@@ -95,13 +112,21 @@ class HuggingFaceAuthorizer:
             self._token = AccessToken(tok["username"], base64.b64decode(tok["peer_public_key"]), float(tok["expiration_time"]),
                                       base64.b64decode(tok["signature"]))
             self.coordinator_ip, self.coordinator_port = resp.get("coordinator_ip"), resp.get("coordinator_port")
+            from dalle_amd.parallel.crypto import RSAPublicKey
+
+            self._authority_public_key = RSAPublicKey.from_bytes(base64.b64decode(resp["auth_server_public_key"]))
         else:
+            if self.authority is None:
+                self.authority = LocalAuthority()
             self.username = self.hf_user_access_token.split(":")[0] if ":" in self.hf_user_access_token else getpass.getuser()
             self._token = self.authority.issue(self.username, self.local_public_key)
+            self._authority_public_key = self.authority.public_key
         logger.info(f"Access for user {self.username} has been granted until {time.ctime(self._token.expiration_time)}")
 
     def is_token_valid(self, tok: AccessToken) -> bool:
-        return self.authority.verify(tok)
+        if self._authority_public_key is None:
+            self.get_token()
+        return verify_access_token(tok, self._authority_public_key)
 
     def does_token_need_refreshing(self, tok: AccessToken) -> bool:
         return tok.expiration_time - time.time() < self._AUTHORITY_REFRESH
