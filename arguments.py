@@ -1,9 +1,10 @@
-"""Flag schema of the training / auxiliary peers -- field-for-field compatible with the reference
-(``arguments.py:8-165``): same names, defaults and CLI syntax (``--flag value``, ``--flag True``).
+"""Command-line schema of the training, TPU-style and auxiliary peers.
 
-``HFTrainerArguments`` no longer subclasses ``transformers.TrainingArguments``; it carries the
-inherited fields the reference actually reads (``seed``, ``run_name``, ``output_dir``, ``local_rank``,
-``do_eval`` ...) plus a few MI355X-engine extensions marked [new].
+Every flag of the reference (``arguments.py:8-165``) keeps its name, default and syntax
+(``--name value``, booleans as ``--name True``; parsed by ``dalle_amd.utils.argparse``), so existing
+launch scripts run unchanged. ``HFTrainerArguments`` does not derive from ``transformers``' class any
+more: it declares the inherited fields the reference reads (``seed``, ``run_name``, ``output_dir``,
+``local_rank``, ``do_eval`` ...) itself. Flags that exist only in this engine say so in their help.
 """
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -11,176 +12,137 @@ from typing import List, Optional
 import torch
 
 
+def flag(default, doc: str = "", factory=None):
+    """A dataclass field carrying its ``--help`` text (list defaults via ``factory``)."""
+    if factory is not None:
+        return field(default_factory=factory, metadata={"help": doc})
+    return field(default=default, metadata={"help": doc})
+
+
 @dataclass
 class HFTrainerArguments:
-    """Arguments for the collaborative trainer loop (formerly huggingface/transformers.Trainer)"""
-    dataloader_num_workers: int = 1
-    per_device_train_batch_size: int = 2
-    per_device_eval_batch_size: int = 2
-    gradient_accumulation_steps: int = 1
-    text_seq_length: int = 256
+    """Micro-batching, the LAMB recipe and the inner trainer loop of one peer."""
 
-    # DALLE-specific params
-    learning_rate: float = 0.0025
-    adam_beta1: float = 0.9
-    adam_beta2: float = 0.96
-    max_grad_norm: float = 4.0
-    weight_decay: float = 0.045
+    # --- batches and sequence
+    per_device_train_batch_size: int = flag(2, "micro-batch per GPU")
+    per_device_eval_batch_size: int = flag(2, "evaluation micro-batch per GPU")
+    gradient_accumulation_steps: int = flag(1, "micro-batches summed into one optimizer.step() call")
+    text_seq_length: int = flag(256, "caption tokens per sample (padded / truncated)")
+    dataloader_num_workers: int = flag(1, "data loader worker processes")
 
-    total_steps: int = 31250  # total number of collaborative SGD updates, used for learning rate schedule
-    warmup_steps: int = 3125
-    adam_epsilon: float = 1e-6
-    clamp_value: float = 10000.0
+    # --- LAMB + schedule (one scheduler step per collaborative epoch)
+    learning_rate: float = flag(0.0025, "peak learning rate")
+    warmup_steps: int = flag(3125, "linear warm-up length, in collaborative epochs")
+    total_steps: int = flag(31250, "epochs until the linear decay reaches zero")
+    adam_beta1: float = flag(0.9)
+    adam_beta2: float = flag(0.96)
+    adam_epsilon: float = flag(1e-6)
+    weight_decay: float = flag(0.045, "decoupled weight decay (biases are exempt)")
+    max_grad_norm: float = flag(4.0, "global clip applied to the averaged gradient inside LAMB")
+    clamp_value: float = flag(10000.0, "upper clamp of the LAMB weight norm in the trust ratio")
 
-    fp16: bool = False
-    do_train: bool = True
-    do_eval: bool = False
+    # --- trainer loop bookkeeping
+    fp16: bool = flag(False, "fp16 autocast with the collaborative (deferred-unscale) grad scaler")
+    do_train: bool = flag(True)
+    do_eval: bool = flag(False)
+    logging_steps: int = flag(100)
+    max_steps: int = flag(10 ** 20, "mini-step budget of this peer")
+    save_steps: int = flag(10 ** 20)
+    save_total_limit: int = flag(2)
+    output_dir: str = flag("outputs", "checkpoints and snapshots of this peer")
+    seed: int = flag(42, "model-initialisation seed")
+    run_name: Optional[str] = flag(None)
+    local_rank: int = flag(-1, "set by torchrun")
+    report_to: List[str] = flag(None, factory=list)
 
-    logging_steps: int = 100
-    max_steps: int = 10 ** 20
-    save_steps: int = 10 ** 20
-    save_total_limit: int = 2
-
-    output_dir: str = "outputs"
-
-    # inherited TrainingArguments fields used by the reference
-    seed: int = 42
-    run_name: Optional[str] = None
-    local_rank: int = -1
-    report_to: List[str] = field(default_factory=list)
-
-    # [new] MI355X engine extensions
-    model_preset: str = field(default="reference", metadata={"help": "dalle_amd.config preset (reference, bench24, tiny, dalle-1.3b)"})
-    dataset_path: Optional[str] = field(default=None, metadata={"help": "local LAION-VQGAN shard dir (parquet/jsonl); default synthetic"})
-    optimizer_bits: int = field(default=8, metadata={"help": "LAMB moment precision: 8 (CPULAMB8Bit) or 32"})
-    grad_averaging: str = field(default="size_adaptive", metadata={"help": "none | fp16 | 8bit | size_adaptive | powersgd"})
-    powersgd_rank: int = 4
-    backend: Optional[str] = field(default=None, metadata={"help": "torch.distributed backend (nccl=RCCL on GPU, gloo on CPU)"})
+    # --- engine-only flags
+    model_preset: str = flag("reference", "engine only: dalle_amd.config preset (reference, bench24, tiny, dalle-1.3b)")
+    dataset_path: Optional[str] = flag(None, "engine only: directory of LAION-VQGAN parquet/jsonl shards (default: synthetic)")
+    optimizer_bits: int = flag(8, "engine only: LAMB moment storage, 8 (CPULAMB8Bit layout) or 32")
+    grad_averaging: str = flag("size_adaptive", "engine only: none | fp16 | 8bit | size_adaptive | powersgd")
+    powersgd_rank: int = flag(4, "engine only: rank of the PowerSGD factors")
+    backend: Optional[str] = flag(None, "engine only: torch.distributed backend (nccl = RCCL on MI355X, gloo on CPU)")
 
     @property
     def device(self) -> torch.device:
-        if torch.cuda.is_available():
-            idx = max(self.local_rank, 0)
-            return torch.device("cuda", idx % torch.cuda.device_count())
-        return torch.device("cpu")
+        if not torch.cuda.is_available():
+            return torch.device("cpu")
+        return torch.device("cuda", max(self.local_rank, 0) % torch.cuda.device_count())
 
     @property
     def n_gpu(self) -> int:
-        return 1 if torch.cuda.is_available() else 0
+        return int(torch.cuda.is_available())
 
     @property
-    def batch_size_per_step(self):
-        """Training sequences contributed by each .step() of this peer.
+    def batch_size_per_step(self) -> int:
+        """Samples one ``optimizer.step()`` of this peer adds to the collaboration.
 
-        One process drives one GPU (one peer per MI355X), so -- unlike the reference, which multiplied
-        by ``torch.cuda.device_count()`` (SURVEY §5.9 gotcha) -- the local device count is 1."""
+        A peer is one process on one GPU, so there is no ``torch.cuda.device_count()`` factor (the
+        reference's factor would over-count 8x on a node where every process sees all GPUs)."""
         return self.per_device_train_batch_size * self.gradient_accumulation_steps
 
 
 @dataclass
 class TPUTrainerArguments(HFTrainerArguments):
-    num_tpus: int = 8  # the total number of TPU cores in use
-    wandb_project: str = "huggingface"
+    num_tpus: int = flag(8, "local devices driven by run_trainer_tpu.py (one worker process each)")
+    wandb_project: str = flag("huggingface")
 
     @property
-    def batch_size_per_step(self):
-        return self.per_device_train_batch_size * self.gradient_accumulation_steps * self.num_tpus
+    def batch_size_per_step(self) -> int:
+        return super().batch_size_per_step * self.num_tpus
 
 
 @dataclass
 class CollaborativeArguments:
-    """Configuration for CollaborativeOptimizer and its internals"""
-    target_batch_size: int = field(
-        default=4096,
-        metadata={"help": "Perform optimizer step after all peers collectively accumulate this many samples"},
-    )
-    matchmaking_time: float = field(
-        default=15.0, metadata={"help": "Averaging group will wait for stragglers for at most this many seconds"}
-    )
-    allreduce_timeout: float = field(
-        default=60, metadata={"help": "Give up on a given all-reduce round after this many seconds"}
-    )
-    averaging_timeout: float = field(
-        default=180, metadata={"help": "Give up on averaging step after this many seconds"}
-    )
-    reuse_grad_buffers: bool = field(default=True, metadata={
-        "help": "Whether or not to use model's .grad buffers for accumulating gradients across local steps."})
+    """Knobs of the collaborative optimizer (epoch size and averaging deadlines)."""
+
+    target_batch_size: int = flag(4096, "global samples per collaborative epoch (one optimizer update)")
+    matchmaking_time: float = flag(15.0, "seconds an averaging round waits for late peers")
+    allreduce_timeout: float = flag(60, "seconds before one all-reduce round is abandoned")
+    averaging_timeout: float = flag(180, "seconds before the whole averaging step is abandoned")
+    reuse_grad_buffers: bool = flag(True, "accumulate micro-batch gradients directly in the .grad buffers")
 
 
 @dataclass
 class BasePeerArguments:
-    """Base arguments that are used for both trainers and for auxiliary peers such as training monitor"""
-    experiment_prefix: str = field(default="my-model", metadata={"help": "A unique experiment name, used as prefix for all DHT keys"})
-    tokenizer_path: Optional[str] = field(default="t5-small", metadata={"help": "Path to the tokenizer"})
-    cache_dir: Optional[str] = field(default="./cache", metadata={"help": "Path to the cache"})
+    """Identity, tokenizer and key-value-store connectivity shared by all peer kinds."""
 
-    authorize: bool = field(default=True, metadata={"help": "Whether or not to use HF authorizer"})
-    client_mode: bool = field(
-        default=False,
-        metadata={"help": "Of True, runs training without incoming connections, in a firewall-compatible mode"},
-    )
-    initial_peers: List[str] = field(
-        default_factory=list,
-        metadata={"help": "Multiaddrs of the key-value store host, e.g. /ip4/127.0.0.1/tcp/31337"},
-    )
-    use_ipfs: bool = field(default=False, metadata={"help": "Accepted for compatibility; there is no public DHT"})
-    host_maddrs: List[str] = field(
-        default_factory=lambda: ["/ip4/0.0.0.0/tcp/0"],
-        metadata={"help": "Multiaddrs to listen on (the first peer hosts the key-value store)"},
-    )
-    announce_maddrs: List[str] = field(
-        default_factory=list,
-        metadata={"help": "Visible multiaddrs the host announces for external connections"},
-    )
-    identity_path: Optional[str] = field(default=None, metadata={"help": "File holding this peer's persistent id"})
-    elastic_coordinator: Optional[str] = field(
-        default=None,
-        metadata={"help": "host:port of the elastic coordinator store (hosted by run_aux_peer.py "
-                          "--host_elastic_coordinator True). When set, trainers form their communicator through "
-                          "it and survive peer death / admit late joiners (SURVEY 5.3)"},
-    )
+    experiment_prefix: str = flag("my-model", "run id: prefix of every key this run stores")
+    tokenizer_path: Optional[str] = flag("t5-small", "tokenizer name or directory")
+    cache_dir: Optional[str] = flag("./cache", "cache directory (accepted; unused, as in the reference)")
+    authorize: bool = flag(True, "obtain an authority-signed access token before joining")
+    client_mode: bool = flag(False, "accept no inbound connections (never hosts the store or a reduce shard)")
+    initial_peers: List[str] = flag(None, "multiaddr of the store host, e.g. /ip4/127.0.0.1/tcp/31337", factory=list)
+    use_ipfs: bool = flag(False, "accepted for compatibility; there is no public DHT")
+    host_maddrs: List[str] = flag(None, "listen multiaddrs (the first peer hosts the store)",
+                                  factory=lambda: ["/ip4/0.0.0.0/tcp/0"])
+    announce_maddrs: List[str] = flag(None, "multiaddrs to advertise instead of the bound ones", factory=list)
+    identity_path: Optional[str] = flag(None, "file with this peer's persistent id")
+    elastic_coordinator: Optional[str] = flag(
+        None, "engine only: host:port of the elastic coordinator store (run_aux_peer.py --host_elastic_coordinator "
+              "True); trainers then build their communicator through it, survive peer death and admit late joiners")
 
 
 @dataclass
 class TrainingPeerArguments(BasePeerArguments):
-    statistics_expiration: float = field(
-        default=600, metadata={"help": "Statistics will be removed if not updated in this many seconds"}
-    )
-    backup_every_steps: Optional[int] = field(
-        default=None, metadata={"help": "Update training state backup on disk once in this many global steps "
-                                        "(default = do not update local state)"}
-    )
-    state_path: str = field(
-        default="state.zip", metadata={"help": "Load this state upon init and when recovering from NaN parameters"})
+    statistics_expiration: float = flag(600, "seconds a published metrics record stays alive")
+    backup_every_steps: Optional[int] = flag(None, "write a state backup every this many epochs (None: never)")
+    state_path: str = flag("state.zip", "backup file, loaded at start-up and after NaN parameters")
 
 
 @dataclass
 class AuxiliaryPeerArguments(BasePeerArguments):
-    """
-    Arguments for run_aux_peer.py that is responsible for connecting peers to one another, tracking
-    learning curves, assisting in all-reduce and uploading checkpoints to the hub
-    """
-    refresh_period: float = field(default=10, metadata={"help": "Period (in seconds) for fetching the keys from DHT"})
-    wandb_project: Optional[str] = field(
-        default=None, metadata={"help": "Name of Weights & Biases project to report the training progress to"}
-    )
-    save_checkpoint_step_interval: int = field(
-        default=2, metadata={"help": "Frequency (in steps) of fetching and saving state from peers"}
-    )
-    repo_url: Optional[str] = field(
-        default=None, metadata={"help": "URL of Hugging Face Hub repository to upload the model and optimizer states"}
-    )
-    local_path: Optional[str] = field(
-        default="Repo", metadata={"help": "Path to local repository to store the model and optimizer states"}
-    )
-    upload_interval: Optional[float] = field(
-        default=None, metadata={"help": "Frequency (in seconds) of uploading the model to Hub"}
-    )
-    store_checkpoints: bool = field(default=True, metadata={"help": "If True, enables CheckpointHandler"})
-    host_elastic_coordinator: bool = field(
-        default=False, metadata={"help": "Host the elastic coordinator store at --elastic_coordinator host:port"})
-    assist_in_averaging: bool = field(
-        default=False, metadata={"help": "If True, this peer will facilitate averaging for other (training) peers"})
-    assist_refresh: float = field(default=1.0, metadata={"help": "Period (in seconds) for tryin to assist averaging"})
-    metrics_log: Optional[str] = field(default=None, metadata={"help": "[new] JSON-lines file for the aggregated metrics"})
-    max_iterations: Optional[int] = field(default=None, metadata={"help": "[new] stop after this many polls (tests)"})
+    """The monitoring / checkpointing peer: aggregates metrics, snapshots and uploads state."""
+
+    refresh_period: float = flag(10, "seconds between two polls of the metrics records")
+    wandb_project: Optional[str] = flag(None, "Weights & Biases project for the aggregated curves")
+    save_checkpoint_step_interval: int = flag(2, "fetch the collaboration state every this many epochs")
+    repo_url: Optional[str] = flag(None, "Hugging Face Hub repository receiving the checkpoints")
+    local_path: Optional[str] = flag("Repo", "local directory (clone) for model_state.pt / optimizer_state.pt")
+    upload_interval: Optional[float] = flag(None, "seconds between two uploads to the Hub")
+    store_checkpoints: bool = flag(True, "enable the checkpoint handler")
+    assist_in_averaging: bool = flag(False, "serve as an extra averaging peer (not implemented, as in the reference)")
+    assist_refresh: float = flag(1.0, "seconds between two averaging-assist attempts")
+    host_elastic_coordinator: bool = flag(False, "engine only: host the elastic coordinator at --elastic_coordinator")
+    metrics_log: Optional[str] = flag(None, "engine only: JSON-lines file receiving the aggregated metrics")
+    max_iterations: Optional[int] = flag(None, "engine only: stop after this many polls (tests)")

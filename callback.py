@@ -1,12 +1,22 @@
-"""CollaborativeCallback: progress reporting, NaN rollback and backups (reference ``callback.py:14-127``).
+"""Trainer callback of a collaborative peer (reference ``callback.py:14-127``).
 
-Also serves state snapshots to auxiliary peers (which are not members of the training process
-group): an aux peer posts ``{run_id}_state_request``; the group's rank 0 answers with a
-``torch.save`` snapshot on the shared filesystem announced under ``{run_id}_state``.
+Responsibilities, each a small piece of this module:
+
+* ``_EpochStats``   -- sums mini-step losses between optimizer epochs and turns them into one
+  :class:`utils.LocalMetrics` record per epoch (published only while this peer is in sync with the
+  collaboration, under its owner-signed subkey, with ``statistics_expiration``);
+* NaN guard         -- one fused finiteness kernel over the parameter arena after every step; broken
+  parameters roll the peer back to its last backup (or abort when it has none);
+* backups           -- ``{"model", "training", "scheduler", "local_epoch"}`` at ``state_path`` every
+  ``backup_every_steps`` epochs; loaded at start-up before and after ``load_state_from_peers`` (the
+  second time only when newer than what the peers provided);
+* ``_SnapshotServer`` -- answers auxiliary peers (which are not in the training process group): an aux
+  peer posts ``{run_id}_state_request``; rank 0 writes a state snapshot to the shared filesystem and
+  announces its path under ``{run_id}_state``.
 """
-import os.path
+import os
 import time
-from typing import Any
+from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
@@ -19,145 +29,137 @@ from task import TrainingTask
 from utils import LocalMetrics, logger
 
 
+@dataclass
+class _EpochStats:
+    loss_sum: float = 0.0
+    mini_steps: int = 0
+    samples: int = 0  # samples this peer contributed to the epoch being accumulated
+    contributed_total: int = 0
+    reported_epoch: int = -1
+
+    def add(self, loss: float):
+        self.loss_sum += float(loss)
+        self.mini_steps += 1
+
+    def close_epoch(self, epoch: int, samples_per_second: float) -> LocalMetrics:
+        record = LocalMetrics(step=int(epoch), samples_per_second=float(samples_per_second),
+                              samples_accumulated=int(self.samples), loss=float(self.loss_sum), mini_steps=int(self.mini_steps))
+        self.contributed_total += self.samples
+        self.reported_epoch = epoch
+        self.loss_sum, self.mini_steps = 0.0, 0
+        return record
+
+
+class _SnapshotServer:
+    def __init__(self, task: TrainingTask, share_dir: str, poll_period: float = 2.0):
+        self.task, self.share_dir, self.poll_period = task, share_dir, poll_period
+        self._next_poll = 0.0
+        self._served = -1
+
+    def poll(self):
+        opt, dht = self.task.collaborative_optimizer, self.task.dht
+        if dht is None or (dist.is_initialized() and dist.get_rank() != 0) or time.time() < self._next_poll:
+            return
+        self._next_poll = time.time() + self.poll_period
+        request = dht.get(opt.run_id + "_state_request", latest=True)
+        if request is None:
+            return
+        asked = request.value.values() if isinstance(request.value, dict) else [request]
+        wanted = max(int(r.value) for r in asked)
+        epoch = opt.local_epoch
+        if wanted <= self._served or epoch < wanted:
+            return
+        os.makedirs(self.share_dir, exist_ok=True)
+        final = os.path.abspath(os.path.join(self.share_dir, "state.pt"))
+        torch.save({"model": self.task.model.state_dict(), "optimizer": opt.state_dict(),
+                    "scheduler": opt.scheduler.state_dict(), "local_epoch": epoch}, final + ".tmp")
+        os.replace(final + ".tmp", final)  # readers never see a half-written file
+        self._served = epoch
+        dht.store(opt.run_id + "_state", subkey=None, value={"path": final, "epoch": epoch},
+                  expiration_time=get_dht_time() + 3600)
+        logger.info(f"State snapshot of epoch {epoch} published for auxiliary peers")
+
+
 class CollaborativeCallback(TrainerCallback):
-    """
-    This callback monitors and reports collaborative training progress,
-    In case of a catastrophic failure, it can also revert training to a backup
-    """
+    """Reports collaborative progress and reverts the peer to a backup after a numerical failure."""
 
     def __init__(self, task: TrainingTask, args: TrainingPeerArguments):
         super().__init__()
         self.task = task
         self.dht, self.collaborative_optimizer = task.dht, task.collaborative_optimizer
         self.statistics_expiration = args.statistics_expiration
-        self.last_reported_collaboration_step = -1
-        self.samples = 0
-        self.steps = 0
-        self.loss = 0
-        self.total_samples_processed = 0
         self.backup_every_steps = args.backup_every_steps
         self.state_path = args.state_path
-        self.share_dir = os.path.join(task.trainer_args.output_dir, "shared_state")
-        self._last_request_check = 0.0
-        self._served_epoch = -1
+        self.stats = _EpochStats()
+        self.snapshots = _SnapshotServer(task, os.path.join(task.trainer_args.output_dir, "shared_state"))
 
+    # -- trainer hooks ------------------------------------------------------------------------
     def on_train_begin(self, args, state, control, **kwargs):
-        if os.path.isfile(self.state_path):
+        have_backup = os.path.isfile(self.state_path)
+        if have_backup:
             self.restore_from_backup(self.state_path)
-            logger.info("Loaded state")
-
-        logger.info("Loading state from peers")
+        logger.info("Synchronising with the collaboration (load_state_from_peers)")
         self.collaborative_optimizer.load_state_from_peers()
-
-        if os.path.isfile(self.state_path):
+        if have_backup:  # the local backup wins only if it is at least as recent as the peers' state
             self.restore_from_backup(self.state_path, check_step=True)
 
     def on_step_end(self, args, state, control, **kwargs):
         control.should_log = True
         if not self.params_are_finite():
             if not os.path.exists(self.state_path):
-                raise RuntimeError("Encountered broken parameters, but there is no backup to fall back to.")
-            logger.warning("Parameters are invalid, reloading model from earlier state")
+                raise RuntimeError("Parameters became NaN/Inf and there is no backup to roll back to")
+            logger.warning("Parameters became NaN/Inf: rolling back to the last backup")
             self.restore_from_backup(self.state_path)
             return control
-
+        opt = self.collaborative_optimizer
         if state.log_history:
-            self.loss += state.log_history[-1]["loss"]
-            self.steps += 1
-            if self.collaborative_optimizer.local_epoch != self.last_reported_collaboration_step:
-                self.last_reported_collaboration_step = self.collaborative_optimizer.local_epoch
-                self.total_samples_processed += self.samples
-                samples_per_second = self.collaborative_optimizer.tracker.performance_ema.samples_per_second
-                statistics = LocalMetrics(
-                    step=self.collaborative_optimizer.local_epoch,
-                    samples_per_second=float(samples_per_second),
-                    samples_accumulated=self.samples,
-                    loss=float(self.loss),
-                    mini_steps=self.steps,
-                )
-                logger.info(f"Current epoch: {self.collaborative_optimizer.local_epoch}")
-                logger.info(f"Your current contribution: {self.total_samples_processed} samples")
-                logger.info(f"Performance: {samples_per_second} samples/sec")
-                if self.steps:
-                    logger.info(f"Local loss: {self.loss / self.steps}")
-
-                self.loss = 0
-                self.steps = 0
-                if self.dht is not None and self.collaborative_optimizer.local_epoch == self.collaborative_optimizer.tracker.global_epoch:
-                    self.dht.store(
-                        key=self.collaborative_optimizer.run_id + "_metrics",
-                        subkey=self.task.local_public_key,
-                        value=statistics.model_dump() if hasattr(statistics, "model_dump") else statistics.dict(),
-                        expiration_time=get_dht_time() + self.statistics_expiration,
-                        return_future=True,
-                    )
-                if self.backup_every_steps is not None and \
-                        self.collaborative_optimizer.local_epoch % self.backup_every_steps == 0:
-                    self.backup_state()
-
-        self.samples = self.collaborative_optimizer.grad_averager.local_samples_accumulated
-        self.serve_state_requests()
+            self.stats.add(state.log_history[-1]["loss"])
+            if opt.local_epoch != self.stats.reported_epoch:
+                self._finish_epoch(opt)
+        self.stats.samples = opt.grad_averager.local_samples_accumulated
+        self.snapshots.poll()
         return control
 
+    def _finish_epoch(self, opt):
+        sps = opt.tracker.performance_ema.samples_per_second
+        steps, loss = self.stats.mini_steps, self.stats.loss_sum
+        record = self.stats.close_epoch(opt.local_epoch, sps)
+        logger.info(f"epoch {opt.local_epoch}: contributed {self.stats.contributed_total} samples so far, "
+                    f"{sps:.2f} samples/s" + (f", mean loss {loss / steps:.5f}" if steps else ""))
+        in_sync = opt.local_epoch == opt.tracker.global_epoch
+        if self.dht is not None and in_sync:
+            payload = record.model_dump() if hasattr(record, "model_dump") else record.dict()
+            self.dht.store(key=opt.run_id + "_metrics", subkey=self.task.local_public_key, value=payload,
+                           expiration_time=get_dht_time() + self.statistics_expiration, return_future=True)
+        if self.backup_every_steps is not None and opt.local_epoch % self.backup_every_steps == 0:
+            self.backup_state()
+
+    # -- numerics / backups ---------------------------------------------------------------------
     @torch.no_grad()
-    def params_are_finite(self):
+    def params_are_finite(self) -> bool:
         arena = getattr(self.task, "_arena", None)
-        if arena is not None:
+        if arena is not None:  # one fused kernel over every parameter
             return grads_finite(arena.data)
-        for param in self.task.model.parameters():
-            if not torch.all(torch.isfinite(param)):
-                return False
-        return True
+        return all(bool(torch.isfinite(p).all()) for p in self.task.model.parameters())
 
     @torch.no_grad()
-    def backup_state(self) -> Any:
-        logger.info("Saving backup")
-        return torch.save(
-            {
-                "model": self.task.model.state_dict(),
-                "training": self.collaborative_optimizer.state_dict(),
-                "scheduler": self.collaborative_optimizer.state_averager.scheduler.state_dict(),
-                "local_epoch": self.collaborative_optimizer.local_epoch,
-            },
-            self.state_path,
-        )
+    def backup_state(self):
+        opt = self.collaborative_optimizer
+        logger.info(f"Writing backup of epoch {opt.local_epoch} to {self.state_path}")
+        snapshot = {"model": self.task.model.state_dict(), "training": opt.state_dict(),
+                    "scheduler": opt.state_averager.scheduler.state_dict(), "local_epoch": opt.local_epoch}
+        torch.save(snapshot, self.state_path)
 
     @torch.no_grad()
-    def restore_from_backup(self, path, check_step=False):
-        state = torch.load(path, map_location="cpu", weights_only=True)
-        current_step = self.collaborative_optimizer.local_epoch
-        backup_step = state['local_epoch']
-        if not check_step or backup_step >= current_step:
-            self.task.model.load_state_dict(state["model"], strict=False)
-            self.collaborative_optimizer.load_state_dict(state["training"])
-            self.collaborative_optimizer.state_averager.scheduler.load_state_dict(state["scheduler"])
-            self.collaborative_optimizer.state_averager.local_epoch = backup_step
-            logger.info("Restored from a backup")
-        else:
-            logger.info("Bypassed restoring state from local backup: backup state is too old.")
-
-    # -- state snapshots for auxiliary peers ------------------------------------------------------
-    def serve_state_requests(self, min_period: float = 2.0):
-        if self.dht is None or (dist.is_initialized() and dist.get_rank() != 0):
+    def restore_from_backup(self, path, check_step: bool = False):
+        snapshot = torch.load(path, map_location="cpu", weights_only=True)
+        opt = self.collaborative_optimizer
+        if check_step and snapshot["local_epoch"] < opt.local_epoch:
+            logger.info(f"Backup (epoch {snapshot['local_epoch']}) is older than the current state "
+                        f"(epoch {opt.local_epoch}); keeping the current state")
             return
-        now = time.time()
-        if now - self._last_request_check < min_period:
-            return
-        self._last_request_check = now
-        run_id = self.collaborative_optimizer.run_id
-        req = self.dht.get(run_id + "_state_request", latest=True)
-        if req is None:
-            return
-        wanted = max([int(v.value) for v in req.value.values()] if isinstance(req.value, dict) else [int(req.value)])
-        epoch = self.collaborative_optimizer.local_epoch
-        if wanted <= self._served_epoch or epoch < wanted:
-            return
-        os.makedirs(self.share_dir, exist_ok=True)
-        path = os.path.abspath(os.path.join(self.share_dir, "state.pt"))
-        tmp = path + ".tmp"
-        torch.save({"model": self.task.model.state_dict(), "optimizer": self.collaborative_optimizer.state_dict(),
-                    "scheduler": self.collaborative_optimizer.scheduler.state_dict(), "local_epoch": epoch}, tmp)
-        os.replace(tmp, path)
-        self._served_epoch = epoch
-        self.dht.store(run_id + "_state", subkey=None, value={"path": path, "epoch": epoch}, expiration_time=get_dht_time() + 3600)
-        logger.info(f"served a state snapshot of epoch {epoch} to auxiliary peers")
+        self.task.model.load_state_dict(snapshot["model"], strict=False)
+        opt.load_state_dict(snapshot["training"])
+        opt.state_averager.scheduler.load_state_dict(snapshot["scheduler"])
+        opt.state_averager.local_epoch = snapshot["local_epoch"]
+        logger.info(f"Restored the backup of epoch {snapshot['local_epoch']}")

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Training peer entrypoint (reference ``run_trainer.py:1-60``), CLI-compatible.
+"""Training peer (counterpart of the reference ``run_trainer.py``; same flags).
 
-One peer per MI355X: launch with ``torchrun --nproc-per-node 8 --master-addr 127.0.0.1 run_trainer.py ...``
-(RCCL over xGMI between the 8 peers of a node), or a single process for one GPU / CPU.
+A peer is one process driving one MI355X. On a node:
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 run_trainer.py <flags>
+gives 8 peers whose gradients average over RCCL / xGMI; a single process trains on one GPU (or the
+CPU). The trainer resumes from the newest ``<output_dir>/checkpoint*`` when there is one.
 """
 import os
 from pathlib import Path
@@ -20,40 +22,42 @@ from task import TrainingTask
 use_hivemind_log_handler("in_root_logger")
 logger = get_logger(__name__)
 
-torch.set_num_threads(int(os.environ.get("DALLE_AMD_CPU_THREADS", "1")))  # Otherwise, it becomes very slow on machines with ~100 CPUs
+# host threads stay few: the GPU does the work, and ~100-core hosts otherwise oversubscribe
+torch.set_num_threads(int(os.environ.get("DALLE_AMD_CPU_THREADS", "1")))
+
+
+def _newest_checkpoint(output_dir: str):
+    candidates = list(Path(output_dir).glob("checkpoint*"))
+    return max(candidates, key=os.path.getctime) if candidates else None
 
 
 def main(argv=None):
-    parser = HfArgumentParser((TrainingPeerArguments, HFTrainerArguments, CollaborativeArguments))
-    training_peer_args, trainer_args, collab_args = parser.parse_args_into_dataclasses(argv)
-    if trainer_args.local_rank < 0 and "LOCAL_RANK" in os.environ:
+    peer_args, trainer_args, collab_args = HfArgumentParser(
+        (TrainingPeerArguments, HFTrainerArguments, CollaborativeArguments)).parse_args_into_dataclasses(argv)
+    if trainer_args.local_rank < 0 and "LOCAL_RANK" in os.environ:  # torchrun
         trainer_args.local_rank = int(os.environ["LOCAL_RANK"])
-
-    logger.info(f"Trying {len(training_peer_args.initial_peers)} initial peers: {training_peer_args.initial_peers}")
-
+    if not trainer_args.do_train or trainer_args.do_eval:
+        raise ValueError("a training peer runs with --do_train True --do_eval False")
+    logger.info(f"initial peers ({len(peer_args.initial_peers)}): {peer_args.initial_peers}")
     utils.log_process_rank(trainer_args)
-    task = TrainingTask(training_peer_args, trainer_args, collab_args)
-    model = task.model.to(trainer_args.device)
 
-    collaborative_callback = callback.CollaborativeCallback(task, training_peer_args)
-    assert trainer_args.do_train and not trainer_args.do_eval
-
+    task = TrainingTask(peer_args, trainer_args, collab_args)
     trainer = CollaborativeHFTrainer(
-        model=model,
+        model=task.model.to(trainer_args.device),
         args=trainer_args,
         tokenizer=task.tokenizer,
         data_collator=task.data_collator,
+        # a stable per-peer data order (the reference's hash() of bytes is salted per process)
         data_seed=int.from_bytes(task.local_public_key[-8:], "little"),
         train_dataset=task.training_dataset,
         eval_dataset=None,
         collaborative_optimizer=task.collaborative_optimizer,
-        callbacks=[collaborative_callback],
+        callbacks=[callback.CollaborativeCallback(task, peer_args)],
     )
-    trainer.remove_callback(PrinterCallback)
-    trainer.remove_callback(ProgressCallback)
-
-    latest_checkpoint_dir = max(Path(trainer_args.output_dir).glob("checkpoint*"), key=os.path.getctime, default=None)
-    trainer.train(model_path=latest_checkpoint_dir)
+    # progress is reported by the collaborative callback (per epoch, across peers), not per mini-step
+    for cb in (PrinterCallback, ProgressCallback):
+        trainer.remove_callback(cb)
+    trainer.train(model_path=_newest_checkpoint(trainer_args.output_dir))
     return trainer, task
 
 

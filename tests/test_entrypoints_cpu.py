@@ -86,5 +86,5 @@ def test_nan_rollback_and_averaging_fallback(tmp_path):
         cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:]
     assert "falling back to local gradients" in r.stdout
-    assert "Parameters are invalid, reloading model from earlier state" in r.stdout
-    assert "Restored from a backup" in r.stdout
+    assert "Parameters became NaN/Inf: rolling back to the last backup" in r.stdout
+    assert "Restored the backup of epoch" in r.stdout
