@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from .averaging import allreduce_weighted
 from .compression import CompressionBase, NoCompression
+from .delayed import AsyncStep, MasterParams
 from .powersgd import PowerSGD
 from .progress import ProgressTracker
 from ..optim.flat import FlatArena
@@ -178,10 +179,16 @@ class GradientAverager:
 
 
 class TrainingStateAverager:
-    """Holds the inner optimizer + scheduler, the local epoch, and averages parameters (D16)."""
+    """Holds the inner optimizer + scheduler, the local epoch, and averages parameters (D16).
+
+    With ``master`` (a ``MasterParams``) the inner optimizer steps on master copies (hivemind's
+    ``offload_optimizer``); with ``delay`` the step itself runs concurrently with the next local
+    step (``delay_optimizer_step``, see ``delayed.py``) and is applied to the model -- followed by
+    the state-averaging round of that epoch -- at the next ``finish_pending`` boundary."""
 
     def __init__(self, optimizer: torch.optim.Optimizer, scheduler=None, params=None, arena: Optional[FlatArena] = None,
-                 group=None, compression: Optional[CompressionBase] = None, average_state_every: int = 1):
+                 group=None, compression: Optional[CompressionBase] = None, average_state_every: int = 1,
+                 master: Optional[MasterParams] = None, delay: bool = False):
         self.optimizer = optimizer
         self.scheduler = scheduler
         self.params = params
@@ -190,16 +197,64 @@ class TrainingStateAverager:
         self.compression = compression or NoCompression()
         self.average_state_every = average_state_every
         self.local_epoch = 0
+        self.master = master
+        self.runner = AsyncStep(master.masters[0].device) if (delay and master is not None and master.masters) else None
+        self._unapplied = False      # an update exists in the master copy but not in the model yet
+        self._averaging_due = False  # the state-averaging round of the last delayed epoch has not run yet
+
+    def _inner_step(self):
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
 
     @torch.no_grad()
     def step(self, optimizer_step: bool = True, averaging_round: bool = True):
         if optimizer_step:
-            self.optimizer.step()
-            if self.scheduler is not None:
-                self.scheduler.step()
+            self.finish_pending(average=False)
+            if self.master is not None:
+                self.master.pull()
+            if self.runner is not None:
+                self.runner.launch(self._inner_step)
+                self._unapplied = True
+                self._averaging_due = averaging_round
+                self.local_epoch += 1
+                return
+            self._inner_step()
+            if self.master is not None:
+                self.master.push()
             self.local_epoch += 1
         if averaging_round and self.average_state_every and self.local_epoch % self.average_state_every == 0:
             self.average_parameters()
+
+    @property
+    def pending(self) -> bool:
+        return self._unapplied or self._averaging_due
+
+    @torch.no_grad()
+    def finish_pending(self, average: bool = True) -> bool:
+        """Apply an in-flight delayed update to the model. ``average=True`` (the collective boundary,
+        reached by every peer at its next ``.step()``) also runs that epoch's state-averaging round;
+        local callers (``state_dict``, backups) pass False and leave the round to the boundary.
+        Returns True if an update was applied."""
+        applied = False
+        if self._unapplied:
+            self.runner.wait()
+            self.master.push()
+            self._unapplied = False
+            applied = True
+        if average and self._averaging_due:
+            self._averaging_due = False
+            if self.average_state_every and self.local_epoch % self.average_state_every == 0:
+                self.average_parameters()
+        return applied
+
+    @torch.no_grad()
+    def drop_pending(self):
+        """Discard an in-flight update (the model state is being replaced from a backup / a peer).
+        The epoch's averaging round stays due: it is a collective every peer must join."""
+        if self.runner is not None:
+            self.runner.wait()
+        self._unapplied = False
 
     @torch.no_grad()
     def average_parameters(self):
@@ -252,9 +307,15 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             flat_params = param_groups
             param_groups = [{"params": flat_params}]
         self._params = flat_params
-        inner = optimizer(param_groups) if callable(optimizer) and not isinstance(optimizer, torch.optim.Optimizer) else optimizer
+        factory = callable(optimizer) and not isinstance(optimizer, torch.optim.Optimizer)
+        if delay_optimizer_step and not factory:
+            logger.warning("delay_optimizer_step needs an optimizer factory (it builds the optimizer over master "
+                           "copies); stepping synchronously")
+        # delayed update: the inner optimizer owns master copies (hivemind's offloaded parameters, kept in HBM)
+        self._master = MasterParams(flat_params, arena) if (delay_optimizer_step and factory and flat_params) else None
+        inner = optimizer(self._master.substitute(param_groups) if self._master else param_groups) if factory else optimizer
         if arena is not None and getattr(inner, "arena", "missing") is None:
-            inner.arena = arena
+            inner.arena = self._master.arena if self._master is not None else arena
         sched = scheduler(inner) if callable(scheduler) else scheduler
         device = device or (flat_params[0].device if flat_params else torch.device("cpu"))
         self.device = device
@@ -267,7 +328,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                                               powersgd=psgd, client_mode=client_mode)
         self.state_averager = TrainingStateAverager(inner, sched, flat_params, arena=arena, group=process_group,
                                                     compression=state_averaging_compression,
-                                                    average_state_every=average_state_every)
+                                                    average_state_every=average_state_every,
+                                                    master=self._master, delay=self._master is not None)
         self.last_epoch_time = None
         if offload_optimizer and device.type == "cuda" and verbose:
             logger.info("offload_optimizer=True: keeping the optimizer on-GPU (fused HIP LAMB; 288 GB HBM)")
@@ -320,6 +382,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 loss = closure()
         if self.auxiliary:
             return loss
+        self.finish_pending()
         self._local_steps = getattr(self, "_local_steps", 0) + 1
         faults.on_local_step(self._local_steps, self._params)
         bs = batch_size if batch_size is not None else self.batch_size_per_step
@@ -379,7 +442,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 return
         self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
         self.state_averager.step(optimizer_step=True, averaging_round=True)
-        faults.after_update(self.local_epoch, self._params)
+        if not self.state_averager.pending:
+            faults.after_update(self.local_epoch, self._params)
         self.grad_averager.reset_accumulated_grads_()
         self.tracker.update_epoch(self.local_epoch)
         self.last_epoch_time = time.perf_counter() - t0
@@ -387,13 +451,33 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             logger.info(f"{self.run_id}: epoch {self.local_epoch} (averaged {total} samples across "
                         f"{self.tracker.global_progress.num_peers} peers in {self.last_epoch_time * 1e3:.1f} ms)")
 
+    # -- delayed parameter update ---------------------------------------------------------------------
+    def finish_pending(self) -> bool:
+        """Step boundary of ``delay_optimizer_step``: the update launched at the previous global step
+        lands in the model, then that epoch's state-averaging round runs. Every peer reaches this at
+        its next ``.step()``; call it directly before reading the model after the last step."""
+        applied = self.state_averager.finish_pending(average=True)
+        if applied:
+            faults.after_update(self.local_epoch, self._params)
+        return applied
+
+    def apply_pending(self) -> bool:
+        """Local part of the boundary only (no collective): the model gets the latest update; the
+        averaging round stays due for the next ``.step()``. Used before checkpoints and at exit."""
+        applied = self.state_averager.finish_pending(average=False)
+        if applied:
+            faults.after_update(self.local_epoch, self._params)
+        return applied
+
     # -- state --------------------------------------------------------------------------------------
     def state_dict(self) -> dict:
+        self.apply_pending()  # model and optimizer state of the same epoch
         sd = self.opt.state_dict()
         sd["state"]["local_epoch"] = self.local_epoch
         return sd
 
     def load_state_dict(self, state_dict: dict):
+        self.state_averager.drop_pending()
         sd = dict(state_dict)
         sd["state"] = dict(sd["state"])
         if "local_epoch" in sd["state"]:
@@ -407,6 +491,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         world, rank = _group_world(self.group)
         if world == 1:
             return False
+        self.apply_pending()  # the donor ships its newest parameters
         dev = self.device
         score = torch.tensor([float(self.local_epoch * world + (world - 1 - rank))], device=dev, dtype=torch.float64 if dev.type == "cpu" else torch.float32)
         dist.all_reduce(score, op=dist.ReduceOp.MAX, group=self.group)
@@ -436,6 +521,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         return rank != donor
 
     def shutdown(self):
+        self.apply_pending()
         self.tracker.shutdown()
 
 

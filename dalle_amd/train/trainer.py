@@ -203,5 +203,8 @@ class CollaborativeHFTrainer:
             self._call("on_step_end")
             if not math.isfinite(total):
                 logger.warning(f"non-finite loss at step {self.state.global_step}")
+        apply_pending = getattr(self.collaborative_optimizer, "apply_pending", None)
+        if apply_pending is not None:  # a delayed optimizer step still in flight lands in the model
+            apply_pending()
         self._call("on_train_end")
         return self.state
