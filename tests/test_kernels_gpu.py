@@ -174,3 +174,50 @@ def test_uniform8bit_quantization_kernel(cuda, n):
     assert torch.equal(c["idx"], c2["idx"]) and torch.equal(c["codebook"], c2["codebook"])
     back = comp.extract(c, n)
     assert ((back - x).norm() / x.norm()).item() < 0.05
+
+
+# ---- randomised geometries (hypothesis): ragged text lengths, both image grids, every pattern ----
+from hypothesis import given, settings, strategies as hst  # noqa: E402
+
+
+@settings(max_examples=10, deadline=None)
+@given(T=hst.integers(1, 300), S=hst.sampled_from([16, 32]), B=hst.integers(1, 2), H=hst.integers(1, 3),
+       attn_type=hst.sampled_from(["axial_row", "axial_col", "conv_like", "full"]), seed=hst.integers(0, 999))
+def test_sparse_attention_random_geometry(cuda, T, S, B, H, attn_type, seed):
+    from dalle_amd.ops import hip_ops
+    dev = cuda
+    torch.manual_seed(seed)
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = (torch.randn(B, n, 3 * H * 64, device=dev) * 1.5).to(torch.bfloat16).requires_grad_(True)
+    out = hip_ops.attention_core(qkv, H, geom, attn_type)
+    cos, sin = rotary_tables(T, S, 64, device=dev)
+    qr_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref.qkv_rotary(qr_in, H, cos, sin)
+    out_ref = ref.sparse_attention_core(q, k, v, geom, attn_type)
+    assert _rel(out, out_ref) < 2e-2, (T, S, attn_type)
+    g = torch.randn_like(out_ref)
+    out.backward(g.to(torch.bfloat16))
+    out_ref.backward(g.to(torch.bfloat16).float())
+    assert _rel(qkv.grad, qr_in.grad) < 3e-2, (T, S, attn_type)
+
+
+@settings(max_examples=10, deadline=None)
+@given(T=hst.integers(1, 300), S=hst.sampled_from([16, 32]), D=hst.sampled_from([256, 1024]), shift=hst.booleans(),
+       seed=hst.integers(0, 999))
+def test_layernorm_shift_random_geometry(cuda, T, S, D, shift, seed):
+    from dalle_amd.ops import hip_ops
+    dev = cuda
+    torch.manual_seed(seed)
+    n = T + S * S - 1
+    x = torch.randn(2, n, D, device=dev, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(D, device=dev)).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device=dev)).requires_grad_(True)
+    y = hip_ops.layernorm_shift(x, w, b, T, S, shift)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = ref.layernorm_shift(xr, wr, br, T, S, shift)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(x.grad, xr.grad) < 2e-2 and _rel(w.grad, wr.grad) < 2e-2 and _rel(b.grad, br.grad) < 2e-2
