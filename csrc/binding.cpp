@@ -43,6 +43,7 @@ void decode_rope(const void*, const float*, const float*, void*, void*, void*, c
                  hipStream_t);
 void decode_attn(const void*, const void*, const void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
 void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
+bool sample_step(const SampleArgs&, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
 void lamb_step(const float*, float*, const float*, float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*,
                const float*, const int*, const long*, const long*, const int*, const float*, const float*, const float*,
@@ -504,6 +505,42 @@ void decode_attn_(Tensor q, Tensor kc, Tensor vc, Tensor out, Tensor pos, int64_
   dalle::decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, BH / H, cur_stream());
 }
 
+// Fused sampler. Returns the raw samples (B,); with text/codes/tok given it also does the decode-step
+// bookkeeping at device position *pos (codes[:, pos - T + 1] = sample, tok = next input token).
+Tensor sample_step(Tensor logits, int64_t top_k, double top_p, double temperature, Tensor seed, Tensor pos,
+                   c10::optional<Tensor> text, c10::optional<Tensor> codes, c10::optional<Tensor> tok, int64_t vt) {
+  CHECK_IN(logits, torch::kFloat32); CHECK_IN(seed, torch::kInt64); CHECK_IN(pos, torch::kInt32);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) >= 1 && logits.size(1) <= 8192, "sample: logits must be (B, V <= 8192)");
+  TORCH_CHECK(seed.numel() == 1 && pos.numel() == 1, "sample: seed / pos are device scalars");
+  const int B = logits.size(0);
+  dalle::SampleArgs a{};
+  a.logits = logits.data_ptr<float>();
+  a.B = B;
+  a.V = logits.size(1);
+  a.top_k = (int)top_k;
+  a.top_p = (float)top_p;
+  a.temperature = (float)temperature;
+  a.seed = seed.data_ptr<int64_t>();
+  a.pos = pos.data_ptr<int>();
+  a.vt = vt;
+  const bool book = text.has_value();
+  TORCH_CHECK(book == codes.has_value() && book == tok.has_value(), "sample: give text, codes and tok together");
+  if (book) {
+    CHECK_IN((*text), torch::kInt64); CHECK_IN((*codes), torch::kInt64); CHECK_IN((*tok), torch::kInt64);
+    TORCH_CHECK(text->dim() == 2 && text->size(0) == B && codes->dim() == 2 && codes->size(0) == B && tok->numel() == B,
+                "sample: text (B, T), codes (B, image_len), tok (B,)");
+    a.text = text->data_ptr<int64_t>();
+    a.T = text->size(1);
+    a.codes = codes->data_ptr<int64_t>();
+    a.img_len = codes->size(1);
+    a.tok = tok->data_ptr<int64_t>();
+  }
+  auto out = torch::empty({B}, logits.options().dtype(torch::kInt64));
+  a.sampled = out.data_ptr<int64_t>();
+  TORCH_CHECK(dalle::sample_step(a, cur_stream()), "sample: unsupported shape");
+  return out;
+}
+
 Tensor vq_embed(Tensor idx, Tensor codebook, int64_t side) {
   CHECK_IN(idx, torch::kInt64); CHECK_IN(codebook, torch::kFloat32);
   const int B = idx.size(0), HW = idx.size(1), C = codebook.size(1);
@@ -610,6 +647,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_residual_", &skinny_residual_);
   m.def("skinny_qkv_rope_", &skinny_qkv_rope_);
   m.def("vq_embed", &vq_embed);
+  m.def("sample_step", &sample_step, py::arg("logits"), py::arg("top_k"), py::arg("top_p"), py::arg("temperature"),
+        py::arg("seed"), py::arg("pos"), py::arg("text") = py::none(), py::arg("codes") = py::none(),
+        py::arg("tok") = py::none(), py::arg("vt") = 0);
   m.def("lamb_grad_norm", &lamb_grad_norm);
   m.def("lamb_step", &lamb_step);
 }

@@ -1,5 +1,6 @@
 // Launch geometry structs shared by the HIP kernels and the (host-compiled) bindings.
 #pragma once
+#include <stdint.h>
 namespace dalle {
 struct AttnGeom {
   int T;        // text positions incl. BOS (257)
@@ -63,6 +64,23 @@ struct SkinnyArgs {
   int H, n;
   float qscale;
   int dbg;  // benchmark-only: bit 0 skips the X loads, bit 1 the W loads
+};
+
+// Fused decode sampler (sample.hip): top-k / top-p / temperature / Gumbel-max + token bookkeeping.
+struct SampleArgs {
+  const float* logits;  // (B, V) fp32
+  int B, V;
+  int top_k;            // <= 0 or >= V: off
+  float top_p;          // >= 1: off
+  float temperature;    // <= 1e-10: greedy
+  const int64_t* seed;  // device scalar
+  const int* pos;       // device scalar: the position this step ran
+  const int64_t* text;  // (B, T) caption ids (BOS first)
+  int T, img_len;
+  int64_t vt;           // text vocabulary size (image token id offset)
+  int64_t* codes;       // (B, img_len), may be null
+  int64_t* tok;         // (B,) next input token, may be null
+  int64_t* sampled;     // (B,) the raw sample, may be null
 };
 
 }  // namespace dalle

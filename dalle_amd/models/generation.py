@@ -12,6 +12,7 @@ The CPU path runs the same step with the reference ops (tests compare it against
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -70,12 +71,14 @@ class DecodeEngine:
         self.obuf = torch.zeros(B, self.H * self.Dh, dtype=self.cdt, device=dev)
         self.codes = torch.zeros(B, cfg.image_seq_len, dtype=torch.long, device=dev)
         self.temperature, self.top_k, self.top_p = 1.0, 0, 1.0
+        # fused HIP sampler (K18); its Gumbel noise is a counter hash of (seed, position, row, token)
+        self.fused_sampler = use_hip and os.environ.get("DALLE_AMD_FUSED_SAMPLER", "1") == "1"
+        self.seed = torch.zeros((), dtype=torch.int64, device=dev)
         self.graph = None
         self._static_logits = None
         self._w = {}
         # decode-step projections through the skinny MFMA GEMM (csrc/kernels/skinny.hip) with the
         # rotary / GEGLU / LayerScale-residual epilogues fused: M = batch <= 64 rows
-        import os
         self.skinny = (use_hip and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0
                        and os.environ.get("DALLE_AMD_SKINNY", "1") != "0")
         self.sk_cnt = torch.zeros(8192, dtype=torch.int32, device=dev) if self.skinny else None
@@ -235,6 +238,13 @@ class DecodeEngine:
         the next caption token while ``pos + 1 < T`` (prefill), else the sampled image token -- and
         record the sample as image code ``pos - T + 1`` (prefill writes are overwritten later)."""
         logits = self._forward_position()
+        if self.fused_sampler and logits.dtype == torch.float32 and logits.shape[-1] <= 8192:
+            # one HIP launch (csrc/kernels/sample.hip): filter + sample + codes / next-token bookkeeping
+            from ..ops.hip_ops import C
+            C().sample_step(logits, int(self.top_k or 0), float(1.0 if self.top_p is None else self.top_p),
+                            float(self.temperature), self.seed, self.pos, self.text_bos, self.codes, self.tok, self.Vt)
+            self.pos.add_(1)
+            return logits
         logits = filter_logits(logits, self.top_k, self.top_p)
         nxt = gumbel_sample(logits, self.temperature)
         p = self.pos.long()
@@ -267,10 +277,14 @@ class DecodeEngine:
 
     @torch.no_grad()
     def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
-                 use_graph: Optional[bool] = None) -> torch.Tensor:
+                 use_graph: Optional[bool] = None, seed: Optional[int] = None) -> torch.Tensor:
         """All ``seq_len`` positions (caption prefill + 1024 sampled image tokens) through one step
-        function; on MI355X that step is a single hipGraph replayed ``seq_len`` times."""
+        function; on MI355X that step is a single hipGraph replayed ``seq_len`` times. ``seed`` fixes
+        the fused sampler's noise (default: drawn from torch's global generator)."""
         self.temperature, self.top_k, self.top_p = temperature, top_k, top_p
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.seed.fill_(int(seed))
         use_graph = self.use_hip if use_graph is None else use_graph
         self._start(text_bos)
         if use_graph:

@@ -24,6 +24,7 @@ hip_sources = [
     "csrc/kernels/gemm.hip",
     "csrc/kernels/quant.hip",
     "csrc/kernels/skinny.hip",
+    "csrc/kernels/sample.hip",
     "csrc/kernels/powersgd.hip",
     "csrc/optim/lamb.hip",
 ]
