@@ -57,3 +57,52 @@ def test_vqgan_decode_shapes():
     z = vae.embed_codes(codes)
     one_hot = torch.nn.functional.one_hot(codes, 64).float() @ vae.codebook
     assert torch.allclose(z, one_hot.view(2, 8, 8, 32).permute(0, 3, 1, 2))
+
+
+_SMALL_DD = dict(ch=32, out_ch=3, ch_mult=(1, 2), num_res_blocks=1, attn_resolutions=(8,), resolution=16, z_channels=32)
+
+
+def test_vqgan_encoder_codes():
+    """get_codebook_indices (dalle-pytorch API): gumbel = argmax of the proj logits, plain VQ = nearest
+    codebook vector; taming checkpoint naming (incl. ``quantize.embedding``) loads; a decoder-only
+    checkpoint still decodes but refuses to encode."""
+    torch.manual_seed(0)
+    img = torch.rand(2, 3, 16, 16)
+    g = VQGanVAE(n_embed=64, embed_dim=32, ddconfig=_SMALL_DD, is_gumbel=True)
+    idx = g.get_codebook_indices(img)
+    assert idx.shape == (2, 64) and idx.dtype == torch.int64 and 0 <= idx.min() and idx.max() < 64
+    h = g.quant_conv(g.encoder(2 * img - 1))
+    assert torch.equal(idx, g.quantize.proj(h).argmax(1).flatten(1))
+    assert torch.equal(idx, g.get_codebook_indices(img))  # the mode is deterministic
+    s = g.get_codebook_indices(img, gumbel_tau=1.0, generator=torch.Generator().manual_seed(1))
+    assert s.shape == idx.shape
+    assert g.decode(idx).shape == (2, 3, 16, 16)
+
+    v = VQGanVAE(n_embed=64, embed_dim=32, ddconfig=_SMALL_DD, is_gumbel=False)
+    assert v.quantize.proj is None
+    vi = v.get_codebook_indices(img)
+    z = v.quant_conv(v.encoder(2 * img - 1)).permute(0, 2, 3, 1).reshape(-1, 32)
+    assert torch.equal(vi.flatten(), torch.cdist(z, v.codebook).argmin(1))
+
+
+def test_vqgan_checkpoint_naming(tmp_path):
+    torch.manual_seed(0)
+    src = VQGanVAE(n_embed=64, embed_dim=32, ddconfig=_SMALL_DD, is_gumbel=False)
+    sd = src.state_dict()
+    sd["quantize.embedding.weight"] = sd.pop("quantize.embed.weight")  # taming VectorQuantizer name
+    import yaml
+
+    cfg = tmp_path / "vq.yaml"
+    cfg.write_text(yaml.safe_dump({"model": {"target": "taming.models.vqgan.VQModel", "params": {
+        "n_embed": 64, "embed_dim": 32, "ddconfig": {**_SMALL_DD, "ch_mult": [1, 2], "attn_resolutions": [8]}}}}))
+    torch.save({"state_dict": sd}, tmp_path / "full.ckpt")
+    full = VQGanVAE(str(tmp_path / "full.ckpt"), str(cfg))
+    img = torch.rand(1, 3, 16, 16)
+    assert torch.equal(full.get_codebook_indices(img), src.get_codebook_indices(img))
+    dec_only = {k: v for k, v in sd.items() if not k.startswith(("encoder.", "quant_conv."))}
+    torch.save({"state_dict": dec_only}, tmp_path / "dec.ckpt")
+    d = VQGanVAE(str(tmp_path / "dec.ckpt"), str(cfg))
+    codes = torch.randint(0, 64, (1, 64))
+    assert torch.allclose(d.decode(codes), src.decode(codes))
+    with pytest.raises(RuntimeError):
+        d.get_codebook_indices(img)
