@@ -39,7 +39,10 @@ def wgrad_sweep(M):
         fl = 2 * M * N * K
         res = {"shape": f"wgrad_M{M}_N{N}_K{K}"}
         res["s1_TF"] = round(fl / timeit(lambda: torch.addmm(acc, g.t(), x, out_dtype=torch.float32, out=acc)) / 1e9)
-        for s in (2, 4, 8):
+        for s in (2, 4, 8, 16, 32):
+            if M % s or M // s < 1024:
+                continue
+
             def f(s=s):
                 part = torch.bmm(g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
                 C.splitk_accum_(acc, part, True)

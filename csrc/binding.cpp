@@ -11,7 +11,7 @@ namespace dalle {
 
 void attn_fwd(const void*, const void*, const void*, void*, float*, const AttnGeom&, int, hipStream_t);
 void attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*, void*, void*,
-              void*, const AttnGeom&, int, hipStream_t);
+              void*, const AttnGeom&, int, hipStream_t, const float*, const float*, void*, float);
 void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
 void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
 bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t);
@@ -218,8 +218,31 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor do
   auto dv = torch::empty_like(q);
   dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                   do_st.data_ptr(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), g, B * H,
-                  cur_stream());
+                  cur_stream(), nullptr, nullptr, nullptr, 0.f);
   return {dq, dk, dv};
+}
+
+// Attention backward with the rotary backward fused into its epilogues: returns dqkv (B, n, 3*H*64)
+// directly (no (B*H, Np, 64) dq / dk / dv intermediates, no rope_bwd pass).
+Tensor attn_bwd_rope(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, Tensor cosT, Tensor sinT, int64_t B,
+                     int64_t T, int64_t S, int64_t n, int64_t K, int64_t H, int64_t pattern, double qscale) {
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(k, torch::kBFloat16); CHECK_IN(v, torch::kBFloat16);
+  CHECK_IN(out, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16); CHECK_IN(lse, torch::kFloat32);
+  CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  auto g = make_attn_geom(T, S, n, K, H, pattern);
+  TORCH_CHECK(q.size(0) == B * H && q.size(1) == g.Np && q.size(2) == 64);
+  TORCH_CHECK(k.sizes() == q.sizes() && v.sizes() == q.sizes());
+  TORCH_CHECK(out.size(0) == B && out.size(1) == n && out.size(2) == H * 64 && dout.sizes() == out.sizes());
+  TORCH_CHECK(lse.numel() == B * H * g.Np);
+  TORCH_CHECK(cosT.dim() == 2 && cosT.size(0) >= n && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes(),
+              "attn_bwd_rope: rotary tables must be (>= n, 64)");
+  auto do_st = torch::empty_like(q);
+  auto delta = torch::empty({B * H, g.Np}, lse.options());
+  auto dqkv = torch::empty({B, n, 3 * H * 64}, q.options());
+  dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                  do_st.data_ptr(), delta.data_ptr<float>(), nullptr, nullptr, nullptr, g, B * H, cur_stream(),
+                  cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(), (float)qscale);
+  return dqkv;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -621,6 +644,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_bwd", &rope_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd_rope", &attn_bwd_rope);
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
   m.def("geglu_bwd_bias", &geglu_bwd_bias, py::arg("h"), py::arg("dout"), py::arg("gb") = py::none());

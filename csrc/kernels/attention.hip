@@ -14,6 +14,9 @@
 // Backward : dQ is query-centric (same schedule as the forward, recomputing P and dP);
 //            dK/dV is key-centric (each wave owns 32 keys, loops over the query tiles that see them)
 //            so no float atomics are needed anywhere.
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "geom.h"
 
@@ -178,6 +181,64 @@ __device__ __forceinline__ int acc_row(int r, int hl) { return (r & 3) + 8 * (r 
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
+
+// Fused rotary backward (replaces rope_bwd_kernel when `dqkv` is set): each backward kernel's dQ / dK
+// / dV tile is rotated back with its tokens' (cos, sin) rows -- rotary pairs are adjacent dims -- and
+// written straight into the token-major projection gradient dqkv (B, n, 3*H*64), slot t (0 q, 1 k,
+// 2 v). No (B*H, Np, 64) dq / dk / dv intermediates and no separate rotary pass (a 750 MB round trip
+// per layer at B48). The tile is re-laid out through LDS first (rope_bwd_store_half) so the table
+// reads and the stores are contiguous per token.
+struct RopeOut {
+  const float* cosT;
+  const float* sinT;
+  __bf16* dqkv;  // nullptr: write dq / dk / dv in storage layout instead
+  float qscale;
+};
+
+// One dim-half (dims 32 dt .. 32 dt + 31) of a wave's 32-token gradient tile, held in the MFMA
+// accumulator layout (lane c32 + 32 hl owns dims 32 dt + 8 gq + 4 hl + i from acc[4 gq + i]), is staged
+// through the wave's 4 KB LDS slot (fp32, 16-byte chunks XOR-swizzled by row) and re-read so that 4
+// lanes own one token's 32 contiguous dims: coalesced cos/sin row reads and 64-byte contiguous stores
+// per token into dqkv. The caller guarantees no other wave touches `stage` (4 KB, 16-byte aligned).
+__device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const AttnGeom& g, int bh, int s0, int t, int dt,
+                                                    const f32x16& acc, float scale, float* stage, int lane) {
+  const int hl = lane >> 5, c32 = lane & 31;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int ch = (2 * gq + hl) ^ (c32 & 7);
+    *reinterpret_cast<f32x4*>(stage + c32 * 32 + 4 * ch) = f32x4{acc[4 * gq], acc[4 * gq + 1], acc[4 * gq + 2], acc[4 * gq + 3]};
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
+  const int q4 = lane & 3;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int tok = it * 16 + (lane >> 2);
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4) ^ (tok & 7)));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4 + 1) ^ (tok & 7)));
+    const int p = st2seq(g, s0 + tok);
+    if (p < 0) continue;
+    const int d0 = 32 * dt + 8 * q4;
+    const float* cp = ro.cosT + (size_t)p * 64 + d0;
+    const float* sp = ro.sinT + (size_t)p * 64 + d0;
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+    const f32x4 n0 = *reinterpret_cast<const f32x4*>(sp), n1 = *reinterpret_cast<const f32x4*>(sp + 4);
+    const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const float c[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    const float sn[8] = {n0[0], n0[1], n0[2], n0[3], n1[0], n1[1], n1[2], n1[3]};
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {  // transposed rotation of the pair (i, i + 1)
+      const float a0 = x[i] * scale, a1 = x[i + 1] * scale;
+      y[i] = a0 * c[i] + a1 * sn[i + 1];
+      y[i + 1] = a1 * c[i + 1] + a0 * sn[i];
+    }
+    *reinterpret_cast<s16x8*>(ro.dqkv + ((size_t)b * g.n + p) * (3 * HD) + t * HD + h * 64 + d0) = pack8(y);
+  }
+  __builtin_amdgcn_wave_barrier();  // every lane has read the slot before it is rewritten
+}
+
 // ------------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------------
@@ -263,7 +324,8 @@ __device__ __forceinline__ void fwd_tiles(SoftmaxState& st, const __bf16* const 
 //   (double-buffered 2 x {Ka, Kb, Va, Vb}, register-staged loads issued before compute, T14).
 // Phase B (wave-private): each image query block streams ITS OWN local key tiles through a private
 //   LDS slot (reusing phase A's buffers) -- no workgroup barrier, no wave idling on other blocks' tiles.
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                           const __bf16* __restrict__ V, __bf16* __restrict__ out,
                                                           float* __restrict__ lse, AttnGeom g) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
@@ -419,10 +481,11 @@ __global__ void attn_bwd_prep_kernel(const __bf16* __restrict__ dout, const __bf
 // ------------------------------------------------------------------------------------------------
 // Backward dQ (query-centric)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
-                                                             __bf16* __restrict__ dQ, AttnGeom g) {
+                                                             __bf16* __restrict__ dQ, AttnGeom g, RopeOut ro) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
   int grp, bh;
   xcd_remap(grp, bh);
@@ -510,6 +573,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
     __syncthreads();
   }
   if (!active) return;
+  if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 4 KB
+    float* stage = reinterpret_cast<float*>(smem) + wave * 1024;
+    rope_bwd_store_half(ro, g, bh, qb * 32, 0, 0, dq0, ro.qscale, stage, lane);
+    rope_bwd_store_half(ro, g, bh, qb * 32, 0, 1, dq1, ro.qscale, stage, lane);
+    return;
+  }
   __bf16* qp = dQ + base + (size_t)qs * 64;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
@@ -531,10 +600,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const __bf16* __res
 // tiles {Q, dO, lse, delta} through a private LDS slot (register prefetch one tile ahead): no
 // workgroup barrier and no wave idling on the other blocks' tiles.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                                const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                const float* __restrict__ lse, const float* __restrict__ delta,
-                                                               __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
+                                                               __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g,
+                                                               RopeOut ro) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[4 * 2 * TILE];  // per wave {Q, dO}
   __shared__ float stats[4][2][32];                                   // per wave {lse, delta}
   int grp, bh;
@@ -616,6 +687,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
     dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
     __builtin_amdgcn_wave_barrier();
   }
+  if (ro.dqkv) {  // this wave's private {Q, dO} slot is free after its last tile
+    float* stage = reinterpret_cast<float*>(Qs);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 0, dk0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 1, dk1, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 0, dv0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 1, dv1, 1.0f, stage, lane);
+    return;
+  }
   __bf16* kp = dK + base + (size_t)ks * 64;
   __bf16* vp = dV + base + (size_t)ks * 64;
 #pragma unroll
@@ -641,10 +720,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const __bf16* __r
 // workgroup) while the critical path stays at half the query tiles. The two parity partials of each
 // key block are summed through LDS at the end (fixed order, deterministic).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                                     const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
-                                                                    __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g) {
+                                                                    __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g,
+                                                                    RopeOut ro) {
   // 2 stages x 2 parities x {Q, dO} tile images (32 KB) + the per-query stats
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 2 * TILE];
   __shared__ float stats[2][2][2][32];  // [stage][parity][lse | delta][row]
@@ -761,7 +842,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
     }
   }
   __syncthreads();
-  if (par == 0 && active) {
+  if (par == 0 && active && ro.dqkv) {
+    const float* mine = red + (wave & 1) * 64 * 64;
+    f32x16 sk0, sk1, sv0, sv1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sk0[r] = dk0[r] + mine[r * 64 + lane];
+      sk1[r] = dk1[r] + mine[(16 + r) * 64 + lane];
+      sv0[r] = dv0[r] + mine[(32 + r) * 64 + lane];
+      sv1[r] = dv1[r] + mine[(48 + r) * 64 + lane];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // this key block's 16 KB of partials are consumed: stage through them
+    __builtin_amdgcn_wave_barrier();
+    float* stage = red + (wave & 1) * 64 * 64;
+    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 0, sk0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 1, sk1, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 0, sv0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 1, sv1, 1.0f, stage, lane);
+  } else if (par == 0 && active) {
     __bf16* kp = dK + base + (size_t)ks * 64;
     __bf16* vp = dV + base + (size_t)ks * 64;
 #pragma unroll
@@ -787,27 +885,49 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_text_kernel(const __bf16
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+// Occupancy variant per kernel (workgroups per CU the register budget is compiled for), overridable
+// with DALLE_AMD_ATTN_OCC="fwd,dq,dkdv_text,dkdv". Measured at B48 (profiles/r1_attn_occupancy.txt):
+// the forward is latency-bound at 2 waves/SIMD (178 VGPRs) and runs 225 -> 183 us at 3 (168 VGPRs,
+// 20 B/lane of spill); dq fits 148 VGPRs either way; the dK/dV kernels spill 184-292 B/lane at 3 and
+// slow down 1.9-2.8x, so they stay at 2.
+static int attn_occ(int which) {
+  static int occ[4] = {0, 0, 0, 0};
+  if (occ[0] == 0) {
+    int v[4] = {3, 3, 2, 2};
+    if (const char* e = getenv("DALLE_AMD_ATTN_OCC")) sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]);
+    for (int i = 0; i < 4; ++i) occ[i] = (v[i] == 3) ? 3 : 2;
+  }
+  return occ[which];
+}
+
+#define ATTN_LAUNCH(kern, which, grid, ...)                                                      \
+  do {                                                                                           \
+    if (attn_occ(which) == 3) hipLaunchKernelGGL(kern<3>, grid, dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, st, __VA_ARGS__);                      \
+  } while (0)
+
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
   dim3 grid((g.Np / 32 + 3) / 4, BH);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                     (__bf16*)out, lse, g);
+  ATTN_LAUNCH(attn_fwd_kernel, 0, grid, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (__bf16*)out, lse, g);
 }
 
 void attn_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
-              void* do_st, float* delta, void* dq, void* dk, void* dv, const AttnGeom& g, int BH, hipStream_t st) {
+              void* do_st, float* delta, void* dq, void* dk, void* dv, const AttnGeom& g, int BH, hipStream_t st,
+              const float* cosT, const float* sinT, void* dqkv, float qscale) {
+  const RopeOut ro{cosT, sinT, static_cast<__bf16*>(dqkv), qscale};
   const int rows = BH * g.Np;
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st, (const __bf16*)dout,
                      (const __bf16*)out, (__bf16*)do_st, delta, g, BH);
   dim3 grid((g.Np / 32 + 3) / 4, BH);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                     (const __bf16*)do_st, lse, delta, (__bf16*)dq, g);
+  ATTN_LAUNCH(attn_bwd_dq_kernel, 1, grid, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)do_st,
+              lse, delta, (__bf16*)dq, g, ro);
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
   // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
-  hipLaunchKernelGGL(attn_bwd_dkdv_text_kernel, dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                     (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
+  ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
+              (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
   // image key blocks (short, local patterns): four blocks per workgroup
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((nimg + 3) / 4, BH), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                     (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g);
+  ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+              (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
 }
 
 }  // namespace dalle

@@ -44,11 +44,15 @@ def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     if w.dtype == torch.bfloat16:
         return w
     key = id(w)
+    # id() and the storage address can both be recycled by a new tensor between forwards: the entry
+    # must also match shape and version counter (begin_forward() clears everything per forward, which
+    # covers the optimizer's raw-pointer updates)
+    stamp = (w.data_ptr(), tuple(w.shape), w._version)
     hit = _wcache.get(key)
-    if hit is not None and hit[0] == w.data_ptr():
+    if hit is not None and hit[0] == stamp:
         return hit[1]
     wb = w.detach().to(torch.bfloat16)
-    _wcache[key] = (w.data_ptr(), wb)
+    _wcache[key] = (stamp, wb)
     return wb
 
 
@@ -87,6 +91,8 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
 SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
 # QKV projection through the hand-written GEMM with the rotary in its epilogue (csrc/kernels/gemm.hip)
 FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "1"))
+# rotary backward fused into the attention-backward epilogues (csrc/kernels/attention.hip RopeOut)
+FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
 
 
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
@@ -268,8 +274,11 @@ class _AttnCore(torch.autograd.Function):
         q, k, v, out, lse, cos, sin = ctx.saved_tensors
         B, T, S, n, K, H, pattern, col = ctx.geo
         gout = gout.to(torch.bfloat16).contiguous()
-        dq, dk, dv = C().attn_bwd(q, k, v, out, gout, lse, B, T, S, n, K, H, pattern)
-        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125)
+        if FUSED_ROPE_BWD:
+            dqkv = C().attn_bwd_rope(q, k, v, out, gout, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125)
+        else:
+            dq, dk, dv = C().attn_bwd(q, k, v, out, gout, lse, B, T, S, n, K, H, pattern)
+            dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125)
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -352,10 +361,14 @@ def _attn_bwd(saved, params, needs, g, resid):
     o2 = out.view(-1, out.shape[-1])
     do = torch.mm(dy, wo).view(out.shape)
     dwo = weight_grad(w_out, dy, o2)
-    dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
-    del do
-    dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
-    del dq, dk, dv
+    if FUSED_ROPE_BWD:  # rotary backward inside the attention-backward epilogues
+        dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
+        del do
+    else:
+        dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
+        del do
+        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
+        del dq, dk, dv
     dh = torch.mm(dqkv, wq).view(x.shape)
     dwq = weight_grad(w_qkv, dqkv, h2)
     resid = resid.contiguous() if resid is not None else None

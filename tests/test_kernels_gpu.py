@@ -221,3 +221,24 @@ def test_layernorm_shift_random_geometry(cuda, T, S, D, shift, seed):
     y.backward(g)
     yr.backward(g.float())
     assert _rel(x.grad, xr.grad) < 2e-2 and _rel(w.grad, wr.grad) < 2e-2 and _rel(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
+def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type, monkeypatch):
+    """attn_bwd_rope (rotary backward in the attention-backward epilogues) == attn_bwd + rope_bwd."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(3)
+    T, S, B, H = 257, 32, 2, 3
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = (torch.randn(B, n, 3 * H * 64, device=cuda)).to(torch.bfloat16)
+    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
+    grads = []
+    for fused in (1, 0):
+        monkeypatch.setattr(hip_ops, "FUSED_ROPE_BWD", fused)
+        x = qkv.clone().requires_grad_(True)
+        hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+        grads.append(x.grad.float())
+    # one bf16 rounding (fused) vs two (separate pass)
+    assert _rel(grads[0], grads[1]) < 8e-3, attn_type
