@@ -36,8 +36,10 @@ __global__ void geglu_bwd_kernel(const __bf16* __restrict__ h, const __bf16* __r
   unpack8(*reinterpret_cast<const s16x8*>(dout + r * F + c), d);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    da[i] = d[i] * gelu_erf(gg[i]);
-    dg[i] = d[i] * a[i] * gelu_erf_grad(gg[i]);
+    float ge, gr;
+    gelu_and_grad(gg[i], ge, gr);
+    da[i] = d[i] * ge;
+    dg[i] = d[i] * a[i] * gr;
   }
   *reinterpret_cast<s16x8*>(dh + r * 2 * F + c) = pack8(da);
   *reinterpret_cast<s16x8*>(dh + r * 2 * F + F + c) = pack8(dg);
@@ -73,8 +75,10 @@ __global__ __launch_bounds__(256) void geglu_bwd_bias_kernel(const __bf16* __res
       unpack8(vd[u], d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        da[i] = d[i] * gelu_erf(gg[i]);
-        dg[i] = d[i] * a[i] * gelu_erf_grad(gg[i]);
+        float ge, gr;
+        gelu_and_grad(gg[i], ge, gr);
+        da[i] = d[i] * ge;
+        dg[i] = d[i] * a[i] * gr;
       }
       const s16x8 pa = pack8(da), pg = pack8(dg);
       *reinterpret_cast<s16x8*>(dh + rr * 2 * F + j) = pa;
@@ -93,8 +97,10 @@ __global__ __launch_bounds__(256) void geglu_bwd_bias_kernel(const __bf16* __res
     unpack8(*reinterpret_cast<const s16x8*>(dout + r * F + j), d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      da[i] = d[i] * gelu_erf(gg[i]);
-      dg[i] = d[i] * a[i] * gelu_erf_grad(gg[i]);
+      float ge, gr;
+      gelu_and_grad(gg[i], ge, gr);
+      da[i] = d[i] * ge;
+      dg[i] = d[i] * a[i] * gr;
     }
     const s16x8 pa = pack8(da), pg = pack8(dg);
     *reinterpret_cast<s16x8*>(dh + r * 2 * F + j) = pa;
