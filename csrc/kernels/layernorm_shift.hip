@@ -94,24 +94,44 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
   const int wave0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   float dwa[PER][4] = {}, dba[PER][4] = {};
-  for (int row = wave0; row < rows; row += nwaves) {
+  // software pipeline: the next row's x / shifted dy / residual-grad loads are in flight while this
+  // row's two wave reductions run (the kernel is latency-bound at 2 waves per SIMD otherwise)
+  auto fetch = [&](int row, f32x4 (&xv)[PER], f32x4 (&rv)[PER], s16x4 (&dv)[PER], float& mean, float& rstd) {
     const int b = row / g.n, p = row - b * g.n;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[PER][4], gy[PER][4];
-    float s1 = 0.f, s2 = 0.f;
+    mean = mean_in[row];
+    rstd = rstd_in[row];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = 4 * (lane + 64 * j);
       const int grp = c < D / 4 ? 0 : (c < D / 2 ? 1 : 2);
       const int gsh = (g.shift && p < g.T && grp == 1) ? 0 : grp;
       const int dst = shift_dest(g, p, gsh);
-      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)row * D + c);
+      xv[j] = *reinterpret_cast<const f32x4*>(x + (size_t)row * D + c);
+      rv[j] = resid ? *reinterpret_cast<const f32x4*>(resid + (size_t)row * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j] = dst >= 0 ? *reinterpret_cast<const s16x4*>(dy + ((size_t)b * g.n + dst) * D + c) : s16x4{0, 0, 0, 0};
+    }
+  };
+  f32x4 xa[PER], ra[PER];
+  s16x4 da[PER];
+  float ma = 0.f, sa = 0.f;
+  if (wave0 < rows) fetch(wave0, xa, ra, da, ma, sa);
+  for (int row = wave0; row < rows; row += nwaves) {
+    f32x4 xb[PER], rb[PER];
+    s16x4 db[PER];
+    float mb = 0.f, sb = 0.f;
+    if (row + nwaves < rows) fetch(row + nwaves, xb, rb, db, mb, sb);
+    const float mean = ma, rstd = sa;
+    float xh[PER][4], gy[PER][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = 4 * (lane + 64 * j);
       const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
-      float gv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (dst >= 0) unpack4(*reinterpret_cast<const s16x4*>(dy + ((size_t)b * g.n + dst) * D + c), gv);
+      float gv[4];
+      unpack4(da[j], gv);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        xh[j][i] = (xv[i] - mean) * rstd;
+        xh[j][i] = (xa[j][i] - mean) * rstd;
         gy[j][i] = gv[i] * wv[i];
         dwa[j][i] += gv[i] * xh[j][i];
         dba[j][i] += gv[i];
@@ -124,12 +144,15 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = 4 * (lane + 64 * j);
-      f32x4 o = {0.f, 0.f, 0.f, 0.f};
-      if (resid) o = *reinterpret_cast<const f32x4*>(resid + (size_t)row * D + c);
+      f32x4 o = ra[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] += rstd * (gy[j][i] - s1 - xh[j][i] * s2);
       *reinterpret_cast<f32x4*>(dx + (size_t)row * D + c) = o;
     }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { xa[j] = xb[j]; ra[j] = rb[j]; da[j] = db[j]; }
+    ma = mb;
+    sa = sb;
   }
   // deterministic two-stage reduction of dweight / dbias (no atomics: every workgroup adding into the
   // same D columns is the worst case for float atomics): waves -> LDS -> one partial row per block.
