@@ -153,7 +153,8 @@ def main():
     value = samples / elapsed
     ms = elapsed / args.steps * 1000
     if rank == 0:
-        tflops = cfg.train_flops_per_sample() * value / world / 1e12
+        tflops = cfg.train_flops_per_sample() * value / world / 1e12  # model FLOPs (no recompute)
+        hw_tflops = cfg.train_flops_per_sample(include_recompute=True) * value / world / 1e12
         print(json.dumps({
             "metric": "training samples/sec (whole node), DALL-E d_model=1024 at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -175,6 +176,7 @@ def main():
                        "grad_compression": args.compression if args.compression != "powersgd"
                        else f"powersgd-rank{args.powersgd_rank}"},
             "model_tflops_per_gpu": round(tflops, 1),
+            "hw_tflops_per_gpu": round(hw_tflops, 1),
             "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1),
             "loss": round(final_loss, 4),
         }), flush=True)

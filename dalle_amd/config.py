@@ -118,15 +118,17 @@ class DALLEConfig:
         head = self.total_tokens * d + self.total_tokens + 2 * d
         return n_attn * attn + n_ff * ff + self.depth * per_layer + head
 
-    def train_flops_per_sample(self) -> float:
-        """Matmul FLOPs of one training sample (fwd + bwd (+ reversible recompute))."""
+    def train_flops_per_sample(self, include_recompute: bool = False) -> float:
+        """Matmul FLOPs of one training sample: forward + backward (3x forward) = MODEL FLOPs, the MFU
+        convention. ``include_recompute`` adds the reversible stack's extra forward recompute (the
+        HARDWARE FLOPs actually executed when the activations are rebuilt instead of stored)."""
         d, inner, n = self.dim, self.inner_dim, self.seq_len
         per_layer = 2 * n * (d * 3 * inner + inner * d + d * 2 * self.ff_mult * d + self.ff_mult * d * d)
         # sparse attention scores: image queries see text + local keys, text is causal
         t, i = self.text_len, self.image_seq_len
         per_layer += 4 * self.heads * self.dim_head * (t * t / 2 + i * (t + self.image_fmap_size))
         head = 2 * (self.text_seq_len * self.total_text_tokens + self.image_seq_len * self.num_image_tokens) * d
-        layer_mult = 4.0 if self.reversible else 3.0  # reversible adds one forward recompute
+        layer_mult = 4.0 if (self.reversible and include_recompute) else 3.0
         return layer_mult * self.depth * per_layer + 3.0 * head
 
 
