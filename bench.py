@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: K more steps with per-phase timing (+ torch.profiler trace)")
     ap.add_argument("--trace", default="", help="chrome trace path for the --profile-steps pass")
+    ap.add_argument("--no-recompute", action="store_true",
+                    help="reversible presets: keep the activations instead of rebuilding them in backward")
     ap.add_argument("--tunable", default="off", choices=["auto", "use", "tune", "off"],
                     help="hipBLASLt solution selection for the library GEMMs (dalle_amd/utils/tuning.py)")
     return ap.parse_args()
@@ -80,6 +82,8 @@ def main():
     tuning = setup_gemm_tuning(args.tunable if (args.tunable != "tune" or rank == 0) else "use")
 
     cfg = get_config(args.model)
+    if args.no_recompute:
+        cfg.reversible_recompute = False
     torch.manual_seed(1234)
     model = DALLE(cfg).to(device)
     arena = FlatArena(model.parameters(), device=device)
@@ -173,6 +177,7 @@ def main():
                        "seq_len": cfg.seq_len, "parallelism": f"dp{world}",
                        "optimizer": f"LAMB ({args.optim_bits}-bit moments) + global clip 4.0",
                        "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning,
+                       "reversible": ("recompute" if cfg.reversible_recompute else "stored activations") if cfg.reversible else "no",
                        "grad_compression": args.compression if args.compression != "powersgd"
                        else f"powersgd-rank{args.powersgd_rank}"},
             "model_tflops_per_gpu": round(tflops, 1),

@@ -180,7 +180,7 @@ class Transformer(nn.Module):
                                 f.scale, attn.heads, attn.attn_type, pre.fn.enabled),
                                (gpre.norm.weight, gpre.norm.bias, ff.net[0].weight, ff.net[0].bias, ff.net[3].weight,
                                 ff.net[3].bias, g.scale, gpre.fn.enabled)))
-            return ops.reversible_stack(x, layers, self.geom, cfg.text_len, cfg.image_fmap_size)
+            return ops.reversible_stack(x, layers, self.geom, cfg.text_len, cfg.image_fmap_size, cfg.reversible_recompute)
         if self.cfg.reversible:
             fns = [(lambda t, f=f: ops.scale_rows(self._attn_out(f, t), f.scale),
                     lambda t, g=g: ops.scale_rows(self._ff_out(g, t), g.scale)) for f, g in pairs]

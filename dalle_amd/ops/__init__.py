@@ -121,9 +121,9 @@ def fused_reversible_available(x) -> bool:
     return x.is_cuda and backend_for(x) == "hip" and os.environ.get("DALLE_AMD_FUSED_REVERSIBLE", "1") != "0"
 
 
-def reversible_stack(x, layers, geom, text_len: int, image_size: int):
+def reversible_stack(x, layers, geom, text_len: int, image_size: int, recompute: bool = True):
     """Reversible residual stack over the fused attention / FF sublayers (HIP only)."""
-    return _hip().reversible_stack(x, layers, geom, text_len, image_size)
+    return _hip().reversible_stack(x, layers, geom, text_len, image_size, recompute)
 
 
 def begin_forward():

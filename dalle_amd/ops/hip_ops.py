@@ -470,14 +470,18 @@ class _FFSublayer(torch.autograd.Function):
 # ---------------------------------------------------------------------------------------------
 class _ReversibleFused(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, blocks, *params):
+    def forward(ctx, x, blocks, recompute, *params):
         x1 = x2 = x.contiguous()
+        stored = None if recompute else []
         with torch.no_grad():
             for fa, ga in blocks:
-                x1, _ = _attn_fwd(x1, x2, *fa[0], save=False)
-                x2, _ = _ff_fwd(x2, x1, *ga[0], save=False)
+                x1, sf = _attn_fwd(x1, x2, *fa[0], save=not recompute)
+                x2, sg = _ff_fwd(x2, x1, *ga[0], save=not recompute)
+                if stored is not None:
+                    stored.append((sf, sg))
         ctx.blocks = blocks
         ctx.params = params
+        ctx.stored = stored
         ctx.save_for_backward(x1, x2)
         return (x1 + x2) * 0.5
 
@@ -495,28 +499,36 @@ class _ReversibleFused(torch.autograd.Function):
                 k = id(p)
                 pending[k] = gr if k not in pending else pending[k] + gr
 
+        stored, ctx.stored = ctx.stored, None
         with torch.no_grad():
-            for fa, ga in reversed(blocks):
+            for bi in reversed(range(len(blocks))):
+                fa, ga = blocks[bi]
                 g_args, g_params = ga
-                x2, saved = _ff_fwd(y2, y1, *g_args, save=True, sign=-1.0)
-                res = _ff_bwd(saved, g_params, [p.requires_grad for p in g_params], dy2, dy1)
-                del saved
+                f_args, f_params = fa
+                if stored is None:  # rebuild this block's inputs (and activations) from its outputs
+                    x2, saved_g = _ff_fwd(y2, y1, *g_args, save=True, sign=-1.0)
+                else:
+                    saved_f, saved_g = stored.pop()
+                res = _ff_bwd(saved_g, g_params, [p.requires_grad for p in g_params], dy2, dy1)
+                del saved_g
                 dy1 = res[0]
                 collect(g_params, res[1:])
-                f_args, f_params = fa
-                x1, saved = _attn_fwd(y1, x2, *f_args, save=True, sign=-1.0)
-                res = _attn_bwd(saved, f_params, [p.requires_grad for p in f_params], dy1, dy2)
-                del saved
+                if stored is None:
+                    x1, saved_f = _attn_fwd(y1, x2, *f_args, save=True, sign=-1.0)
+                    y1, y2 = x1, x2
+                res = _attn_bwd(saved_f, f_params, [p.requires_grad for p in f_params], dy1, dy2)
+                del saved_f
                 dy2 = res[0]
                 collect(f_params, res[1:])
-                y1, y2 = x1, x2
         dx = dy1 + dy2
-        return (dx, None, *[pending.get(id(p)) for p in ctx.params])
+        return (dx, None, None, *[pending.get(id(p)) for p in ctx.params])
 
 
-def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int):
+def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int, recompute: bool = True):
     """``layers``: per block ((ln_w, ln_b, w_qkv, w_out, b_out, scale, heads, attn_type, shift),
-    (ln_w, ln_b, w1, b1, w2, b2, scale, shift)). Returns mean(y1, y2) of the reversible stack."""
+    (ln_w, ln_b, w1, b1, w2, b2, scale, shift)). Returns mean(y1, y2) of the reversible stack.
+    ``recompute=False`` keeps every block's activations from the forward instead of rebuilding them
+    in backward (same coupling math; one forward less per step for ~depth x the activation memory)."""
     blocks, uniq, seen = [], [], set()
     for (aln_w, aln_b, w_qkv, w_out, b_out, ascale, heads, attn_type, ashift), (fln_w, fln_b, w1, b1, w2, b2, fscale, fshift) in layers:
         dim_head = w_qkv.shape[0] // 3 // heads
@@ -531,7 +543,7 @@ def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: i
             if id(p) not in seen:
                 seen.add(id(p))
                 uniq.append(p)
-    return _ReversibleFused.apply(x, blocks, *uniq)
+    return _ReversibleFused.apply(x, blocks, bool(recompute), *uniq)
 
 
 def attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):

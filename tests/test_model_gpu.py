@@ -94,3 +94,26 @@ def test_fused_reversible_matches_unfused(cuda, arena, monkeypatch):
     for name, g in g1.items():
         rel = ((g - g2[name]).norm() / (g2[name].norm() + 1e-8)).item()
         assert rel < 2e-2, (name, rel)
+
+
+def test_reversible_stored_activations_match_recompute(cuda):
+    """reversible_recompute=False (activations kept from the forward) == the rebuild-in-backward path:
+    same loss bitwise, gradients equal up to the reconstruction rounding of the recompute."""
+    torch.manual_seed(0)
+    cfg = _cfg(True)
+    m = DALLE(cfg).to(cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+    grads, losses = [], []
+    for recompute in (True, False):
+        m.cfg.reversible_recompute = recompute
+        m.zero_grad(set_to_none=True)
+        loss = m(text, img, return_loss=True)
+        loss.backward()
+        losses.append(loss.item())
+        grads.append({n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None})
+    m.cfg.reversible_recompute = True
+    assert losses[0] == losses[1]
+    for n, g in grads[0].items():
+        rel = ((g - grads[1][n]).norm() / (g.norm() + 1e-8)).item()
+        assert rel < 2e-2, (n, rel)
