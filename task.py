@@ -80,6 +80,7 @@ class TrainingTask:
         self.tokenizer.pad_token = self.tokenizer.eos_token
         if cfg.text_seq_len != trainer_args.text_seq_length:
             cfg = type(cfg)(**{**cfg.to_dict(), "text_seq_len": trainer_args.text_seq_length})
+        cfg.reversible_recompute = bool(trainer_args.reversible_recompute)
         self.config = cfg
 
         logger.info(f"Creating model ({trainer_args.model_preset}: depth {cfg.depth}, dim {cfg.dim})")
