@@ -200,12 +200,17 @@ struct RopeOut {
 // through the wave's 4 KB LDS slot (fp32, 16-byte chunks XOR-swizzled by row) and re-read so that 4
 // lanes own one token's 32 contiguous dims: coalesced cos/sin row reads and 64-byte contiguous stores
 // per token into dqkv. The caller guarantees no other wave touches `stage` (4 KB, 16-byte aligned).
+// 16-byte chunk swizzle of the staging slot (rows of 128 B): a bijection on row & 7 (so the ds_write_b128
+// groups of 8 consecutive rows hit 8 distinct chunk slots) whose parity is bit 2 of the row (so each
+// ds_read_b128 lane group -- 4 rows x 4 lanes, two rows of each parity -- covers all 16 slots of 256 B).
+__device__ __forceinline__ int stage_swz(int row) { return ((row >> 2) & 1) | ((row & 3) << 1); }
+
 __device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const AttnGeom& g, int bh, int s0, int t, int dt,
                                                     const f32x16& acc, float scale, float* stage, int lane) {
   const int hl = lane >> 5, c32 = lane & 31;
 #pragma unroll
   for (int gq = 0; gq < 4; ++gq) {
-    const int ch = (2 * gq + hl) ^ (c32 & 7);
+    const int ch = (2 * gq + hl) ^ stage_swz(c32);
     *reinterpret_cast<f32x4*>(stage + c32 * 32 + 4 * ch) = f32x4{acc[4 * gq], acc[4 * gq + 1], acc[4 * gq + 2], acc[4 * gq + 3]};
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -215,8 +220,8 @@ __device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const Att
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int tok = it * 16 + (lane >> 2);
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4) ^ (tok & 7)));
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4 + 1) ^ (tok & 7)));
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4) ^ stage_swz(tok)));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4 + 1) ^ stage_swz(tok)));
     const int p = st2seq(g, s0 + tok);
     if (p < 0) continue;
     const int d0 = 32 * dt + 8 * q4;
