@@ -44,6 +44,8 @@ void decode_rope(const void*, const float*, const float*, void*, void*, void*, c
 void decode_attn(const void*, const void*, const void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
 void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 bool sample_step(const SampleArgs&, hipStream_t);
+bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
+void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
 void lamb_step(const float*, float*, const float*, float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*,
                const float*, const int*, const long*, const long*, const int*, const float*, const float*, const float*,
@@ -285,6 +287,29 @@ std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout, c10::optional<Tensor> 
   }
   dalle::geglu_bwd_bias(h.data_ptr(), dout.data_ptr(), dh.data_ptr(), part.data_ptr<float>(),
                         dalle::GradSink{pb, nullptr, nullptr, (int)F2, db.defined() ? 0 : 1}, M, F2 / 2, cur_stream());
+  return {dh, db};
+}
+
+// FF-out dgrad GEMM with the GEGLU backward + FF-in bias grad in its epilogue (csrc/kernels/gemm.hip
+// EPI 2): dy (M, K) bf16, w2t = W2^T (F, K) bf16, h = FF-in pre-activation (M, 2F) -> (dh, dbias).
+std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
+  CHECK_IN(dy, torch::kBFloat16); CHECK_IN(w2t, torch::kBFloat16); CHECK_IN(h, torch::kBFloat16);
+  TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2, "ff_dgrad_geglu: 2-D operands");
+  const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
+  TORCH_CHECK(w2t.size(1) == K && h.size(0) == M && h.size(1) == 2 * F, "ff_dgrad_geglu: shape mismatch");
+  TORCH_CHECK(M % 256 == 0 && F % 256 == 0 && K % 64 == 0, "ff_dgrad_geglu: M, F multiples of 256 and K of 64");
+  auto dh = torch::empty_like(h);
+  auto part = torch::empty({M / 128, 2 * F}, h.options().dtype(torch::kFloat32));
+  float* pb = sink_ptr(gb, 2 * F, "ff_dgrad_geglu dbias");
+  Tensor db;
+  if (!pb) {
+    db = torch::empty({2 * F}, h.options().dtype(torch::kFloat32));
+    pb = db.data_ptr<float>();
+  }
+  TORCH_CHECK(dalle::gemm_geglu_bwd(dy.data_ptr(), w2t.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), M, F, K,
+                                    cur_stream()), "ff_dgrad_geglu: unsupported shape");
+  dalle::column_sum(part.data_ptr<float>(), M / 128, 2 * F, dalle::GradSink{pb, nullptr, nullptr, (int)(2 * F), db.defined() ? 0 : 1},
+                    cur_stream());
   return {dh, db};
 }
 
@@ -648,6 +673,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
   m.def("geglu_bwd_bias", &geglu_bwd_bias, py::arg("h"), py::arg("dout"), py::arg("gb") = py::none());
+  m.def("ff_dgrad_geglu", &ff_dgrad_geglu, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
   m.def("scale_residual_", &scale_residual_);
   m.def("scale_residual_out", &scale_residual_out);
   m.def("scale_residual_bwd", &scale_residual_bwd, py::arg("g"), py::arg("y"), py::arg("scale"),

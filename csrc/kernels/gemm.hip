@@ -176,6 +176,12 @@ struct RopeEpi {
   const float* sinT;
   int T, Tp, S, logS, n, Np, H, col_major;
   float qscale;
+  // EPI 2 (GEGLU backward fused into the FF-out dgrad GEMM, see gemm_geglu_bwd): h = the FF-in
+  // pre-activation [value | gate] (M, 2F), dh its gradient, part = per-128-row partial bias grads
+  const __bf16* gh;
+  __bf16* gdh;
+  float* gpart;
+  int F;
 };
 
 __device__ __forceinline__ int rope_epi_seq2st(const RopeEpi& e, int p) {
@@ -251,6 +257,50 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
       const int row = idx >> 3, ch = idx & 7;
       const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
       *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+    }
+  } else if (EPI == 2) {
+    // GEGLU backward: the staged tile is du = dy . W2 (bf16, as the unfused path rounds it) for F-columns
+    // [c0, c0 + 64); each lane owns one 8-column chunk of 16 rows: da_value = du * gelu(gate),
+    // da_gate = du * value * gelu'(gate) straight into dh, and the chunk's column sums of the propagated
+    // (bf16) values -- the FF-in bias gradient -- reduced over the 8 lanes sharing it (fixed xor tree)
+    // into one partial row per 128-row wave block.
+    const int F = rope.F;
+    const int c = col0 + wn * 64 + (lane & 7) * 8;
+    float sv[8] = {}, sg[8] = {};
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 8 + (lane >> 3), ch = lane & 7;
+      const size_t r = (size_t)(row0 + wm * 128 + row);
+      float d[8], a[8], gg[8], da[8], dg[8];
+      unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), d);
+      unpack8(*reinterpret_cast<const s16x8*>(rope.gh + r * 2 * F + c), a);
+      unpack8(*reinterpret_cast<const s16x8*>(rope.gh + r * 2 * F + F + c), gg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float ge, gr;
+        gelu_and_grad(gg[i], ge, gr);
+        da[i] = d[i] * ge;
+        dg[i] = d[i] * a[i] * gr;
+      }
+      const s16x8 pa = pack8(da), pg = pack8(dg);
+      *reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + c) = pa;
+      *reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + F + c) = pg;
+      unpack8(pa, da);
+      unpack8(pg, dg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sv[i] += da[i]; sg[i] += dg[i]; }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sv[i] += __shfl_xor(sv[i], o, 64);
+        sg[i] += __shfl_xor(sg[i], o, 64);
+      }
+    if (lane < 8) {
+      float* pr = rope.gpart + (size_t)((row0 >> 7) + wm) * 2 * F;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { pr[c + i] = sv[i]; pr[F + c + i] = sg[i]; }
     }
   } else {
     // the wave's 64 columns are exactly one (part, head): rotate each 8-column chunk of each row and
@@ -593,6 +643,23 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
       }
       return false;
   }
+}
+
+// FF-out dgrad with the GEGLU backward in the epilogue: du = dy (M, K) . W2^T where w2t = W2^T (F, K)
+// bf16, then dh (M, 2F) = GEGLU'(h, du) and part ((M / 128), 2F) = partial FF-in bias grads. The
+// (M, F) du intermediate never exists.
+bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, float* part, int M, int F, int K,
+                    hipStream_t st) {
+  if (M % GBM || F % GBN || K % GBK) return false;
+  RopeEpi e{};
+  e.gh = (const __bf16*)h;
+  e.gdh = (__bf16*)dh;
+  e.gpart = part;
+  e.F = F;
+  const int nwg = (M / GBM) * (F / GBN);
+  hipLaunchKernelGGL((gemm_nt_8ph_kernel<2, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
+                     (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);
+  return true;
 }
 
 // QKV projection + rotary into the attention storage layout (q pre-scaled); M = B*n rows

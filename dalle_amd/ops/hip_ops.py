@@ -56,6 +56,19 @@ def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     return wb
 
 
+def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
+    """Transposed (in, out) bf16 copy of a Linear weight, cached per forward like ``bf16_weight``: the
+    B operand of an NT GEMM that multiplies by W instead of W^T (the fused FF dgrad)."""
+    key = ("t", id(w))
+    stamp = (w.data_ptr(), tuple(w.shape), w._version)
+    hit = _wcache.get(key)
+    if hit is not None and hit[0] == stamp:
+        return hit[1]
+    wt = bf16_weight(w).t().contiguous()
+    _wcache[key] = (stamp, wt)
+    return wt
+
+
 _tables: Dict[tuple, tuple] = {}
 
 
@@ -93,6 +106,8 @@ SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
 FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "1"))
 # rotary backward fused into the attention-backward epilogues (csrc/kernels/attention.hip RopeOut)
 FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
+# GEGLU backward fused into the FF-out dgrad GEMM epilogue (csrc/kernels/gemm.hip EPI 2)
+FUSED_GEGLU_DGRAD = int(os.environ.get("DALLE_AMD_FUSED_GEGLU_DGRAD", "1"))
 
 
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
@@ -414,10 +429,16 @@ def _ff_bwd(saved, params, needs, g, resid):
         dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
         db2, dscale = gsum * s, dscale.view(scale.shape)
     dy = dy.view(-1, dy.shape[-1])
-    du = torch.mm(dy, w2b)
-    dw2 = weight_grad(w2, dy, u)
-    da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
-    del du
+    M, F = dy.shape[0], w2b.shape[1]
+    if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
+        # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
+        da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
+        dw2 = weight_grad(w2, dy, u)
+    else:
+        du = torch.mm(dy, w2b)
+        dw2 = weight_grad(w2, dy, u)
+        da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
+        del du
     dh = torch.mm(da, w1b).view(x.shape)
     dw1 = weight_grad(w1, da, h2)
     resid = resid.contiguous() if resid is not None else None

@@ -164,3 +164,26 @@ def test_qkv_rope_gemm_matches_unfused(cuda, attn_type):
     for a, b_ in [(q, q2), (k, k2), (v, v2)]:
         assert a.shape == b_.shape
         assert _rel(a, b_) < 1e-2
+
+
+@pytest.mark.parametrize("M,F,K", [(512, 1024, 256), (2560, 4096, 1024)])
+def test_ff_dgrad_geglu_epilogue(cuda, M, F, K):
+    """du = dy W2 with the GEGLU backward + FF-in bias grad in the GEMM epilogue == mm + geglu_bwd_bias,
+    and both against the fp32 reference."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(5)
+    C = hip_ops.C()
+    dy = (torch.randn(M, K, device=cuda) * 0.5).to(torch.bfloat16)
+    w2 = torch.randn(K, F, device=cuda) * 0.03  # Linear(F -> K).weight
+    h = torch.randn(M, 2 * F, device=cuda).to(torch.bfloat16)
+    dh, db = C.ff_dgrad_geglu(dy, w2.t().contiguous().to(torch.bfloat16), h)
+    du = torch.mm(dy, w2.to(torch.bfloat16))
+    dh_ref, db_ref = C.geglu_bwd_bias(h, du)
+    assert _rel(dh, dh_ref) < 1e-2 and _rel(db, db_ref) < 1e-2
+    # fp32 reference of the math
+    hf = h.float().requires_grad_(True)
+    out = hf[:, :F] * torch.nn.functional.gelu(hf[:, F:])
+    out.backward(dy.float() @ w2.to(torch.bfloat16).float())
+    assert _rel(dh, hf.grad) < 2e-2
+    assert _rel(db, hf.grad.sum(0)) < 2e-2
