@@ -14,9 +14,11 @@ void attn_bwd(const void*, const void*, const void*, const void*, const void*, c
               void*, const AttnGeom&, int, hipStream_t, const float*, const float*, void*, float);
 void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
 void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
-bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t);
+bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t,
+                  const void* = nullptr, const float* = nullptr, float* = nullptr);
 bool ln_shift_bwd(const float*, const float*, const void*, const float*, const float*, const float*, float*, float*,
-                  const GradSink&, const ShiftGeom&, int, int, hipStream_t);
+                  const GradSink&, const ShiftGeom&, int, int, hipStream_t, const void* = nullptr, const float* = nullptr,
+                  void* = nullptr, float* = nullptr, const GradSink* = nullptr);
 void geglu_fwd(const void*, void*, long, int, hipStream_t);
 void geglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 void geglu_bwd_bias(const void*, const void*, void*, float*, const GradSink&, long, int, hipStream_t);
@@ -100,6 +102,28 @@ std::vector<Tensor> ln_shift_fwd(Tensor x, Tensor w, Tensor b, int64_t T, int64_
                                 mean.data_ptr<float>(), rstd.data_ptr<float>(), g, B * n, D, (float)eps, cur_stream());
   TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
   return {y, mean, rstd};
+}
+
+// Sublayer boundary, forward: x = res + scale_prev * y_prev (returned) and LN(+shift)(x) in one pass.
+std::vector<Tensor> ln_shift_fwd_res(Tensor res, Tensor yprev, Tensor sprev, Tensor w, Tensor b, int64_t T, int64_t S, bool shift,
+                                     double eps) {
+  CHECK_IN(res, torch::kFloat32); CHECK_IN(yprev, torch::kBFloat16); CHECK_IN(sprev, torch::kFloat32);
+  CHECK_IN(w, torch::kFloat32); CHECK_IN(b, torch::kFloat32);
+  TORCH_CHECK(res.dim() == 3, "res must be (B, n, D)");
+  const int B = res.size(0), n = res.size(1), D = res.size(2);
+  TORCH_CHECK(yprev.numel() == res.numel() && sprev.numel() == D && w.numel() == D && b.numel() == D,
+              "ln_shift_fwd_res: shape mismatch");
+  if (shift) TORCH_CHECK(n >= T && n - T <= S * S && D % 4 == 0, "token shift geometry mismatch");
+  auto x = torch::empty_like(res);
+  auto y = torch::empty({B, n, D}, res.options().dtype(torch::kBFloat16));
+  auto mean = torch::empty({B * n}, res.options());
+  auto rstd = torch::empty({B * n}, res.options());
+  dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
+  bool ok = dalle::ln_shift_fwd(res.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(), mean.data_ptr<float>(),
+                                rstd.data_ptr<float>(), g, B * n, D, (float)eps, cur_stream(), yprev.data_ptr(),
+                                sprev.data_ptr<float>(), x.data_ptr<float>());
+  TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
+  return {x, y, mean, rstd};
 }
 
 // grad sink: an fp32 contiguous buffer of `n` floats that the kernel ACCUMULATES into (a .grad view
@@ -188,6 +212,35 @@ Tensor rope_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cosT, Tensor sinT, int64
   dalle::rope_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(),
                   g, B, (float)qscale, cur_stream());
   return dqkv;
+}
+
+// Sublayer boundary, backward: LN(+shift) backward of this sublayer (dx = resid + LN'(dy), dweight/dbias
+// into gw/gb) fused with the previous sublayer's LayerScale-residual backward (dy_prev = bf16(sprev * dx),
+// dscale_prev / dbias_prev into gsp / gbp). All four grad sinks are required (the flat-arena path).
+std::vector<Tensor> ln_shift_bwd_sr(Tensor x, Tensor w, Tensor dy, Tensor mean, Tensor rstd, int64_t T, int64_t S, bool shift,
+                                    Tensor resid, Tensor yprev, Tensor sprev, Tensor gw, Tensor gb, Tensor gsp, Tensor gbp) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(dy, torch::kBFloat16);
+  CHECK_IN(mean, torch::kFloat32); CHECK_IN(rstd, torch::kFloat32); CHECK_IN(resid, torch::kFloat32);
+  CHECK_IN(yprev, torch::kBFloat16); CHECK_IN(sprev, torch::kFloat32);
+  const int B = x.size(0), n = x.size(1), D = x.size(2);
+  TORCH_CHECK(dy.sizes() == x.sizes() && resid.sizes() == x.sizes() && yprev.numel() == x.numel() && sprev.numel() == D &&
+              mean.numel() == B * n && rstd.numel() == B * n, "ln_shift_bwd_sr: shape mismatch");
+  float* pw = sink_ptr(gw, D, "ln_shift_bwd_sr dweight");
+  float* pb = sink_ptr(gb, D, "ln_shift_bwd_sr dbias");
+  float* ps = sink_ptr(gsp, D, "ln_shift_bwd_sr dscale_prev");
+  float* pbp = sink_ptr(gbp, D, "ln_shift_bwd_sr dbias_prev");
+  auto dx = torch::empty_like(x);
+  auto dyp = torch::empty(x.sizes(), dy.options());
+  auto part = torch::empty({2, 512, 2 * D}, x.options());  // per-block partial rows [dw | db] and [g*y_prev | g]
+  const dalle::GradSink sink{pw, pb, nullptr, D, 1};
+  const dalle::GradSink sink2{ps, pbp, sprev.data_ptr<float>(), D, 1};  // dbias_prev = sprev * sum(g)
+  dalle::ShiftGeom g{n, (int)T, (int)S, shift ? 1 : 0};
+  bool ok = dalle::ln_shift_bwd(x.data_ptr<float>(), w.data_ptr<float>(), dy.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                resid.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), sink, g, B * n, D, cur_stream(),
+                                yprev.data_ptr(), sprev.data_ptr<float>(), dyp.data_ptr(), part.data_ptr<float>() + 512 * 2 * D,
+                                &sink2);
+  TORCH_CHECK(ok, "ln_shift: unsupported hidden size ", D);
+  return {dx, dyp};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -662,6 +715,8 @@ void psgd_reconstruct_(Tensor grad, Tensor E, Tensor P, Tensor Q) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dalle_amd HIP/CDNA4 kernels (gfx950)";
   m.def("ln_shift_fwd", &ln_shift_fwd);
+  m.def("ln_shift_fwd_res", &ln_shift_fwd_res);
+  m.def("ln_shift_bwd_sr", &ln_shift_bwd_sr);
   m.def("ln_shift_bwd", &ln_shift_bwd, py::arg("x"), py::arg("w"), py::arg("dy"), py::arg("mean"), py::arg("rstd"),
         py::arg("T"), py::arg("S"), py::arg("shift"), py::arg("resid") = py::none(), py::arg("gw") = py::none(),
         py::arg("gb") = py::none());

@@ -37,11 +37,15 @@ __device__ __forceinline__ int shift_src(const ShiftGeom& g, int p, int grp) {
   return (k % g.S) ? p - 1 : -1;
 }
 
-template <int D>
+// RES (sublayer boundary of the fused sequential stack): the row is first finished as
+// x = res + scale * y_prev (the previous sublayer's LayerScale residual, written to xout), then
+// normalised -- one pass over the residual stream instead of scale_residual + ln_shift_fwd.
+template <int D, bool RES = false>
 __global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ bias, __bf16* __restrict__ y,
                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                           ShiftGeom g, int rows, float eps) {
+                                                           ShiftGeom g, int rows, float eps, const __bf16* __restrict__ yprev,
+                                                           const float* __restrict__ sprev, float* __restrict__ xout) {
   constexpr int PER = D / 256;  // float4 per lane
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -54,6 +58,15 @@ __global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restri
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     v[j] = *reinterpret_cast<const f32x4*>(xr + 4 * (lane + 64 * j));
+    if (RES) {
+      const int c = 4 * (lane + 64 * j);
+      float yv[4];
+      unpack4(*reinterpret_cast<const s16x4*>(yprev + (size_t)row * D + c), yv);
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(sprev + c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[j][i] += sv[i] * yv[i];
+      *reinterpret_cast<f32x4*>(xout + (size_t)row * D + c) = v[j];
+    }
     s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
   }
   const float mean = wave_sum(s) * (1.0f / D);
@@ -83,17 +96,24 @@ __global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restri
   }
 }
 
-template <int D>
+// SR (sublayer boundary of the fused sequential stack): dx is also the upstream grad of the PREVIOUS
+// sublayer's LayerScale residual, so the same pass emits its dy_prev = bf16(scale_prev * dx) and the
+// column partials [sum dx * y_prev | sum dx] (-> dscale_prev, dbias_prev) into part2 -- no separate
+// scale_residual_bwd re-reading dx.
+template <int D, bool SR = false>
 __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const __bf16* __restrict__ dy, const float* __restrict__ mean_in,
                                                            const float* __restrict__ rstd_in, const float* __restrict__ resid,
                                                            float* __restrict__ dx, float* __restrict__ dw, ShiftGeom g,
-                                                           int rows) {
+                                                           int rows, const __bf16* __restrict__ yprev,
+                                                           const float* __restrict__ sprev, __bf16* __restrict__ dyprev,
+                                                           float* __restrict__ part2) {
   constexpr int PER = D / 256;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int wave0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   float dwa[PER][4] = {}, dba[PER][4] = {};
+  float sya[SR ? PER : 1][4] = {}, sga[SR ? PER : 1][4] = {};
   // software pipeline: the next row's x / shifted dy / residual-grad loads are in flight while this
   // row's two wave reductions run (the kernel is latency-bound at 2 waves per SIMD otherwise)
   auto fetch = [&](int row, f32x4 (&xv)[PER], f32x4 (&rv)[PER], s16x4 (&dv)[PER], float& mean, float& rstd) {
@@ -148,6 +168,18 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] += rstd * (gy[j][i] - s1 - xh[j][i] * s2);
       *reinterpret_cast<f32x4*>(dx + (size_t)row * D + c) = o;
+      if (SR) {
+        float yp[4], dp[4];
+        unpack4(*reinterpret_cast<const s16x4*>(yprev + (size_t)row * D + c), yp);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(sprev + c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dp[i] = o[i] * sv[i];
+          sya[SR ? j : 0][i] += o[i] * yp[i];
+          sga[SR ? j : 0][i] += o[i];
+        }
+        *reinterpret_cast<s16x4*>(dyprev + (size_t)row * D + c) = pack4(dp);
+      }
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) { xa[j] = xb[j]; ra[j] = rb[j]; da[j] = db[j]; }
@@ -170,6 +202,21 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * D; c += blockDim.x)
     dw[(size_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (SR) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = 4 * (lane + 64 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[wv][c + i] = sya[SR ? j : 0][i];
+        red[wv][D + c + i] = sga[SR ? j : 0][i];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += blockDim.x)
+      part2[(size_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
 }
 
 // sum `nrows` partial rows of width `width` (column-parallel, fixed order)
@@ -220,39 +267,54 @@ void column_sum(const float* part, int nrows, int width, float* out, hipStream_t
 
 template <int D>
 static void launch_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g,
-                       int rows, float eps, hipStream_t st) {
-  hipLaunchKernelGGL(ln_shift_fwd_kernel<D>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, (__bf16*)y, mean, rstd, g, rows, eps);
+                       int rows, float eps, hipStream_t st, const void* yprev, const float* sprev, float* xout) {
+  if (yprev)
+    hipLaunchKernelGGL((ln_shift_fwd_kernel<D, true>), dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, (__bf16*)y, mean, rstd, g,
+                       rows, eps, (const __bf16*)yprev, sprev, xout);
+  else
+    hipLaunchKernelGGL((ln_shift_fwd_kernel<D, false>), dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, (__bf16*)y, mean, rstd,
+                       g, rows, eps, (const __bf16*)nullptr, (const float*)nullptr, (float*)nullptr);
 }
 
 template <int D>
 static void launch_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, const float* resid,
-                       float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, hipStream_t st) {
-  // part is a (LN_BWD_BLOCKS x 2D) partial buffer; the sink receives [dw | db]
+                       float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, hipStream_t st,
+                       const void* yprev, const float* sprev, void* dyprev, float* part2, const GradSink* sink2) {
+  // part (and part2) are (LN_BWD_BLOCKS x 2D) partial buffers; the sink receives [dw | db], sink2 [dscale | dbias]_prev
   int blocks = (rows + 3) / 4;
   if (blocks > LN_BWD_BLOCKS) blocks = LN_BWD_BLOCKS;
-  hipLaunchKernelGGL(ln_shift_bwd_kernel<D>, dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid, dx, part,
-                     g, rows);
+  if (yprev) {
+    hipLaunchKernelGGL((ln_shift_bwd_kernel<D, true>), dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid,
+                       dx, part, g, rows, (const __bf16*)yprev, sprev, (__bf16*)dyprev, part2);
+    column_sum(part2, blocks, 2 * D, *sink2, st);
+  } else {
+    hipLaunchKernelGGL((ln_shift_bwd_kernel<D, false>), dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid,
+                       dx, part, g, rows, (const __bf16*)nullptr, (const float*)nullptr, (__bf16*)nullptr, (float*)nullptr);
+  }
   column_sum(part, blocks, 2 * D, sink, st);
 }
 
+// yprev / sprev / xout (all or none): the fused boundary x = res + sprev * yprev (see ln_shift_fwd_kernel RES)
 bool ln_shift_fwd(const float* x, const float* w, const float* b, void* y, float* mean, float* rstd, const ShiftGeom& g, int rows,
-                  int D, float eps, hipStream_t st) {
+                  int D, float eps, hipStream_t st, const void* yprev, const float* sprev, float* xout) {
   switch (D) {
-    case 256: launch_fwd<256>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
-    case 512: launch_fwd<512>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
-    case 1024: launch_fwd<1024>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
-    case 2048: launch_fwd<2048>(x, w, b, y, mean, rstd, g, rows, eps, st); return true;
+    case 256: launch_fwd<256>(x, w, b, y, mean, rstd, g, rows, eps, st, yprev, sprev, xout); return true;
+    case 512: launch_fwd<512>(x, w, b, y, mean, rstd, g, rows, eps, st, yprev, sprev, xout); return true;
+    case 1024: launch_fwd<1024>(x, w, b, y, mean, rstd, g, rows, eps, st, yprev, sprev, xout); return true;
+    case 2048: launch_fwd<2048>(x, w, b, y, mean, rstd, g, rows, eps, st, yprev, sprev, xout); return true;
     default: return false;
   }
 }
 
+// yprev / sprev / dyprev / part2 / sink2 (all or none): the fused boundary (see ln_shift_bwd_kernel SR)
 bool ln_shift_bwd(const float* x, const float* w, const void* dy, const float* mean, const float* rstd, const float* resid,
-                  float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, int D, hipStream_t st) {
+                  float* dx, float* part, const GradSink& sink, const ShiftGeom& g, int rows, int D, hipStream_t st,
+                  const void* yprev, const float* sprev, void* dyprev, float* part2, const GradSink* sink2) {
   switch (D) {
-    case 256: launch_bwd<256>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
-    case 512: launch_bwd<512>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
-    case 1024: launch_bwd<1024>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
-    case 2048: launch_bwd<2048>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st); return true;
+    case 256: launch_bwd<256>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st, yprev, sprev, dyprev, part2, sink2); return true;
+    case 512: launch_bwd<512>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st, yprev, sprev, dyprev, part2, sink2); return true;
+    case 1024: launch_bwd<1024>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st, yprev, sprev, dyprev, part2, sink2); return true;
+    case 2048: launch_bwd<2048>(x, w, dy, mean, rstd, resid, dx, part, sink, g, rows, st, yprev, sprev, dyprev, part2, sink2); return true;
     default: return false;
   }
 }

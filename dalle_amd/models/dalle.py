@@ -186,6 +186,20 @@ class Transformer(nn.Module):
                     lambda t, g=g: ops.scale_rows(self._ff_out(g, t), g.scale)) for f, g in pairs]
             return reversible_sequence(x, fns)
         cfg = self.cfg
+        if x.is_cuda:
+            subs = []
+            for f, g in pairs:
+                pre, attn = f.fn, f.fn.fn.fn
+                subs.append(("attn", ops.attn_meta(x, attn.to_qkv.weight, attn.heads, self.geom, attn.attn_type, pre.fn.enabled),
+                             (pre.norm.weight, pre.norm.bias, attn.to_qkv.weight, attn.to_out[0].weight, attn.to_out[0].bias,
+                              f.scale)))
+                gpre, ff = g.fn, g.fn.fn.fn
+                subs.append(("ff", ((cfg.text_len, cfg.image_fmap_size, bool(gpre.fn.enabled)),),
+                             (gpre.norm.weight, gpre.norm.bias, ff.net[0].weight, ff.net[0].bias, ff.net[3].weight,
+                              ff.net[3].bias, g.scale)))
+            out = ops.sequential_stack(x, subs)
+            if out is not None:
+                return out
         for f, g in pairs:
             pre, attn = f.fn, f.fn.fn.fn
             x = ops.attn_sublayer(x, pre.norm.weight, pre.norm.bias, attn.to_qkv.weight, attn.to_out[0].weight,

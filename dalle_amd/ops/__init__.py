@@ -116,6 +116,19 @@ def ff_sublayer(x, ln_w, ln_b, w1, b1, w2, b2, scale, text_len: int, image_size:
     return proj_residual(x, ff_hidden(h, w1, b1), w2, b2, scale)
 
 
+def attn_meta(x, w_qkv, heads: int, geom, attn_type: str, shift: bool):
+    """Per-sublayer constants of the fused attention core: (heads, cos, sin, meta)."""
+    return _hip().attn_args(x, w_qkv, heads, geom, attn_type, shift)
+
+
+def sequential_stack(x, subs):
+    """Non-reversible layer stack as one fused HIP autograd node (``hip_ops.sequential_stack``), or None
+    when it does not apply (CPU, no flat-arena grad buffers): the caller runs the sublayers one by one."""
+    if not (x.is_cuda and backend_for(x) == "hip" and torch.is_grad_enabled()):
+        return None
+    return _hip().sequential_stack(x, subs)
+
+
 def fused_reversible_available(x) -> bool:
     """True when the reversible stack can run on the fused HIP sublayers (``hip_ops.reversible_stack``)."""
     return x.is_cuda and backend_for(x) == "hip" and os.environ.get("DALLE_AMD_FUSED_REVERSIBLE", "1") != "0"

@@ -330,12 +330,14 @@ def _sinks(params, needs):
     return None
 
 
-def _attn_fwd(res, inp, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta, save: bool, sign: float = 1.0):
-    """res + sign * scale * to_out(attn(rope(to_qkv(LN_shift(inp))))); returns (out, saved-or-None)."""
+# Each sublayer = LN_shift (prologue) -> core (projections, attention / GEGLU) -> LayerScale residual
+# (epilogue). The cores are shared by the per-sublayer autograd nodes, the reversible stack and the
+# sequential stack, which fuses each epilogue with the NEXT sublayer's prologue (ln_shift_fwd_res /
+# ln_shift_bwd_sr).
+def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, meta, save: bool = True):
+    """to_out(attn(rope(to_qkv(h)))) + b_out (bf16, pre-LayerScale) and the saved tensors."""
     T, S, K, H, pattern, shift = meta
-    inp = inp.contiguous()
     B, n, d = inp.shape
-    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
     h2 = h.view(-1, d)
     wq = bf16_weight(w_qkv)
     col = pattern == PATTERN_IDS["axial_col"]
@@ -350,28 +352,16 @@ def _attn_fwd(res, inp, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta, 
     wo = bf16_weight(w_out)
     y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())
     s = scale.reshape(-1).contiguous()
-    xo = torch.empty_like(res)
-    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
     if not save:
-        return xo, None
-    return xo, (inp, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, (B, n, T, S, K, H, pattern, shift, col))
+        return y, s, None
+    return y, s, (inp, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, (B, n, T, S, K, H, pattern, shift, col))
 
 
-def _attn_bwd(saved, params, needs, g, resid):
-    """Backward of ``_attn_fwd`` for the branch upstream grad ``g`` (fp32): returns (d inp + resid,
-    dln_w, dln_b, dw_qkv, dw_out, db_out, dscale); the parameter grads are None when they went to the
-    arena sinks. ``resid`` (fp32, may be None) is added to d inp inside the LayerNorm-backward kernel."""
+def _attn_core_bwd(saved, params, dy):
+    """dy (bf16, grad of the pre-LayerScale output) -> dh (grad of the LN output) + (dw_qkv, dw_out)."""
     x, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, geo = saved
     ln_w, ln_b, w_qkv, w_out, b_out, scale = params
     B, n, T, S, K, H, pattern, shift, col = geo
-    g = g.contiguous()
-    sk = _sinks(params, needs)
-    if sk is not None:
-        dy, _, _ = C().scale_residual_bwd(g, y, s, sk[5], sk[4])
-        db = dscale = None
-    else:
-        dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
-        db, dscale = gsum * s, dscale.view(scale.shape)
     dy = dy.view(-1, dy.shape[-1])
     o2 = out.view(-1, out.shape[-1])
     do = torch.mm(dy, wo).view(out.shape)
@@ -386,20 +376,12 @@ def _attn_bwd(saved, params, needs, g, resid):
         del dq, dk, dv
     dh = torch.mm(dqkv, wq).view(x.shape)
     dwq = weight_grad(w_qkv, dqkv, h2)
-    resid = resid.contiguous() if resid is not None else None
-    if sk is not None:
-        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid, sk[0], sk[1])
-    else:
-        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid)
-    return dx, dlw, dlb, dwq, dwo, db, dscale
+    return dh, dwq, dwo
 
 
-def _ff_fwd(res, inp, ln_w, ln_b, w1, b1, w2, b2, scale, meta, save: bool, sign: float = 1.0):
-    """res + sign * scale * (W2 GEGLU(W1 LN_shift(inp) + b1) + b2); returns (out, saved-or-None)."""
-    T, S, shift = meta
-    inp = inp.contiguous()
+def _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save: bool = True):
+    """W2 GEGLU(W1 h + b1) + b2 (bf16, pre-LayerScale) and the saved tensors."""
     d = inp.shape[-1]
-    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
     h2 = h.view(-1, d)
     w1b, w2b = bf16_weight(w1), bf16_weight(w2)
     a = torch.addmm(bf16_weight(b1), h2, w1b.t())
@@ -408,26 +390,15 @@ def _ff_fwd(res, inp, ln_w, ln_b, w1, b1, w2, b2, scale, meta, save: bool, sign:
         del a
     y = torch.addmm(bf16_weight(b2), u, w2b.t())
     s = scale.reshape(-1).contiguous()
-    xo = torch.empty_like(res)
-    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
     if not save:
-        return xo, None
-    return xo, (inp, mean, rstd, h2, w1b, a, u, w2b, y, s, meta)
+        return y, s, None
+    return y, s, (inp, mean, rstd, h2, w1b, a, u, w2b, y, s, meta)
 
 
-def _ff_bwd(saved, params, needs, g, resid):
-    """Backward of ``_ff_fwd`` (same contract as ``_attn_bwd``)."""
+def _ff_core_bwd(saved, params, dy, sk):
+    """Same contract as ``_attn_core_bwd``; the FF-in bias grad goes to sink ``sk[3]`` when given."""
     x, mean, rstd, h2, w1b, a, u, w2b, y, s, meta = saved
     ln_w, ln_b, w1, b1, w2, b2, scale = params
-    T, S, shift = meta
-    g = g.contiguous()
-    sk = _sinks(params, needs)
-    if sk is not None:
-        dy, _, _ = C().scale_residual_bwd(g, y, s, sk[6], sk[5])
-        db2 = dscale = None
-    else:
-        dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
-        db2, dscale = gsum * s, dscale.view(scale.shape)
     dy = dy.view(-1, dy.shape[-1])
     M, F = dy.shape[0], w2b.shape[1]
     if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
@@ -441,11 +412,67 @@ def _ff_bwd(saved, params, needs, g, resid):
         del du
     dh = torch.mm(da, w1b).view(x.shape)
     dw1 = weight_grad(w1, da, h2)
+    return dh, dw1, db1, dw2
+
+
+def _attn_fwd(res, inp, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta, save: bool, sign: float = 1.0):
+    """res + sign * scale * to_out(attn(rope(to_qkv(LN_shift(inp))))); returns (out, saved-or-None)."""
+    T, S, K, H, pattern, shift = meta
+    inp = inp.contiguous()
+    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    y, s, saved = _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, meta, save)
+    xo = torch.empty_like(res)
+    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
+    return xo, saved
+
+
+def _residual_bwd(g, y, s, scale, sk, i_scale, i_bias):
+    """LayerScale-residual backward: dy = bf16(s * g); dscale / dbias to the sinks or returned."""
+    if sk is not None:
+        dy, _, _ = C().scale_residual_bwd(g, y, s, sk[i_scale], sk[i_bias])
+        return dy, None, None
+    dy, dscale, gsum = C().scale_residual_bwd(g, y, s)
+    return dy, gsum * s, dscale.view(scale.shape)
+
+
+def _ln_bwd(x, ln_w, dh, mean, rstd, meta_ln, resid, sk):
+    T, S, shift = meta_ln
     resid = resid.contiguous() if resid is not None else None
     if sk is not None:
-        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid, sk[0], sk[1])
-    else:
-        dx, dlw, dlb = C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid)
+        return C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid, sk[0], sk[1])
+    return C().ln_shift_bwd(x, ln_w.contiguous(), dh, mean, rstd, T, S, shift, resid)
+
+
+def _attn_bwd(saved, params, needs, g, resid):
+    """Backward of ``_attn_fwd`` for the branch upstream grad ``g`` (fp32): returns (d inp + resid,
+    dln_w, dln_b, dw_qkv, dw_out, db_out, dscale); the parameter grads are None when they went to the
+    arena sinks. ``resid`` (fp32, may be None) is added to d inp inside the LayerNorm-backward kernel."""
+    x, mean, rstd, geo = saved[0], saved[1], saved[2], saved[15]
+    sk = _sinks(params, needs)
+    dy, db, dscale = _residual_bwd(g.contiguous(), saved[10], saved[12], params[5], sk, 5, 4)
+    dh, dwq, dwo = _attn_core_bwd(saved, params, dy)
+    dx, dlw, dlb = _ln_bwd(x, params[0], dh, mean, rstd, (geo[2], geo[3], geo[7]), resid, sk)
+    return dx, dlw, dlb, dwq, dwo, db, dscale
+
+
+def _ff_fwd(res, inp, ln_w, ln_b, w1, b1, w2, b2, scale, meta, save: bool, sign: float = 1.0):
+    """res + sign * scale * (W2 GEGLU(W1 LN_shift(inp) + b1) + b2); returns (out, saved-or-None)."""
+    T, S, shift = meta
+    inp = inp.contiguous()
+    h, mean, rstd = C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    y, s, saved = _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save)
+    xo = torch.empty_like(res)
+    C().scale_residual_out(res.contiguous(), y, s if sign > 0 else -s, xo)
+    return xo, saved
+
+
+def _ff_bwd(saved, params, needs, g, resid):
+    """Backward of ``_ff_fwd`` (same contract as ``_attn_bwd``)."""
+    x, mean, rstd, meta = saved[0], saved[1], saved[2], saved[10]
+    sk = _sinks(params, needs)
+    dy, db2, dscale = _residual_bwd(g.contiguous(), saved[8], saved[9], params[6], sk, 6, 5)
+    dh, dw1, db1, dw2 = _ff_core_bwd(saved, params, dy, sk)
+    dx, dlw, dlb = _ln_bwd(x, params[0], dh, mean, rstd, meta, resid, sk)
     return dx, dlw, dlb, dw1, db1, dw2, db2, dscale
 
 
@@ -565,6 +592,109 @@ def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: i
                 seen.add(id(p))
                 uniq.append(p)
     return _ReversibleFused.apply(x, blocks, bool(recompute), *uniq)
+
+
+# ---------------------------------------------------------------------------------------------
+# Sequential (non-reversible) stack as ONE autograd node: every sublayer boundary runs as a single
+# kernel -- forward x_{i+1} = x_i + s_i * y_i fused with LN_shift_{i+1}(x_{i+1}) (ln_shift_fwd_res),
+# backward LN_shift_{i+1}' + residual fused with sublayer i's LayerScale backward (ln_shift_bwd_sr)
+# -- so the fp32 residual stream is read once per boundary in each direction instead of twice.
+# Parameter grads go straight to the flat-arena sinks (required; otherwise the per-sublayer nodes run).
+# ---------------------------------------------------------------------------------------------
+FUSED_SEQUENTIAL = int(os.environ.get("DALLE_AMD_FUSED_SEQUENTIAL", "1"))
+
+# per sublayer kind: (index of the LayerScale param, of the output-projection bias) in its param tuple
+_SCALE_BIAS = {"attn": (5, 4), "ff": (6, 5)}
+
+
+def _ln_meta(kind, args):
+    """(text_len, image_size, shift) of a sublayer's LN-shift prologue."""
+    m = args[-1]
+    return (m[0], m[1], m[5]) if kind == "attn" else m
+
+
+class _SequentialFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, subs, *params):
+        x = x.contiguous()
+        saved_all = []
+        kind, args, prm = subs[0]
+        T, S, shift = _ln_meta(kind, args)
+        h, mean, rstd = C().ln_shift_fwd(x, prm[0].contiguous(), prm[1].contiguous(), T, S, shift, 1e-5)
+        inp = x
+        for i, (kind, args, prm) in enumerate(subs):
+            if kind == "attn":
+                y, s, saved = _attn_core_fwd(inp, h, mean, rstd, *prm[2:], *args[-3:])
+            else:
+                y, s, saved = _ff_core_fwd(inp, h, mean, rstd, *prm[2:], args[-1])
+            saved_all.append(saved)
+            if i + 1 < len(subs):
+                nkind, nargs, nprm = subs[i + 1]
+                T, S, shift = _ln_meta(nkind, nargs)
+                inp, h, mean, rstd = C().ln_shift_fwd_res(inp, y, s, nprm[0].contiguous(), nprm[1].contiguous(), T, S, shift,
+                                                          1e-5)
+            else:
+                out = torch.empty_like(inp)
+                C().scale_residual_out(inp, y, s, out)
+        ctx.subs, ctx.saved_all, ctx.nparams = subs, saved_all, len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        subs, saved_all = ctx.subs, ctx.saved_all
+        ctx.saved_all = None
+        sinks = [[grad_sink(p) for p in prm] for _, _, prm in subs]
+        g = gout.float().contiguous()
+        with torch.no_grad():
+            kind, args, prm = subs[-1]
+            i_s, i_b = _SCALE_BIAS[kind]
+            sv = saved_all[-1]
+            y, s = (sv[10], sv[12]) if kind == "attn" else (sv[8], sv[9])
+            dy, _, _ = C().scale_residual_bwd(g, y, s, sinks[-1][i_s], sinks[-1][i_b])
+            for i in range(len(subs) - 1, -1, -1):
+                kind, args, prm = subs[i]
+                sv = saved_all[i]
+                saved_all[i] = None
+                sk = sinks[i]
+                if kind == "attn":
+                    dh, _, _ = _attn_core_bwd(sv, prm, dy)
+                else:
+                    dh, _, _, _ = _ff_core_bwd(sv, prm, dy, sk)
+                x, mean, rstd = sv[0], sv[1], sv[2]
+                T, S, shift = _ln_meta(kind, args)
+                if i > 0:
+                    pkind, _, _ = subs[i - 1]
+                    ps_, pb_ = _SCALE_BIAS[pkind]
+                    pv = saved_all[i - 1]
+                    yp, sp = (pv[10], pv[12]) if pkind == "attn" else (pv[8], pv[9])
+                    g, dy = C().ln_shift_bwd_sr(x, prm[0].contiguous(), dh, mean, rstd, T, S, shift, g, yp, sp, sk[0], sk[1],
+                                                sinks[i - 1][ps_], sinks[i - 1][pb_])
+                else:
+                    g, _, _ = C().ln_shift_bwd(x, prm[0].contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
+                del sv
+        return (g, None, *([None] * ctx.nparams))
+
+
+def attn_args(x, w_qkv, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):
+    dim_head = w_qkv.shape[0] // 3 // heads
+    assert dim_head == 64, "the HIP attention kernels are specialised for dim_head = 64"
+    cos, sin = _rope_tables(geom, dim_head, x.device)
+    return (heads, cos, sin, (geom.text_len, geom.image_size, geom.kernel_size, heads, PATTERN_IDS[attn_type], bool(shift)))
+
+
+def sequential_stack(x, subs):
+    """``subs``: per sublayer ("attn", (heads, cos, sin, meta), (ln_w, ln_b, w_qkv, w_out, b_out, scale)) or
+    ("ff", (meta,), (ln_w, ln_b, w1, b1, w2, b2, scale)). Returns None when some parameter has no fp32
+    arena grad buffer (the caller then runs the per-sublayer nodes)."""
+    uniq, seen = [], set()
+    for _, _, prm in subs:
+        for p in prm:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+    if not (FUSED_SEQUENTIAL and FUSE_WGRAD) or any(not p.requires_grad or grad_sink(p) is None for p in uniq):
+        return None
+    return _SequentialFused.apply(x, subs, *uniq)
 
 
 def attn_sublayer(x, ln_w, ln_b, w_qkv, w_out, b_out, scale, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):

@@ -18,11 +18,21 @@ COMMON = ["--model_preset", "tiny", "--text_seq_length", "64", "--authorize", "F
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port whose successor is free too (run_trainer's key-value store binds MASTER_PORT + 1)."""
+    for _ in range(50):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        s2 = socket.socket()
+        try:
+            s2.bind(("127.0.0.1", p + 1))
+            return p
+        except OSError:
+            continue
+        finally:
+            s2.close()
+    raise RuntimeError("no free port pair")
 
 
 def _run(tmp_path, nproc, extra, timeout=110):

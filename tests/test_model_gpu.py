@@ -117,3 +117,31 @@ def test_reversible_stored_activations_match_recompute(cuda):
     for n, g in grads[0].items():
         rel = ((g - grads[1][n]).norm() / (g.norm() + 1e-8)).item()
         assert rel < 2e-2, (n, rel)
+
+
+def test_sequential_fused_stack_matches_per_sublayer(cuda, monkeypatch):
+    """Non-reversible stack as one node with fused sublayer boundaries (ln_shift_fwd_res / ln_shift_bwd_sr)
+    == the per-sublayer autograd nodes, with every gradient landing in the flat arena."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = _cfg(False)
+    m = DALLE(cfg).to(cuda)
+    arena = FlatArena(m.parameters(), device=cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+    grads, losses = [], []
+    for fused in (1, 0):
+        monkeypatch.setattr(hip_ops, "FUSED_SEQUENTIAL", fused)
+        arena.zero_grad()
+        loss = m(text, img, return_loss=True)
+        loss.backward()
+        losses.append(loss.item())
+        grads.append(arena.grad.clone())
+    assert abs(losses[0] - losses[1]) <= 1e-5 * abs(losses[1])
+    rel = ((grads[0] - grads[1]).norm() / grads[1].norm()).item()
+    assert rel < 1e-3, rel
+    # per parameter too (shared blocks accumulate from several sublayers)
+    for p, o in zip(arena.params, arena.offsets):
+        a, b = grads[0][o:o + p.numel()], grads[1][o:o + p.numel()]
+        assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 1e-2

@@ -36,6 +36,16 @@ def test_serving_on_gpu(cuda):
         assert all(len(r["images"]) == 2 for r in res)
         assert gen.engines[8].graph is not None  # the decode step was captured
         again = gen.submit(["prompt 0"], images_per_prompt=8, temperature=0.0).result(timeout=100)
-        assert again["batch_padded"] == 8 and len(set(again["images"])) == 1  # greedy: one image 8 times
+        assert again["batch_padded"] == 8
+        # greedy: the same codes 8 times; the VQGAN decode of a batch may differ by ~1e-6 per image, so
+        # compare pixels with one 8-bit level of slack instead of the PNG bytes
+        import base64
+        import io
+
+        import numpy as np
+        from PIL import Image
+
+        px = [np.asarray(Image.open(io.BytesIO(base64.b64decode(b)))).astype(int) for b in again["images"]]
+        assert all(np.abs(a - px[0]).max() <= 1 for a in px)
     finally:
         gen.close()
