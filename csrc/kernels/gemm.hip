@@ -234,6 +234,19 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   __bf16* ep = smem + wave * (128 * 64);
+  // EPI 2: all 32 [value | gate] pre-activation loads of a lane (16 rows x 2 halves) are issued before
+  // any math instead of the 8 a partially unrolled loop keeps in flight (the epilogue does not overlap
+  // this workgroup's MFMA work, so its HBM latency is exposed once per tile)
+  s16x8 hv[2][8], hg[2][8];
+  const int gcol = col0 + wn * 64 + (lane & 7) * 8;
+  auto load_h = [&](int half) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const size_t r = (size_t)(row0 + wm * 128 + (half * 8 + k) * 8 + (lane >> 3));
+      hv[half][k] = *reinterpret_cast<const s16x8*>(rope.gh + r * 2 * rope.F + gcol);
+      hg[half][k] = *reinterpret_cast<const s16x8*>(rope.gh + r * 2 * rope.F + rope.F + gcol);
+    }
+  };
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = j * 16 + fr;
@@ -265,16 +278,18 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
     // (bf16) values -- the FF-in bias gradient -- reduced over the 8 lanes sharing it (fixed xor tree)
     // into one partial row per 128-row wave block.
     const int F = rope.F;
-    const int c = col0 + wn * 64 + (lane & 7) * 8;
+    const int c = gcol;
     float sv[8] = {}, sg[8] = {};
-#pragma unroll 4
+    load_h(0);
+    load_h(1);
+#pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int row = it * 8 + (lane >> 3), ch = lane & 7;
       const size_t r = (size_t)(row0 + wm * 128 + row);
       float d[8], a[8], gg[8], da[8], dg[8];
       unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), d);
-      unpack8(*reinterpret_cast<const s16x8*>(rope.gh + r * 2 * F + c), a);
-      unpack8(*reinterpret_cast<const s16x8*>(rope.gh + r * 2 * F + F + c), gg);
+      unpack8(hv[it >> 3][it & 7], a);
+      unpack8(hg[it >> 3][it & 7], gg);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float ge, gr;

@@ -130,6 +130,64 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
     return torch.mm(g2.t(), x2, out_dtype=torch.float32)
 
 
+class _WgradOverlap:
+    """Weight-gradient GEMMs on a side HIP stream. Inside the fused stack's backward the wgrads
+    (dW = g^T x, accumulated into the arena) depend on nothing the main stream produces afterwards, so
+    they run concurrently with the next dgrad GEMMs, the attention backward and the bandwidth-bound
+    LN / GEGLU kernels. Inputs are kept alive on the host and released only after the main stream
+    has been made to wait for the side-stream work that read them (a GPU-side event wait, ``LAG``
+    submissions later) -- ``record_stream`` instead would defer the caching allocator's reuse of these
+    GB-sized blocks and force fresh allocations. The order of the accumulations into a shared block's
+    grad is unchanged (one side stream), so results are bitwise the same.
+
+    Off by default (``DALLE_AMD_WGRAD_STREAM=1`` enables it): on the bench24 step the concurrent
+    GEMMs contend for the CUs and L2 and the step is ~2% SLOWER (257.3 / 258.1 vs 262.9 samples/s on
+    one box, profiles/r1_wgrad_side_stream.txt)."""
+
+    LAG = 4
+
+    def __init__(self):
+        self.enabled = os.environ.get("DALLE_AMD_WGRAD_STREAM", "0") == "1"
+        self._streams = {}
+        self.stream = None
+        self._pending = []
+
+    def begin(self, device: torch.device) -> bool:
+        if not (self.enabled and device.type == "cuda") or torch.cuda.is_current_stream_capturing():
+            return False
+        st = self._streams.get(device.index)
+        if st is None:
+            st = self._streams[device.index] = torch.cuda.Stream(device=device)
+        self.stream = st
+        return True
+
+    def end(self):
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.stream = None
+            self._pending.clear()
+
+    def __call__(self, w, g2, x2):
+        st = self.stream
+        if st is None:
+            return weight_grad(w, g2, x2)
+        main = torch.cuda.current_stream()
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            r = weight_grad(w, g2, x2)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        assert r is None, "side-stream weight grads must accumulate into the arena"
+        self._pending.append((ev, g2, x2))
+        while len(self._pending) > self.LAG:
+            old, _, _ = self._pending.pop(0)
+            main.wait_event(old)  # later main-stream reuse of those blocks is ordered after the read
+        return None
+
+
+_wgrad = _WgradOverlap()
+
+
 def grad_sink(p: torch.Tensor, needed: bool = True):
     """The fp32 ``.grad`` buffer (flattened view) a kernel may accumulate ``p``'s gradient into, or None
     (then the op returns the gradient to autograd as usual). Same contract as ``weight_grad``."""
@@ -365,7 +423,7 @@ def _attn_core_bwd(saved, params, dy):
     dy = dy.view(-1, dy.shape[-1])
     o2 = out.view(-1, out.shape[-1])
     do = torch.mm(dy, wo).view(out.shape)
-    dwo = weight_grad(w_out, dy, o2)
+    dwo = _wgrad(w_out, dy, o2)
     if FUSED_ROPE_BWD:  # rotary backward inside the attention-backward epilogues
         dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
         del do
@@ -375,7 +433,7 @@ def _attn_core_bwd(saved, params, dy):
         dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
         del dq, dk, dv
     dh = torch.mm(dqkv, wq).view(x.shape)
-    dwq = weight_grad(w_qkv, dqkv, h2)
+    dwq = _wgrad(w_qkv, dqkv, h2)
     return dh, dwq, dwo
 
 
@@ -404,14 +462,14 @@ def _ff_core_bwd(saved, params, dy, sk):
     if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
         da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
-        dw2 = weight_grad(w2, dy, u)
+        dw2 = _wgrad(w2, dy, u)
     else:
         du = torch.mm(dy, w2b)
-        dw2 = weight_grad(w2, dy, u)
+        dw2 = _wgrad(w2, dy, u)
         da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
         del du
     dh = torch.mm(da, w1b).view(x.shape)
-    dw1 = weight_grad(w1, da, h2)
+    dw1 = _wgrad(w1, da, h2)
     return dh, dw1, db1, dw2
 
 
@@ -645,6 +703,16 @@ class _SequentialFused(torch.autograd.Function):
         ctx.saved_all = None
         sinks = [[grad_sink(p) for p in prm] for _, _, prm in subs]
         g = gout.float().contiguous()
+        overlap = _wgrad.begin(g.device)
+        try:
+            g = _SequentialFused._backward(subs, saved_all, sinks, g)
+        finally:
+            if overlap:
+                _wgrad.end()
+        return (g, None, *([None] * ctx.nparams))
+
+    @staticmethod
+    def _backward(subs, saved_all, sinks, g):
         with torch.no_grad():
             kind, args, prm = subs[-1]
             i_s, i_b = _SCALE_BIAS[kind]
@@ -672,7 +740,7 @@ class _SequentialFused(torch.autograd.Function):
                 else:
                     g, _, _ = C().ln_shift_bwd(x, prm[0].contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
                 del sv
-        return (g, None, *([None] * ctx.nparams))
+        return g
 
 
 def attn_args(x, w_qkv, heads: int, geom: AttnGeometry, attn_type: str, shift: bool):

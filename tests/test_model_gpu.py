@@ -145,3 +145,22 @@ def test_sequential_fused_stack_matches_per_sublayer(cuda, monkeypatch):
     for p, o in zip(arena.params, arena.offsets):
         a, b = grads[0][o:o + p.numel()], grads[1][o:o + p.numel()]
         assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 1e-2
+
+
+def test_wgrad_side_stream_bitwise(cuda, monkeypatch):
+    """Weight grads on a side HIP stream (DALLE_AMD_WGRAD_STREAM=1) give bitwise the same arena grads."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = _cfg(False)
+    m = DALLE(cfg).to(cuda)
+    arena = FlatArena(m.parameters(), device=cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(hip_ops._wgrad, "enabled", on)
+        arena.zero_grad()
+        m(text, img, return_loss=True).backward()
+        grads.append(arena.grad.clone())
+    assert torch.equal(grads[0], grads[1])
