@@ -486,15 +486,44 @@ __global__ void attn_bwd_prep_kernel(const __bf16* __restrict__ dout, const __bf
 // ------------------------------------------------------------------------------------------------
 // Backward dQ (query-centric)
 // ------------------------------------------------------------------------------------------------
+// dS for one key tile of the wave's 32 queries -> dQ^T += K^T dS^T (S^T layout as in the forward).
+__device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* Ks, const __bf16* Vs, int tile,
+                                        const bf16x8 (&qf)[4], const bf16x8 (&dof)[4], float lq, float dl,
+                                        const AttnGeom& g, int qb, int qs, int lane) {
+  const int hl = lane >> 5, c32 = lane & 31;
+  f32x16 s = {}, dp = {};
+#pragma unroll
+  for (int ss = 0; ss < 4; ++ss) {
+    s = MFMA32(row_operand(Ks, ss, c32, hl), qf[ss], s);
+    dp = MFMA32(row_operand(Vs, ss, c32, hl), dof[ss], dp);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], LOG2E, -lq)) * (dp[r] - dl);
+  if (!tile_full(g, qb, tile)) {
+    const uint32_t mh = key_mask(g, qs, tile) >> (4 * hl);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = mask_bit(mh, r) ? s[r] : 0.f;
+  }
+  const bf16x8 d0 = cvt8(s, 0), d1 = cvt8(s, 8);
+  dq0 = MFMA32(tr_operand(Ks, 0, 0, lane), d0, dq0);
+  dq0 = MFMA32(tr_operand(Ks, 1, 0, lane), d1, dq0);
+  dq1 = MFMA32(tr_operand(Ks, 0, 1, lane), d0, dq1);
+  dq1 = MFMA32(tr_operand(Ks, 1, 1, lane), d1, dq1);
+}
+
+// dQ (query-centric). Workgroup = 4 waves = 4 consecutive 32-query blocks of one (b, h), same two
+// phases as the forward: (A) the text key tiles, staged cooperatively two per barrier step with the
+// next pair's loads in flight; (B) each image query block streams ITS OWN local key tiles through a
+// private LDS slot (no workgroup barrier, no wave idling on the other blocks' tiles).
 template <int MINB>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
                                                              __bf16* __restrict__ dQ, AttnGeom g, RopeOut ro) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TILE];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
   int grp, bh;
   xcd_remap(grp, bh);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int qb0 = grp * 4;
   const int qb = qb0 + wave;
@@ -502,18 +531,9 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   const bool active = qb < nqb;
   const size_t base = (size_t)bh * g.Np * 64;
 
-  const int u_text_end = qb_last < ntext ? qb_last + 1 : ntext;
-  const int first_img_qb = max(qb0, ntext);
-  const int u_loc_lo = (qb_last >= ntext) ? local_lo_tile(g, first_img_qb) : 0;
-  const int n_loc = (qb_last >= ntext) ? (qb_last - u_loc_lo + 1) : 0;
-  const int ntiles = u_text_end + n_loc;
-  int my_text_end = 0, my_lo = 1, my_hi = 0;
-  if (active) {
-    if (qb < ntext) my_text_end = qb + 1;
-    else { my_text_end = ntext; my_lo = local_lo_tile(g, qb); my_hi = qb; }
-  }
-
-  const int qs = qb * 32 + c32;
+  const int n_text = qb_last < ntext ? qb_last + 1 : ntext;  // text tiles of the workgroup union
+  const int my_text_end = active ? min(qb + 1, ntext) : 0;
+  const int qs = qb * 32 + (lane & 31);
   const int qrow = active ? qs : 0;
   bf16x8 qf[4], dof[4];
   {
@@ -524,59 +544,74 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   }
   const float lq = lse[(size_t)bh * g.Np + qrow];
   const float dl = delta[(size_t)bh * g.Np + qrow];
+  f32x16 dq0 = {}, dq1 = {};
 
+  // ---- phase A: shared text tiles, two per step ----
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
   const int st_off = lds_idx(st_row, st_col);
-  auto tile_id = [&](int t) { return t < u_text_end ? t : u_loc_lo + (t - u_text_end); };
-  s16x8 kreg, vreg;
-  {
-    const size_t off = base + (size_t)(tile_id(0) * 32 + st_row) * 64 + st_col;
-    kreg = *reinterpret_cast<const s16x8*>(Kt + off);
-    vreg = *reinterpret_cast<const s16x8*>(V + off);
-    *reinterpret_cast<s16x8*>(smem + st_off) = kreg;
-    *reinterpret_cast<s16x8*>(smem + TILE + st_off) = vreg;
-  }
+  const int npairs = (n_text + 1) >> 1;
+  s16x8 sreg[4];  // Ka, Kb, Va, Vb chunks of this thread
+  auto load_pair = [&](int pi) {
+    const int ta = 2 * pi, tb = min(2 * pi + 1, n_text - 1);
+    const size_t oa = base + (size_t)(ta * 32 + st_row) * 64 + st_col;
+    const size_t ob = base + (size_t)(tb * 32 + st_row) * 64 + st_col;
+    sreg[0] = *reinterpret_cast<const s16x8*>(Kt + oa);
+    sreg[1] = *reinterpret_cast<const s16x8*>(Kt + ob);
+    sreg[2] = *reinterpret_cast<const s16x8*>(V + oa);
+    sreg[3] = *reinterpret_cast<const s16x8*>(V + ob);
+  };
+  auto store_pair = [&](int buf) {
+    __bf16* S0 = smem + buf * (4 * TILE);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<s16x8*>(S0 + i * TILE + st_off) = sreg[i];
+  };
+  load_pair(0);
+  store_pair(0);
   __syncthreads();
-
-  f32x16 dq0 = {}, dq1 = {};
-  for (int t = 0; t < ntiles; ++t) {
-    const int tile = tile_id(t);
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      const size_t off = base + (size_t)(tile_id(t + 1) * 32 + st_row) * 64 + st_col;
-      kreg = *reinterpret_cast<const s16x8*>(Kt + off);
-      vreg = *reinterpret_cast<const s16x8*>(V + off);
-    }
-    const __bf16* Ks = smem + (t & 1) * (2 * TILE);
-    const __bf16* Vs = Ks + TILE;
-    const bool need = (tile < my_text_end) || (tile >= my_lo && tile <= my_hi);
-    if (need) {
-      f32x16 s = {}, dp = {};
-#pragma unroll
-      for (int ss = 0; ss < 4; ++ss) {
-        s = MFMA32(row_operand(Ks, ss, c32, hl), qf[ss], s);
-        dp = MFMA32(row_operand(Vs, ss, c32, hl), dof[ss], dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = fast_exp2(fmaf(s[r], LOG2E, -lq)) * (dp[r] - dl);
-      if (!tile_full(g, qb, tile)) {
-        const uint32_t mh = key_mask(g, qs, tile) >> (4 * hl);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = mask_bit(mh, r) ? s[r] : 0.f;
-      }
-      const bf16x8 d0 = cvt8(s, 0), d1 = cvt8(s, 8);
-      dq0 = MFMA32(tr_operand(Ks, 0, 0, lane), d0, dq0);
-      dq0 = MFMA32(tr_operand(Ks, 1, 0, lane), d1, dq0);
-      dq1 = MFMA32(tr_operand(Ks, 0, 1, lane), d0, dq1);
-      dq1 = MFMA32(tr_operand(Ks, 1, 1, lane), d1, dq1);
-    }
-    if (more) {
-      __bf16* Kn = smem + ((t + 1) & 1) * (2 * TILE);
-      *reinterpret_cast<s16x8*>(Kn + st_off) = kreg;
-      *reinterpret_cast<s16x8*>(Kn + TILE + st_off) = vreg;
-    }
+  for (int pi = 0; pi < npairs; ++pi) {
+    const bool more = pi + 1 < npairs;
+    if (more) load_pair(pi + 1);
+    const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
+    const int ta = 2 * pi, tb = 2 * pi + 1;
+    if (ta < my_text_end) dq_tile(dq0, dq1, S0, S0 + 2 * TILE, ta, qf, dof, lq, dl, g, qb, qs, lane);
+    if (tb < my_text_end) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
+    if (more) store_pair((pi + 1) & 1);
     __syncthreads();
   }
+
+  // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
+  if (active && qb >= ntext) {
+    __bf16* P = smem + wave * (2 * TILE);
+    const int lo = local_lo_tile(g, qb);
+    s16x8 kr[4], vr[4];
+    auto load_loc = [&](int t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+        const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
+        kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
+        vr[j] = *reinterpret_cast<const s16x8*>(V + off);
+      }
+    };
+    load_loc(lo);
+    for (int t = lo; t <= qb; ++t) {
+      // the previous tile's LDS reads were consumed by its MFMAs (in program order before these stores)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+        *reinterpret_cast<s16x8*>(P + lds_idx(row, col)) = kr[j];
+        *reinterpret_cast<s16x8*>(P + TILE + lds_idx(row, col)) = vr[j];
+      }
+      if (t < qb) load_loc(t + 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stores landed before any lane reads them
+      __builtin_amdgcn_wave_barrier();
+      dq_tile(dq0, dq1, P, P + TILE, t, qf, dof, lq, dl, g, qb, qs, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  // the epilogue's per-wave staging slot (4 KB at wave * 4 KB) overlaps other waves' phase-B slots
+  __syncthreads();
+
   if (!active) return;
   if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 4 KB
     float* stage = reinterpret_cast<float*>(smem) + wave * 1024;
