@@ -64,6 +64,8 @@ class HFTrainerArguments:
     grad_averaging: str = flag("size_adaptive", "engine only: none | fp16 | 8bit | size_adaptive | powersgd")
     powersgd_rank: int = flag(4, "engine only: rank of the PowerSGD factors")
     backend: Optional[str] = flag(None, "engine only: torch.distributed backend (nccl = RCCL on MI355X, gloo on CPU)")
+    offload_optimizer_to_host: bool = flag(False, "engine only: optimizer master copy + state in pinned host memory, "
+                                                   "stepped on the CPU (default: in HBM, fused HIP LAMB)")
 
     @property
     def device(self) -> torch.device:

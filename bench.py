@@ -2,19 +2,32 @@
 """Headline benchmark: training samples/s (whole node) of DALL-E d_model=1024, 24 layers,
 256 text + 32x32 image tokens, bf16 data-parallel on 1/2/4/8 MI355X (BASELINE.json config 2).
 
-One process per GPU (torchrun), RCCL over xGMI. Every timed step is a full training step:
-forward + backward (fused HIP kernels), gradient all-reduce across ranks (bucketed, RCCL),
-global grad-norm clip and a LAMB optimizer update on every parameter -- i.e. the collaborative
-optimizer with ``target_batch_size`` equal to the global batch, so each step is a global step.
+One process per GPU, RCCL over xGMI. ``python bench.py --gpus N`` either runs under a launcher that
+already set ``WORLD_SIZE`` (torchrun: the driver's multi-GPU form) or, when it did not and N > 1,
+starts the N worker processes itself (this script again, with torchrun's env contract) BEFORE any
+GPU call in the parent. Every worker asserts that the process group really has N ranks.
+
+Every timed step is a full training step: forward + backward (fused HIP kernels), gradient
+all-reduce across ranks (bucketed, RCCL), global grad-norm clip and a LAMB optimizer update on
+every parameter, i.e. a global step of the collaborative optimizer with ``target_batch_size`` equal
+to the global batch. ``--engine collab`` times the collaborative optimizer's own ``.step()``
+(``CollaborativeOptimizer``: accumulation, progress tracker, sample-weighted averaging, delayed
+8-bit LAMB) -- the loop ``run_trainer.py`` drives -- and also reports its tracker's
+``performance_ema`` (the reference's metric, ``callback.py:63``) summed over peers.
 
 Data: synthetic LAION-shaped pairs (256 caption ids padded with 1, 1024 VQGAN codes), random-init
-weights. ``python bench.py --gpus N --steps K --warmup W``; rank 0 prints ONE JSON line.
+weights. Rank 0 prints ONE JSON line.
+
+CPU rehearsal: ``BENCH_BACKEND=gloo python bench.py --gpus 2 --model tiny --batch 2`` runs the same
+path with gloo on CPU when no GPU is visible (tests/test_bench_cpu.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,28 +42,34 @@ from dalle_amd.models.dalle import DALLE  # noqa: E402
 from dalle_amd.optim import FlatArena, LAMB8bit  # noqa: E402
 from dalle_amd.parallel.dp import GradSync  # noqa: E402
 
+METRIC = "training samples/sec (whole node), DALL-E d_model=1024 at 1/2/4/8 MI355X"
 MODEL_NAMES = {
     "bench24": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
     "dalle-1024-24l": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
     "reference": "DALL-E d_model=1024, 64 layers (5 shared blocks), reversible, 256 text + 32x32 image tokens",
     "dalle-1.3b": "DALL-E ~1.3B, reversible, 256 text + 32x32 image tokens",
+    "tiny": "DALL-E tiny (2 layers, 64 text + 16x16 image tokens)",
 }
 BASELINE_VALUE = None  # the reference publishes no throughput numbers
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 48)), help="per-GPU micro-batch (48: best measured, 74 GB of 288)")
     ap.add_argument("--model", default="bench24")
-    ap.add_argument("--optim-bits", type=int, default=32, choices=[8, 32])
+    ap.add_argument("--engine", default="step", choices=["step", "collab"],
+                    help="step: model + GradSync + fused LAMB; collab: the CollaborativeOptimizer.step() loop")
+    ap.add_argument("--optim-bits", type=int, default=None, choices=[8, 32],
+                    help="LAMB moment storage (default: 32 for --engine step, 8 = the reference's CPULAMB8Bit for collab)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--compression", default="none", choices=["none", "powersgd", "uniform8bit"],
                     help="gradient averaging: plain bucketed all-reduce, PowerSGD rank-4 with error feedback "
                          "(BASELINE config 3) or the hivemind size-adaptive fp16 / uniform-8-bit butterfly")
     ap.add_argument("--powersgd-rank", type=int, default=4)
+    ap.add_argument("--no-delay", action="store_true", help="collab engine: synchronous optimizer step")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed run: K more steps with per-phase timing (+ torch.profiler trace)")
     ap.add_argument("--trace", default="", help="chrome trace path for the --profile-steps pass")
@@ -61,57 +80,154 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------------------------------------
+# launcher: N worker processes, started before the parent touches any GPU
+# ------------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_workers(n: int) -> int:
+    """Run this script as ``n`` ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* like torchrun) and return
+    the first non-zero exit code (the others are terminated), or 0. The parent never initialises
+    HIP: ``torch.cuda.device_count()`` only reads the device list on this stack."""
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+# ------------------------------------------------------------------------------------------------
+# one rank
+# ------------------------------------------------------------------------------------------------
+def _param_groups(model):
+    no_decay = ["bias", "LayerNorm.weight"]  # task.py:138-150 (only biases match dalle-pytorch names)
+    named = list(model.named_parameters())
+    return [
+        {"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": 0.045},
+        {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0},
+    ]
+
+
+def _lamb(groups, bits, arena=None):
+    return LAMB8bit(groups, lr=0.0025, betas=(0.9, 0.96), eps=1e-6, weight_decay=0.045, clamp_value=10000.0,
+                    max_grad_norm=4.0, reuse_grad_buffers=True, optim_bits=bits, arena=arena)
+
+
+def run_rank(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a 1-GPU box, with
-    # BENCH_BACKEND=gloo) share devices round-robin
-    dev_index = local_rank % max(1, torch.cuda.device_count())
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     backend = os.environ.get("BENCH_BACKEND", "nccl")
+    use_cuda = torch.cuda.is_available()
+    if backend == "nccl" and not use_cuda:
+        raise SystemExit("bench.py: no GPU visible (set BENCH_BACKEND=gloo for the CPU rehearsal)")
+    if use_cuda:
+        # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a 1-GPU box
+        # with BENCH_BACKEND=gloo) share devices round-robin
+        device = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(device)
+    else:
+        device = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, (os.cpu_count() or 2) // max(1, world))))
+
+    def sync():
+        if use_cuda:
+            torch.cuda.synchronize(device)
+
     if world > 1:
-        torch.cuda.set_device(dev_index)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+            dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
-    device = torch.device("cuda", dev_index)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
     torch.backends.cuda.matmul.allow_tf32 = False
-    from dalle_amd.utils.tuning import setup_gemm_tuning
-    tuning = setup_gemm_tuning(args.tunable if (args.tunable != "tune" or rank == 0) else "use")
+    tuning = "off"
+    if use_cuda:
+        from dalle_amd.utils.tuning import setup_gemm_tuning
+        tuning = setup_gemm_tuning(args.tunable if (args.tunable != "tune" or rank == 0) else "use")
 
     cfg = get_config(args.model)
     if args.no_recompute:
         cfg.reversible_recompute = False
+    bits = args.optim_bits if args.optim_bits is not None else (8 if args.engine == "collab" else 32)
     torch.manual_seed(1234)
     model = DALLE(cfg).to(device)
     arena = FlatArena(model.parameters(), device=device)
+    model.grad_arena = arena
     if world > 1:  # identical init on every rank
         dist.broadcast(arena.data, 0)
-    no_decay = ["bias", "LayerNorm.weight"]  # task.py:138-150 (only biases match dalle-pytorch names)
+    groups = _param_groups(model)
     named = list(model.named_parameters())
-    groups = [
-        {"params": [p for n, p in named if not any(nd in n for nd in no_decay)], "weight_decay": 0.045},
-        {"params": [p for n, p in named if any(nd in n for nd in no_decay)], "weight_decay": 0.0},
-    ]
-    opt = LAMB8bit(groups, lr=0.0025, betas=(0.9, 0.96), eps=1e-6, weight_decay=0.045, clamp_value=10000.0,
-                   max_grad_norm=4.0, reuse_grad_buffers=True, optim_bits=args.optim_bits, arena=arena)
-    sync = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype)
-    if args.compression == "powersgd":
-        # compression work runs at every world size (the all-reduces are skipped only when world == 1)
-        from dalle_amd.parallel.powersgd import PowerSGD
-        psgd = PowerSGD([p for _, p in named], rank=args.powersgd_rank, seed=0)
-        reduce_grads = psgd.allreduce_
-    elif args.compression == "uniform8bit":
-        from dalle_amd.parallel.averaging import allreduce_weighted
-        from dalle_amd.parallel.compression import reference_averaging_compression
-        comp = reference_averaging_compression()
+    pg = dist.group.WORLD if world > 1 else None
 
-        def reduce_grads():
-            allreduce_weighted(arena.grad, 1.0, compression=comp)  # a no-op on one GPU
+    if args.engine == "collab":
+        from dalle_amd.parallel.compression import reference_averaging_compression, NoCompression
+        from dalle_amd.parallel.optimizer import CollaborativeOptimizer
+        comp = reference_averaging_compression() if args.compression == "uniform8bit" else NoCompression()
+        copt = CollaborativeOptimizer(
+            dht=None, run_id="bench", params=groups, optimizer=lambda g: _lamb(g, bits),
+            target_batch_size=args.batch * world, batch_size_per_step=args.batch,
+            offload_optimizer=True, delay_optimizer_step=not args.no_delay, reuse_grad_buffers=True,
+            grad_compression=comp, state_averaging_compression=comp, process_group=pg, arena=arena,
+            powersgd_rank=args.powersgd_rank if args.compression == "powersgd" else None,
+            tracker_mode="static", device=device)
+
+        def opt_step():
+            copt.step()
+        zero = None  # the collaborative optimizer resets the accumulated grads after each global step
     else:
-        reduce_grads = sync.all_reduce
+        opt = _lamb(groups, bits, arena=arena)
+        sync_grads = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype)
+        if args.compression == "powersgd":
+            # compression work runs at every world size (the all-reduces are skipped only when world == 1)
+            from dalle_amd.parallel.powersgd import PowerSGD
+            psgd = PowerSGD([p for _, p in named], rank=args.powersgd_rank, seed=0)
+            reduce_grads = psgd.allreduce_
+        elif args.compression == "uniform8bit":
+            from dalle_amd.parallel.averaging import allreduce_weighted
+            from dalle_amd.parallel.compression import reference_averaging_compression
+            comp = reference_averaging_compression()
+
+            def reduce_grads():
+                allreduce_weighted(arena.grad, 1.0, compression=comp, segments=arena.segments())  # no-op on one GPU
+        else:
+            reduce_grads = sync_grads.all_reduce
+
+        def opt_step():
+            reduce_grads()
+            opt.step()
+        zero = arena.zero_grad
 
     gen = torch.Generator().manual_seed(1000 + rank)
     batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
@@ -122,36 +238,49 @@ def main():
     def step(i, timer=None):
         phase = timer if timer is not None else (lambda name: prof_range(name))
         b = batches[i % len(batches)]
-        arena.zero_grad()
+        if zero is not None:
+            zero()
         with phase("forward"):
             loss = model(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
         with phase("backward"):
             loss.backward()
-        with phase("grad_allreduce"):
-            reduce_grads()
-        with phase("optimizer"):
-            opt.step()
+        with phase("grad_averaging+optimizer"):
+            opt_step()
         return loss
 
     for i in range(args.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=device)
+    if args.engine == "collab":
+        copt.apply_pending()
+    per_rank = [elapsed]
+    names = [torch.cuda.get_device_name(device) if use_cuda else "cpu"]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        per_rank = [None] * world
+        names_all = [None] * world
+        dist.all_gather_object(per_rank, elapsed)
+        dist.all_gather_object(names_all, names[0])
+        names = names_all
+    elapsed = max(per_rank)
     final_loss = float(loss.item())
+    ema = None
+    if args.engine == "collab":
+        sps = [copt.tracker.performance_ema.samples_per_second]
+        if world > 1:
+            sps = [None] * world
+            dist.all_gather_object(sps, copt.tracker.performance_ema.samples_per_second)
+        ema = sum(sps)
 
     samples = args.batch * world * args.steps
     value = samples / elapsed
@@ -159,8 +288,12 @@ def main():
     if rank == 0:
         tflops = cfg.train_flops_per_sample() * value / world / 1e12  # model FLOPs (no recompute)
         hw_tflops = cfg.train_flops_per_sample(include_recompute=True) * value / world / 1e12
-        print(json.dumps({
-            "metric": "training samples/sec (whole node), DALL-E d_model=1024 at 1/2/4/8 MI355X",
+        n_attn = len(set(map(str, cfg.shared_attn_ids)))
+        n_ff = len(set(map(str, cfg.shared_ff_ids)))
+        sharing = (f"{n_attn} unique attn / {n_ff} unique ff blocks over {cfg.depth} layers"
+                   if (n_attn < cfg.depth or n_ff < cfg.depth) else "none")
+        out = {
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
@@ -170,21 +303,35 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
-            "dtype": "bf16",
+            "dtype": "bf16" if use_cuda else "fp32",
             "data": "synthetic LAION-shaped pairs (256 caption ids + 32x32 VQGAN codes), random-init weights",
             "config": {"model": MODEL_NAMES.get(args.model, args.model),
                        "preset": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": cfg.seq_len, "parallelism": f"dp{world}",
-                       "optimizer": f"LAMB ({args.optim_bits}-bit moments) + global clip 4.0",
+                       "weight_sharing": sharing,
+                       "unique_params": cfg.unique_param_count(),
+                       "engine": "CollaborativeOptimizer.step" if args.engine == "collab" else "GradSync + fused LAMB",
+                       "optimizer": f"LAMB ({bits}-bit moments) + global clip 4.0",
                        "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning,
                        "reversible": ("recompute" if cfg.reversible_recompute else "stored activations") if cfg.reversible else "no",
                        "grad_compression": args.compression if args.compression != "powersgd"
                        else f"powersgd-rank{args.powersgd_rank}"},
+            "rccl_world": world if backend == "nccl" else None,
+            "backend": backend if world > 1 else "none",
+            "devices": names,
+            "per_rank_ms_per_step": [round(t / args.steps * 1000, 3) for t in per_rank],
             "model_tflops_per_gpu": round(tflops, 1),
             "hw_tflops_per_gpu": round(hw_tflops, 1),
-            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1),
+            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1) if use_cuda else None,
             "loss": round(final_loss, 4),
-        }), flush=True)
+        }
+        if ema is not None:
+            out["collab_performance_ema_samples_per_s"] = round(ema, 3)
+        if os.environ.get("BENCH_DUMP_PARAMS"):
+            out["param_checksum"] = float(arena.data.double().sum())
+        print(json.dumps(out), flush=True)
+    if os.environ.get("BENCH_DUMP_PARAMS"):
+        torch.save(arena.data.detach().cpu(), f"{os.environ['BENCH_DUMP_PARAMS']}.rank{rank}.pt")
     if args.profile_steps:
         # untimed diagnostic pass: per-phase wall times (synchronised) and an optional trace
         timer = StepTimer()
@@ -205,5 +352,15 @@ def main():
         dist.destroy_process_group()
 
 
+def main() -> int:
+    args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_workers(args.gpus)
+    run_rank(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

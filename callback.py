@@ -29,19 +29,29 @@ from task import TrainingTask
 from utils import LocalMetrics, logger
 
 
+def rank_state_path(path: str) -> str:
+    """``state.zip`` for a single peer; ``state.rank{r}.zip`` for rank r of a multi-process job."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        root, ext = os.path.splitext(path)
+        return f"{root}.rank{dist.get_rank()}{ext}"
+    return path
+
+
 @dataclass
 class _EpochStats:
-    loss_sum: float = 0.0
+    loss_sum: object = 0.0  # a device scalar while the epoch runs: read once, when the epoch closes
     mini_steps: int = 0
     samples: int = 0  # samples this peer contributed to the epoch being accumulated
     contributed_total: int = 0
     reported_epoch: int = -1
 
-    def add(self, loss: float):
-        self.loss_sum += float(loss)
+    def add(self, loss):
+        t = getattr(loss, "tensor", loss)  # DeferredScalar -> its tensor (no host sync per micro-step)
+        self.loss_sum = self.loss_sum + (t if torch.is_tensor(t) else float(t))
         self.mini_steps += 1
 
     def close_epoch(self, epoch: int, samples_per_second: float) -> LocalMetrics:
+        self.loss_sum = float(self.loss_sum)
         record = LocalMetrics(step=int(epoch), samples_per_second=float(samples_per_second),
                               samples_accumulated=int(self.samples), loss=float(self.loss_sum), mini_steps=int(self.mini_steps))
         self.contributed_total += self.samples
@@ -89,8 +99,9 @@ class CollaborativeCallback(TrainerCallback):
         self.dht, self.collaborative_optimizer = task.dht, task.collaborative_optimizer
         self.statistics_expiration = args.statistics_expiration
         self.backup_every_steps = args.backup_every_steps
-        self.state_path = args.state_path
+        self.state_path = rank_state_path(args.state_path)
         self.stats = _EpochStats()
+        self._checked_version = None
         self.snapshots = _SnapshotServer(task, os.path.join(task.trainer_args.output_dir, "shared_state"))
 
     # -- trainer hooks ------------------------------------------------------------------------
@@ -105,13 +116,17 @@ class CollaborativeCallback(TrainerCallback):
 
     def on_step_end(self, args, state, control, **kwargs):
         control.should_log = True
-        if not self.params_are_finite():
+        opt = self.collaborative_optimizer
+        # parameters change only at global steps (a delayed update lands one local step later): check them
+        # then, not after every micro-step -- the check is a device->host read
+        version = (opt.local_epoch, opt.state_averager.pending)
+        if version != self._checked_version and not self.params_are_finite():
             if not os.path.exists(self.state_path):
                 raise RuntimeError("Parameters became NaN/Inf and there is no backup to roll back to")
             logger.warning("Parameters became NaN/Inf: rolling back to the last backup")
             self.restore_from_backup(self.state_path)
             return control
-        opt = self.collaborative_optimizer
+        self._checked_version = version
         if state.log_history:
             self.stats.add(state.log_history[-1]["loss"])
             if opt.local_epoch != self.stats.reported_epoch:
@@ -148,7 +163,10 @@ class CollaborativeCallback(TrainerCallback):
         logger.info(f"Writing backup of epoch {opt.local_epoch} to {self.state_path}")
         snapshot = {"model": self.task.model.state_dict(), "training": opt.state_dict(),
                     "scheduler": opt.state_averager.scheduler.state_dict(), "local_epoch": opt.local_epoch}
-        torch.save(snapshot, self.state_path)
+        # every peer owns its file (ranks of one node must not write the same path) and a reader never
+        # sees a torn file: write a temporary, then rename it into place
+        torch.save(snapshot, self.state_path + ".tmp")
+        os.replace(self.state_path + ".tmp", self.state_path)
 
     @torch.no_grad()
     def restore_from_backup(self, path, check_step: bool = False):

@@ -25,10 +25,13 @@ void geglu_bwd_bias(const void*, const void*, void*, float*, const GradSink&, lo
 void scale_residual(const float*, const void*, const float*, float*, long, int, hipStream_t);
 void scale_residual_bwd(const float*, const void*, const float*, void*, float*, const GradSink&, long, int, hipStream_t);
 void nonfinite(const float*, long, int*, hipStream_t);
+void zero_if_flag(float*, long, const int*, hipStream_t);
 bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
 void uq8_compress(const float*, long, uint8_t*, float*, void*, hipStream_t);
 size_t uq8_workspace_bytes();
 void uq8_dequant(const uint8_t*, const float*, float*, long, float, int, hipStream_t);
+void uq8_seg_compress(const float*, const long*, const long*, const int*, int, uint8_t*, float*, hipStream_t);
+void uq8_seg_dequant(const uint8_t*, const long*, const float*, const long*, const int*, int, float*, float, int, hipStream_t);
 bool skinny_gemm(int, SkinnyArgs, hipStream_t);
 int skinny_ks(int, int, int, int);
 void skinny_force_config(int, int, int, int);
@@ -49,9 +52,9 @@ bool sample_step(const SampleArgs&, hipStream_t);
 bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
-void lamb_step(const float*, float*, const float*, float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*,
-               const float*, const int*, const long*, const long*, const int*, const float*, const float*, const float*,
-               float*, float*, float*, float*, int, long, float, float, float, float, int, hipStream_t);
+void lamb_step(float*, const float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*, const float*,
+               const int*, const int*, const long*, const long*, const int*, const float*, const float*, const float*, float*,
+               float*, float*, float*, int, long, float, float, float, float, int, hipStream_t);
 }  // namespace dalle
 
 using torch::Tensor;
@@ -548,6 +551,41 @@ void uq8_dequant_(Tensor q, Tensor codebook, Tensor out, double weight, bool acc
                      accumulate ? 1 : 0, cur_stream());
 }
 
+// Segmented uniform 8-bit (one codebook per part, one launch for all parts). The part tables are
+// device tensors built once per averaging plan; their extents were checked on the host when the
+// plan was built (x_end = max(x_off + len), q_end = max(q_off + len)) and are re-checked here
+// against the buffers, so no part can read or write outside them.
+void uq8_seg_compress(Tensor x, Tensor x_off, Tensor q_off, Tensor len, Tensor q, Tensor codebook, int64_t x_end,
+                      int64_t q_end) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(x_off, torch::kInt64); CHECK_IN(q_off, torch::kInt64);
+  CHECK_IN(len, torch::kInt32); CHECK_IN(q, torch::kUInt8); CHECK_IN(codebook, torch::kFloat32);
+  const long nseg = len.numel();
+  TORCH_CHECK(x_off.numel() == nseg && q_off.numel() == nseg && codebook.numel() == nseg * 256, "uq8_seg_compress: table sizes");
+  TORCH_CHECK(x_end <= x.numel() && q_end <= q.numel(), "uq8_seg_compress: parts exceed the buffers");
+  dalle::uq8_seg_compress(x.data_ptr<float>(), x_off.data_ptr<int64_t>(), q_off.data_ptr<int64_t>(), len.data_ptr<int>(),
+                          (int)nseg, q.data_ptr<uint8_t>(), codebook.data_ptr<float>(), cur_stream());
+}
+
+void uq8_seg_dequant_(Tensor q, Tensor q_off, Tensor codebook, Tensor out_off, Tensor len, Tensor out, double weight,
+                      bool accumulate, int64_t q_end, int64_t out_end) {
+  CHECK_IN(q, torch::kUInt8); CHECK_IN(q_off, torch::kInt64); CHECK_IN(codebook, torch::kFloat32);
+  CHECK_IN(out_off, torch::kInt64); CHECK_IN(len, torch::kInt32); CHECK_IN(out, torch::kFloat32);
+  const long nseg = len.numel();
+  TORCH_CHECK(q_off.numel() == nseg && out_off.numel() == nseg && codebook.numel() == nseg * 256, "uq8_seg_dequant: table sizes");
+  TORCH_CHECK(q_end <= q.numel() && out_end <= out.numel(), "uq8_seg_dequant: parts exceed the buffers");
+  dalle::uq8_seg_dequant(q.data_ptr<uint8_t>(), q_off.data_ptr<int64_t>(), codebook.data_ptr<float>(), out_off.data_ptr<int64_t>(),
+                         len.data_ptr<int>(), (int)nseg, out.data_ptr<float>(), (float)weight, accumulate ? 1 : 0, cur_stream());
+}
+
+// Zero x if it holds a NaN/Inf; returns the device flag (no host sync).
+Tensor zero_if_nonfinite_(Tensor x) {
+  CHECK_IN(x, torch::kFloat32);
+  auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
+  dalle::nonfinite(x.data_ptr<float>(), x.numel(), flag.data_ptr<int>(), cur_stream());
+  dalle::zero_if_flag(x.data_ptr<float>(), x.numel(), flag.data_ptr<int>(), cur_stream());
+  return flag;
+}
+
 Tensor nonfinite(Tensor x) {
   CHECK_IN(x, torch::kFloat32);
   auto flag = torch::zeros({1}, x.options().dtype(torch::kInt32));
@@ -659,23 +697,34 @@ void lamb_grad_norm(Tensor g, Tensor partial, double max_norm, Tensor coef, Tens
                         norm.data_ptr<float>(), cur_stream());
 }
 
-void lamb_step(Tensor p, Tensor g, Tensor delta, Tensor q1, Tensor q2, Tensor absmax1, Tensor absmax2, Tensor m32, Tensor v32,
-               Tensor code1, Tensor code2, Tensor block_tensor, Tensor tstart, Tensor tsize, Tensor tmode, Tensor twd, Tensor tlr,
-               Tensor coef, Tensor partial, Tensor trust, Tensor wnorm, Tensor snorm, double beta1, double beta2, double eps,
-               double clamp_value, bool use_clip) {
-  CHECK_IN(p, torch::kFloat32); CHECK_IN(g, torch::kFloat32); CHECK_IN(delta, torch::kFloat32);
+// bslot[blk]: the block's slot in its mode's compact state array (8-bit: q1/q2 rows of 4096 +
+// absmax; fp32: m32/v32 rows). The table is built and range-checked on the host by the engine
+// (dalle_amd/optim/fused.py); here the array sizes are checked against the slot counts it reports.
+void lamb_step(Tensor p, Tensor g, Tensor q1, Tensor q2, Tensor absmax1, Tensor absmax2, Tensor m32, Tensor v32,
+               Tensor code1, Tensor code2, Tensor block_tensor, Tensor bslot, Tensor tstart, Tensor tsize, Tensor tmode,
+               Tensor twd, Tensor tlr, Tensor coef, Tensor partial, Tensor trust, Tensor wnorm, Tensor snorm, int64_t n8_blocks,
+               int64_t n32_blocks, double beta1, double beta2, double eps, double clamp_value, bool use_clip) {
+  CHECK_IN(p, torch::kFloat32); CHECK_IN(g, torch::kFloat32);
   CHECK_IN(q1, torch::kUInt8); CHECK_IN(q2, torch::kUInt8);
-  CHECK_IN(block_tensor, torch::kInt32); CHECK_IN(tstart, torch::kInt64); CHECK_IN(tsize, torch::kInt64);
+  CHECK_IN(absmax1, torch::kFloat32); CHECK_IN(absmax2, torch::kFloat32);
+  CHECK_IN(m32, torch::kFloat32); CHECK_IN(v32, torch::kFloat32);
+  CHECK_IN(block_tensor, torch::kInt32); CHECK_IN(bslot, torch::kInt32);
+  CHECK_IN(tstart, torch::kInt64); CHECK_IN(tsize, torch::kInt64);
   const long n = p.numel();
-  TORCH_CHECK(n % 4096 == 0 && g.numel() == n && delta.numel() == n && q1.numel() == n && q2.numel() == n);
-  TORCH_CHECK(m32.numel() == n && v32.numel() == n && absmax1.numel() == n / 4096 && absmax2.numel() == n / 4096);
-  TORCH_CHECK(block_tensor.numel() == n / 4096 && partial.numel() >= 2 * (n / 4096));
+  const long nb = n / 4096;
+  TORCH_CHECK(n % 4096 == 0 && g.numel() == n, "lamb_step: arena sizes");
+  TORCH_CHECK(q1.numel() == n8_blocks * 4096 && q2.numel() == n8_blocks * 4096 && absmax1.numel() == n8_blocks &&
+                  absmax2.numel() == n8_blocks, "lamb_step: 8-bit state sizes");
+  TORCH_CHECK(m32.numel() == n32_blocks * 4096 && v32.numel() == n32_blocks * 4096, "lamb_step: fp32 state sizes");
+  TORCH_CHECK(n8_blocks + n32_blocks == nb, "lamb_step: every block needs exactly one state slot");
+  TORCH_CHECK(block_tensor.numel() == nb && bslot.numel() == nb && partial.numel() >= 2 * nb);
   TORCH_CHECK(code1.numel() == 256 && code2.numel() == 256);
   const int nt = tstart.numel();
   TORCH_CHECK(tsize.numel() == nt && tmode.numel() == nt && twd.numel() == nt && tlr.numel() == nt && trust.numel() == nt);
-  dalle::lamb_step(p.data_ptr<float>(), p.data_ptr<float>(), g.data_ptr<float>(), delta.data_ptr<float>(), q1.data_ptr<uint8_t>(),
-                   q2.data_ptr<uint8_t>(), absmax1.data_ptr<float>(), absmax2.data_ptr<float>(), m32.data_ptr<float>(),
-                   v32.data_ptr<float>(), code1.data_ptr<float>(), code2.data_ptr<float>(), block_tensor.data_ptr<int>(),
+  // 1-element placeholders keep the pointers valid when one mode has no tensors
+  dalle::lamb_step(p.data_ptr<float>(), g.data_ptr<float>(), q1.data_ptr<uint8_t>(), q2.data_ptr<uint8_t>(),
+                   absmax1.data_ptr<float>(), absmax2.data_ptr<float>(), m32.data_ptr<float>(), v32.data_ptr<float>(),
+                   code1.data_ptr<float>(), code2.data_ptr<float>(), block_tensor.data_ptr<int>(), bslot.data_ptr<int>(),
                    (const long*)tstart.data_ptr<int64_t>(), (const long*)tsize.data_ptr<int64_t>(), tmode.data_ptr<int>(),
                    twd.data_ptr<float>(), tlr.data_ptr<float>(), coef.data_ptr<float>(), partial.data_ptr<float>(),
                    trust.data_ptr<float>(), wnorm.data_ptr<float>(), snorm.data_ptr<float>(), nt, n, (float)beta1, (float)beta2,
@@ -740,6 +789,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("qkv_rope", &qkv_rope);
   m.def("uq8_compress", &uq8_compress);
   m.def("uq8_dequant_", &uq8_dequant_);
+  m.def("uq8_seg_compress", &uq8_seg_compress);
+  m.def("zero_if_nonfinite_", &zero_if_nonfinite_);
+  m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);

@@ -214,6 +214,17 @@ __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __res
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// x[:] = 0 if flag != 0 (the flag written by nonfinite_kernel earlier on the same stream): the
+// trainer's "zero the accumulated grads only if they are not finite" without a host round trip
+__global__ void zero_if_flag_kernel(float* __restrict__ x, long n, const int* __restrict__ flag) {
+  if (flag[0] == 0) return;
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long stride = (long)gridDim.x * blockDim.x * 4;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  for (; i + 3 < n; i += stride) *reinterpret_cast<f32x4*>(x + i) = z;
+  for (; i < n; ++i) x[i] = 0.f;
+}
+
 void geglu_fwd(const void* h, void* out, long M, int F, hipStream_t st) {
   const long t = M * (F / 8);
   hipLaunchKernelGGL(geglu_fwd_kernel, dim3((t + 255) / 256), dim3(256), 0, st, (const __bf16*)h, (__bf16*)out, M, F);
@@ -251,6 +262,13 @@ void nonfinite(const float* x, long n, int* flag, hipStream_t st) {
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(nonfinite_kernel, dim3(blocks), dim3(256), 0, st, x, n, flag);
+}
+
+void zero_if_flag(float* x, long n, const int* flag, hipStream_t st) {
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(zero_if_flag_kernel, dim3(blocks), dim3(256), 0, st, x, n, flag);
 }
 
 }  // namespace dalle

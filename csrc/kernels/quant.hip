@@ -138,6 +138,110 @@ __global__ void uq8_dequant_kernel(const uint8_t* __restrict__ q, const float* _
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Segmented form (the butterfly's per-tensor parts, hivemind compresses every part of every tensor
+// separately): ONE launch quantises all parts, one workgroup per part. A part is at most a few
+// hundred KB, so its three passes (sum/max, variance, quantise + histogram) re-read it from L2;
+// the codebook is written by the same workgroup. Same fixed-point bin sums as above, so the result
+// is deterministic and identical on every peer.
+//   part s: x[x_off[s] : x_off[s] + len[s]]  ->  q[q_off[s] : q_off[s] + len[s]], codebook[256 s : 256 s + 256]
+__global__ __launch_bounds__(Q_THREADS) void uq8_seg_compress_kernel(const float* __restrict__ x, const long* __restrict__ x_off,
+                                                                     const long* __restrict__ q_off, const int* __restrict__ len,
+                                                                     uint8_t* __restrict__ q, float* __restrict__ codebook) {
+  __shared__ double red[Q_THREADS / 64];
+  __shared__ float redm[Q_THREADS / 64];
+  __shared__ double bc[3];  // mean, 1/scale, 2^shift
+  __shared__ long long hs[256];
+  __shared__ unsigned hc[256];
+  const int s = blockIdx.x;
+  const float* __restrict__ xs = x + x_off[s];
+  uint8_t* __restrict__ qs = q + q_off[s];
+  const int n = len[s];
+  double sum = 0.0;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += Q_THREADS) {
+    const float v = xs[i];
+    sum += v;
+    m = fmaxf(m, fabsf(v));
+  }
+  const double t = block_sum_d(sum, red);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mm = 0.f;
+    for (int i = 0; i < Q_THREADS / 64; ++i) mm = fmaxf(mm, redm[i]);
+    bc[0] = t / (double)(n > 0 ? n : 1);
+    const double lim = 4.611686018427388e18 / ((double)(n > 0 ? n : 1) * ((double)mm + 1e-30));
+    int sh = (int)floor(log2(lim));
+    sh = sh > 60 ? 60 : (sh < -60 ? -60 : sh);
+    bc[2] = ldexp(1.0, sh);
+  }
+  hs[threadIdx.x] = 0;
+  hc[threadIdx.x] = 0;
+  __syncthreads();
+  const double mean = bc[0];
+  double v2 = 0.0;
+  for (int i = threadIdx.x; i < n; i += Q_THREADS) {
+    const double d = (double)xs[i] - mean;
+    v2 += d * d;
+  }
+  const double t2 = block_sum_d(v2, red);
+  if (threadIdx.x == 0) {
+    const double stdv = sqrt(t2 / (double)(n > 1 ? n - 1 : 1));
+    double scale = 6.0 * stdv / 256.0;
+    bc[1] = 1.0 / (scale > 1e-30 ? scale : 1e-30);
+  }
+  __syncthreads();
+  const float meanf = (float)mean;
+  const float inv = (float)bc[1];
+  const double fx = bc[2];
+  for (int i = threadIdx.x; i < n; i += Q_THREADS) {
+    const float v = xs[i];
+    float r = rintf((v - meanf) * inv) + 128.f;
+    r = fminf(fmaxf(r, 0.f), 255.f);
+    const int b = (int)r;
+    qs[i] = (uint8_t)b;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&hs[b]), (unsigned long long)llrint((double)v * fx));
+    atomicAdd(&hc[b], 1u);
+  }
+  __syncthreads();
+  const unsigned c = hc[threadIdx.x];
+  codebook[(size_t)s * 256 + threadIdx.x] = c ? (float)((double)hs[threadIdx.x] / fx / (double)c) : 0.f;
+}
+
+// out[out_off[s] + i] [+]= weight * codebook[256 s + q[q_off[s] + i]]
+__global__ __launch_bounds__(Q_THREADS) void uq8_seg_dequant_kernel(const uint8_t* __restrict__ q, const long* __restrict__ q_off,
+                                                                    const float* __restrict__ codebook,
+                                                                    const long* __restrict__ out_off, const int* __restrict__ len,
+                                                                    float* __restrict__ out, float weight, int accumulate) {
+  __shared__ float cb[256];
+  const int s = blockIdx.x;
+  cb[threadIdx.x] = codebook[(size_t)s * 256 + threadIdx.x];
+  __syncthreads();
+  const uint8_t* __restrict__ qs = q + q_off[s];
+  float* __restrict__ os = out + out_off[s];
+  const int n = len[s];
+  for (int i = threadIdx.x; i < n; i += Q_THREADS) {
+    const float v = weight * cb[qs[i]];
+    os[i] = accumulate ? os[i] + v : v;
+  }
+}
+
+void uq8_seg_compress(const float* x, const long* x_off, const long* q_off, const int* len, int nseg, uint8_t* q,
+                      float* codebook, hipStream_t st) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(uq8_seg_compress_kernel, dim3(nseg), dim3(Q_THREADS), 0, st, x, x_off, q_off, len, q, codebook);
+}
+
+void uq8_seg_dequant(const uint8_t* q, const long* q_off, const float* codebook, const long* out_off, const int* len, int nseg,
+                     float* out, float weight, int accumulate, hipStream_t st) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(uq8_seg_dequant_kernel, dim3(nseg), dim3(Q_THREADS), 0, st, q, q_off, codebook, out_off, len, out, weight,
+                     accumulate);
+}
+
 void uq8_compress(const float* x, long n, uint8_t* q, float* codebook, void* ws, hipStream_t st) {
   // ws: [Q_BLOCKS doubles | Q_BLOCKS floats | 4 doubles | Q_BLOCKS*256 int64 | Q_BLOCKS*256 uint32]
   double* part = reinterpret_cast<double*>(ws);

@@ -164,6 +164,16 @@ def grads_finite(buf: torch.Tensor) -> bool:
     return bool(torch.isfinite(buf).all())
 
 
+def zero_grads_if_nonfinite_(buf: torch.Tensor) -> torch.Tensor:
+    """Zero a flat fp32 gradient buffer iff it holds a NaN/Inf, entirely on the device (no host sync):
+    the trainer's guarded ``zero_grad`` (``lib/training/hf_trainer.py:73-78``). Returns the flag tensor."""
+    if buf.is_cuda and backend_for(buf) == "hip":
+        return _hip().zero_if_nonfinite_(buf)
+    bad = ~torch.isfinite(buf).all()
+    buf.mul_((~bad).to(buf.dtype)).nan_to_num_(0.0, 0.0, 0.0)
+    return bad.to(torch.int32).reshape(1)
+
+
 def residual_add(x, y):
     return x + y.to(x.dtype)
 

@@ -882,3 +882,8 @@ def logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len: int, nu
 
 def nonfinite_flag(x: torch.Tensor) -> torch.Tensor:
     return C().nonfinite(x.contiguous())
+
+
+def zero_if_nonfinite_(x: torch.Tensor) -> torch.Tensor:
+    assert x.is_contiguous() and x.dtype == torch.float32
+    return C().zero_if_nonfinite_(x)

@@ -22,7 +22,8 @@ ALIGN = 4096
 
 
 class FlatArena:
-    def __init__(self, params: Sequence[torch.nn.Parameter], device=None, dtype=torch.float32, align: int = ALIGN):
+    def __init__(self, params: Sequence[torch.nn.Parameter], device=None, dtype=torch.float32, align: int = ALIGN,
+                 pin_memory: bool = False):
         seen = set()
         uniq: List[torch.nn.Parameter] = []
         for p in params:
@@ -38,8 +39,10 @@ class FlatArena:
             off += (p.numel() + align - 1) // align * align
         self.numel = off
         device = device if device is not None else (uniq[0].device if uniq else "cpu")
-        self.data = torch.zeros(off, dtype=dtype, device=device)
-        self.grad = torch.zeros(off, dtype=dtype, device=device)
+        # pinned host arenas (optimizer offload) make the D2H / H2D transfers DMA-able and asynchronous
+        pin = bool(pin_memory) and torch.device(device).type == "cpu" and torch.cuda.is_available()
+        self.data = torch.zeros(off, dtype=dtype, device=device, pin_memory=pin)
+        self.grad = torch.zeros(off, dtype=dtype, device=device, pin_memory=pin)
         for p, o in zip(uniq, self.offsets):
             n = p.numel()
             self.data[o:o + n].copy_(p.data.reshape(-1))
@@ -68,6 +71,11 @@ class FlatArena:
 
     def grads_are_bound(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == self.grad[o:].data_ptr() for p, o in zip(self.params, self.offsets))
+
+    def segments(self) -> List[tuple]:
+        """``(offset, numel)`` of every tensor in the flat buffers (the alignment padding excluded):
+        the unit the averaging compressors work on (per-tensor choice, per-part codebooks)."""
+        return [(o, p.numel()) for p, o in zip(self.params, self.offsets)]
 
     def tensor_views(self, buf: torch.Tensor) -> List[torch.Tensor]:
         return [buf[o:o + p.numel()].view_as(p) for p, o in zip(self.params, self.offsets)]

@@ -15,6 +15,12 @@ side HIP stream ordered by two events:
 so the optimizer kernels fill the gaps of the next micro-batch's kernels instead of serialising with
 them. On CPU peers the same step runs in a background thread (the torch ops release the GIL).
 
+Host offload (``offload_device="cpu"``, the reference's regime: ``CPULAMB8Bit`` on offloaded params,
+``lib/training/lamb_8bit.py:138``; and the dead ``lib/training/offload.py`` wrapper's purpose): the
+master copy lives in PINNED host memory and the optimizer step runs in the background thread on the
+CPU; the pull is one D2H copy of the parameter + gradient arenas, the push one H2D copy. Only for
+models whose optimizer state must leave HBM -- with 288 GB per MI355X none of the presets needs it.
+
 Nothing but the master copy is touched by the side stream / thread, and the main stream touches the
 master copy only before ``ev_ready`` and after ``ev_done``: the overlap is race-free by
 construction.
@@ -33,7 +39,7 @@ class MasterParams:
     """fp32 master copies of the trainable parameters, laid out like the model's arena (identical
     offsets), so model <-> master transfers are single contiguous copies."""
 
-    def __init__(self, params: List[torch.nn.Parameter], arena: Optional[FlatArena] = None):
+    def __init__(self, params: List[torch.nn.Parameter], arena: Optional[FlatArena] = None, device=None):
         self.model_params = list(params)
         self.model_arena = arena
         order = arena.params if arena is not None else self.model_params
@@ -44,11 +50,13 @@ class MasterParams:
         self._of = {}
         masters = []
         for p in order:
-            m = torch.nn.Parameter(p.detach().clone().float(), requires_grad=True)
+            m = torch.nn.Parameter(p.detach().to(device or p.device, dtype=torch.float32, copy=True), requires_grad=True)
             self._of[id(p)] = m
             masters.append(m)
         self.masters = masters
-        self.arena = FlatArena(masters, device=masters[0].device) if (arena is not None and masters) else None
+        self.offloaded = bool(masters) and masters[0].device.type == "cpu" and order[0].device.type != "cpu"
+        self.arena = FlatArena(masters, device=masters[0].device, pin_memory=self.offloaded) \
+            if (arena is not None and masters) else None
         if self.arena is None:
             for m in masters:
                 m.grad = torch.zeros_like(m)
@@ -65,6 +73,7 @@ class MasterParams:
     def pull(self):
         """model params + averaged grads -> master (before the step)."""
         if self.arena is not None:
+            # D2H for an offloaded master: a synchronous copy -- the host step reads it right after
             self.arena.data.copy_(self.model_arena.data)
             self.arena.grad.copy_(self.model_arena.grad)
             return
@@ -79,7 +88,7 @@ class MasterParams:
     def push(self):
         """master params -> model (the update becomes visible to compute)."""
         if self.arena is not None:
-            self.model_arena.data.copy_(self.arena.data)
+            self.model_arena.data.copy_(self.arena.data, non_blocking=self.offloaded)  # pinned H2D: async DMA
             return
         for p, m in self._pairs:
             p.data.copy_(m.data)

@@ -12,7 +12,7 @@ any process that is not itself a trainer):
   store, so generations never see each other's keys.
 * **failure** -- collectives run under a timeout (the watchdog: ``allreduce_timeout``); a dead peer makes
   them raise (gloo: connection closed; RCCL: ``Work.wait`` timeout). The survivors then ``regroup()``:
-  abort / destroy the old communicator and rendezvous in generation ``g + 1``. Whoever arrives first
+  abort the old communicator (never a blocking teardown) and rendezvous in generation ``g + 1``. Whoever arrives first
   bumps the generation counter with a compare-and-set, so a failure seen by several ranks bumps it once.
 * **joining** -- a peer that arrives after a generation froze raises the ``join_pending`` flag and waits
   for the next generation; members poll the flag once per global step (``poll_join``: one store read
@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..utils.logging import get_logger
+from .watchdog import abort_group
 
 logger = get_logger(__name__)
 
@@ -138,8 +139,11 @@ class ElasticGroup:
         """Abort the current communicator and rendezvous in the next generation with whoever is alive."""
         old = self.generation
         if dist.is_initialized():
+            # ABORT first (ncclCommAbort: releases kernels stuck on a dead peer without waiting for them),
+            # then drop the registry entry so the next generation can initialise the default group again
+            abort_group()
             try:
-                dist.destroy_process_group()  # RCCL: aborts the communicator (ncclCommAbort)
+                dist.destroy_process_group()
             except Exception as e:  # noqa: BLE001 - a broken group may fail to tear down cleanly
                 logger.warning(f"[elastic] destroy_process_group: {e!r}")
         # first survivor to get here opens generation old+1 (compare-and-set: bumped exactly once)

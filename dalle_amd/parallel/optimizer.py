@@ -15,9 +15,16 @@ Normative behaviour (``task.py:127-134``, ``arguments.py:59-78``):
 7. Resync: a peer whose epoch lags the collaboration loads the state from a donor peer.
 
 Peers are the ranks of a ``torch.distributed`` process group (backend "nccl" = RCCL over xGMI on a
-MI355X node; "gloo" for CPU peers). Progress is tracked with one tiny all-reduce per local step
-(``progress.py``), which makes the epoch decision identical on every rank, so the static RCCL
-communicator replaces hivemind's matchmaking.
+MI355X node; "gloo" for CPU peers). Progress is asynchronous (``progress.py``, mode ``store``): every
+peer adds its samples to a per-epoch counter in the job's key/value store and accumulates at its own
+pace; whoever sees the total reach ``target_batch_size`` enters the round. The round opens with ONE
+tiny all-gather of every peer's ``(samples, epoch)`` -- the exact weights, and a collective decision
+on resynchronising lagging peers -- so the static RCCL communicator replaces hivemind's matchmaking.
+Homogeneous nodes may use mode ``static`` (no communication outside the averaging itself).
+
+Deadlines (``watchdog.py``): the averaging round runs under ``averaging_timeout``; on expiry or a dead
+peer the communicator is aborted, the peer keeps its own gradients and parameters for that epoch and
+continues without the group (or re-forms one through an ``ElasticGroup``).
 """
 from __future__ import annotations
 
@@ -32,11 +39,21 @@ from .compression import CompressionBase, NoCompression
 from .delayed import AsyncStep, MasterParams
 from .powersgd import PowerSGD
 from .progress import ProgressTracker
+from .watchdog import Deadline, abort_group, wait_device
 from ..optim.flat import FlatArena
 from ..utils import faults
 from ..utils.logging import get_logger
 
 logger = get_logger(__name__)
+
+
+def _segments_of(tensors) -> List[tuple]:
+    """``(offset, numel)`` of tensors packed back to back (``torch.cat`` of their flattened views)."""
+    out, off = [], 0
+    for t in tensors:
+        out.append((off, t.numel()))
+        off += t.numel()
+    return out
 
 
 def _group_world(group):
@@ -50,7 +67,8 @@ class GradientAverager:
 
     def __init__(self, params: List[torch.nn.Parameter], arena: Optional[FlatArena] = None, group=None,
                  reuse_grad_buffers: bool = False, compression: Optional[CompressionBase] = None,
-                 powersgd: Optional[PowerSGD] = None, client_mode: bool = False):
+                 powersgd: Optional[PowerSGD] = None, client_mode: bool = False,
+                 averaging_timeout: Optional[float] = None):
         self.params = params
         self.arena = arena
         self.group = group
@@ -58,10 +76,17 @@ class GradientAverager:
         self.compression = compression or NoCompression()
         self.powersgd = powersgd
         self.client_mode = client_mode
+        self.averaging_timeout = averaging_timeout
         self.local_samples_accumulated = 0
         self.local_times_accumulated = 0
         self._acc: Optional[List[torch.Tensor]] = None
         self.last_averaging_ok = True
+        self.last_round_exact = False  # the last round was an uncompressed all-reduce that succeeded
+        self.detached = False          # the communicator was aborted: this peer continues alone
+        self.comm_failed = False       # set when a collective failed (timeout / dead peer)
+
+    def _world(self):
+        return (1, 0) if self.detached else _group_world(self.group)
 
     # -- accumulation -----------------------------------------------------------------------------
     @torch.no_grad()
@@ -88,41 +113,59 @@ class GradientAverager:
     @torch.no_grad()
     def step(self, total_samples: Optional[int] = None, epoch: int = 0) -> bool:
         """Replace the accumulated grads with the collaboration-wide weighted mean (in the params'
-        ``.grad``). Returns False if averaging failed and the local mean was used instead."""
+        ``.grad``). Returns False if averaging failed and this peer's own mean gradient was used."""
         t = max(1, self.local_times_accumulated)
         s = float(self.local_samples_accumulated)
-        world, _ = _group_world(self.group)
+        world, _ = self._world()
         grads = self._grads()
-        ok = True
-        try:
-            faults.before_averaging(epoch)
-            if world == 1:
-                for g in grads:
-                    g.div_(t)
-            elif self.powersgd is not None:
-                total = float(total_samples) if total_samples else None
-                if total is None:
-                    tt = torch.tensor([s], device=grads[0].device, dtype=torch.float32)
-                    dist.all_reduce(tt, group=self.group)
-                    total = float(tt.item())
-                if not self.reuse_grad_buffers:
-                    for p, g in zip(self.params, grads):
-                        p.grad = g
-                self.powersgd.allreduce_(scale=(s / t) * world / max(total, 1e-30))
-            else:
-                # x_p = per-peer MEAN gradient (g_p / t_p), weighted by its sample count s_p
-                flat, views = self._flat(grads)
-                shards = None if isinstance(self.compression, NoCompression) else self._shard_weights(world)
-                allreduce_weighted(flat, weight=s, group=self.group, compression=self.compression,
-                                   shard_weights=shards, total_weight=total_samples)
-                if views is not None:
-                    self._unflat(flat, views)
-        except Exception as e:  # noqa: BLE001 - a dead / slow peer must not kill training (SURVEY §5.3)
-            logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
-            ok = False
-            if not (self.arena is not None and self.reuse_grad_buffers and world > 1):
-                for g in grads:
-                    g.div_(t)
+        ok, exact = True, False
+        if world == 1:
+            try:
+                faults.before_averaging(epoch)
+            except Exception as e:  # noqa: BLE001
+                logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
+                ok = False
+            for g in grads:
+                g.div_(t)
+        else:
+            flat, views = self._flat(grads)  # x_p = this peer's MEAN gradient (g_p / t_p), one flat buffer
+            try:
+                faults.before_averaging(epoch)
+                injected = False
+            except Exception as e:  # noqa: BLE001 - an injected failure happens before any collective
+                logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
+                ok, injected = False, True
+            if not injected:
+                backup = flat.clone()
+                deadline = Deadline(self.averaging_timeout)
+                try:
+                    if self.powersgd is not None:
+                        total = float(total_samples) if total_samples else None
+                        if total is None:
+                            tt = torch.tensor([s], device=flat.device, dtype=torch.float32)
+                            dist.all_reduce(tt, group=self.group)
+                            total = float(tt.item())
+                        if views is not None:  # PowerSGD reads and writes the params' .grad
+                            self._unflat(flat, views)
+                            for p, g in zip(self.params, views):
+                                p.grad = g
+                        self.powersgd.allreduce_(scale=s * world / max(total, 1e-30))
+                        if views is not None:
+                            flat, views = self._flat_nodiv(grads), grads
+                    else:
+                        shards = None if isinstance(self.compression, NoCompression) else self._shard_weights(world)
+                        segs = self.arena.segments() if views is None else _segments_of(views)
+                        allreduce_weighted(flat, weight=s, group=self.group, compression=self.compression,
+                                           shard_weights=shards, total_weight=total_samples, segments=segs)
+                        exact = isinstance(self.compression, NoCompression)
+                    wait_device(flat.device, deadline, "gradient averaging")
+                except Exception as e:  # noqa: BLE001 - a dead / slow peer must not kill training (SURVEY §5.3)
+                    logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
+                    ok, exact = False, False
+                    self.comm_failed = True
+                    flat.copy_(backup)
+            if views is not None:
+                self._unflat(flat, views)
         if not self.reuse_grad_buffers:
             for p, g in zip(self.params, grads):
                 if p.grad is None:
@@ -130,6 +173,7 @@ class GradientAverager:
                 else:
                     p.grad.copy_(g)
         self.last_averaging_ok = ok
+        self.last_round_exact = exact
         return ok
 
     def _shard_weights(self, world: int):
@@ -152,8 +196,13 @@ class GradientAverager:
         if self.arena is not None and self.reuse_grad_buffers:
             self.arena.grad.div_(t)
             return self.arena.grad, None
-        flat = torch.cat([g.reshape(-1).float() for g in grads]) / t
-        return flat, grads
+        for g in grads:
+            g.div_(t)
+        return self._flat_nodiv(grads), grads
+
+    @staticmethod
+    def _flat_nodiv(grads):
+        return torch.cat([g.reshape(-1).float() for g in grads])
 
     @staticmethod
     def _unflat(flat, views):
@@ -184,11 +233,18 @@ class TrainingStateAverager:
     With ``master`` (a ``MasterParams``) the inner optimizer steps on master copies (hivemind's
     ``offload_optimizer``); with ``delay`` the step itself runs concurrently with the next local
     step (``delay_optimizer_step``, see ``delayed.py``) and is applied to the model -- followed by
-    the state-averaging round of that epoch -- at the next ``finish_pending`` boundary."""
+    the state-averaging round of that epoch -- at the next ``finish_pending`` boundary.
+
+    State averaging re-converges replicas that drifted (compressed or failed gradient rounds). After an
+    EXACT round (uncompressed RCCL all-reduce: every peer received bit-identical averaged gradients and
+    applied the same deterministic update to identical parameters) the replicas are already identical,
+    so the round is skipped when ``skip_if_exact`` ("skip when all peers apply identical
+    updates") -- on every peer alike, since the exactness flag is the same on all of them."""
 
     def __init__(self, optimizer: torch.optim.Optimizer, scheduler=None, params=None, arena: Optional[FlatArena] = None,
                  group=None, compression: Optional[CompressionBase] = None, average_state_every: int = 1,
-                 master: Optional[MasterParams] = None, delay: bool = False):
+                 master: Optional[MasterParams] = None, delay: bool = False, averaging_timeout: Optional[float] = None,
+                 skip_if_exact: bool = True):
         self.optimizer = optimizer
         self.scheduler = scheduler
         self.params = params
@@ -199,8 +255,14 @@ class TrainingStateAverager:
         self.local_epoch = 0
         self.master = master
         self.runner = AsyncStep(master.masters[0].device) if (delay and master is not None and master.masters) else None
+        self.averaging_timeout = averaging_timeout
+        self.skip_if_exact = skip_if_exact
+        self.detached = False
+        self.comm_failed = False
+        self.rounds_skipped = 0
         self._unapplied = False      # an update exists in the master copy but not in the model yet
         self._averaging_due = False  # the state-averaging round of the last delayed epoch has not run yet
+        self._exact = False          # the gradient round of the pending epoch was exact
 
     def _inner_step(self):
         self.optimizer.step()
@@ -208,7 +270,8 @@ class TrainingStateAverager:
             self.scheduler.step()
 
     @torch.no_grad()
-    def step(self, optimizer_step: bool = True, averaging_round: bool = True):
+    def step(self, optimizer_step: bool = True, averaging_round: bool = True, exact: bool = False):
+        self._exact = bool(exact)
         if optimizer_step:
             self.finish_pending(average=False)
             if self.master is not None:
@@ -258,22 +321,29 @@ class TrainingStateAverager:
 
     @torch.no_grad()
     def average_parameters(self):
-        world, _ = _group_world(self.group)
+        world, _ = (1, 0) if self.detached else _group_world(self.group)
         if world == 1:
             return
+        if self.skip_if_exact and self._exact:
+            self.rounds_skipped += 1
+            return
+        buf = self.arena.data if self.arena is not None else torch.cat([p.detach().reshape(-1).float() for p in self.params])
+        segs = self.arena.segments() if self.arena is not None else _segments_of(self.params)
+        backup = buf.clone()
+        deadline = Deadline(self.averaging_timeout)
         try:
-            if self.arena is not None:
-                allreduce_weighted(self.arena.data, 1.0, self.group, self.compression, total_weight=float(world))
-            else:
-                flat = torch.cat([p.detach().reshape(-1).float() for p in self.params])
-                allreduce_weighted(flat, 1.0, self.group, self.compression, total_weight=float(world))
-                off = 0
-                for p in self.params:
-                    k = p.numel()
-                    p.data.copy_(flat[off:off + k].view_as(p))
-                    off += k
+            allreduce_weighted(buf, 1.0, self.group, self.compression, total_weight=float(world), segments=segs)
+            wait_device(buf.device, deadline, "state averaging")
         except Exception as e:  # noqa: BLE001
             logger.warning(f"state averaging failed ({e!r}); keeping local parameters")
+            self.comm_failed = True
+            buf.copy_(backup)
+        if self.arena is None:
+            off = 0
+            for p in self.params:
+                k = p.numel()
+                p.data.copy_(buf[off:off + k].view_as(p))
+                off += k
 
 
 class CollaborativeOptimizer(torch.optim.Optimizer):
@@ -287,8 +357,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                  grad_compression: Optional[CompressionBase] = None,
                  state_averaging_compression: Optional[CompressionBase] = None, average_state_every: int = 1,
                  client_mode: bool = False, auxiliary: bool = False, verbose: bool = False, process_group=None,
-                 arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "collective",
-                 device=None, elastic=None, **kwargs):
+                 arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "auto",
+                 device=None, elastic=None, skip_exact_state_averaging: bool = True, offload_device=None, **kwargs):
         self.dht, self.run_id = dht, run_id
         self.target_batch_size = target_batch_size
         self.batch_size_per_step = batch_size_per_step
@@ -312,7 +382,10 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             logger.warning("delay_optimizer_step needs an optimizer factory (it builds the optimizer over master "
                            "copies); stepping synchronously")
         # delayed update: the inner optimizer owns master copies (hivemind's offloaded parameters, kept in HBM)
-        self._master = MasterParams(flat_params, arena) if (delay_optimizer_step and factory and flat_params) else None
+        # offload_device="cpu": the master copy + optimizer state live in pinned host memory and the step
+        # runs on the CPU (the reference's CPULAMB8Bit regime); default: an HBM master copy
+        want_master = factory and flat_params and (delay_optimizer_step or offload_device is not None)
+        self._master = MasterParams(flat_params, arena, device=offload_device) if want_master else None
         inner = optimizer(self._master.substitute(param_groups) if self._master else param_groups) if factory else optimizer
         if arena is not None and getattr(inner, "arena", "missing") is None:
             inner.arena = self._master.arena if self._master is not None else arena
@@ -320,19 +393,28 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         device = device or (flat_params[0].device if flat_params else torch.device("cpu"))
         self.device = device
         peer_id = dht.peer_id if dht is not None else f"rank{_group_world(process_group)[1]}"
+        if tracker_mode == "auto":
+            # asynchronous store records on a static group; the elastic generations keep the lockstep tracker
+            tracker_mode = "collective" if elastic is not None else "store"
         self.tracker = ProgressTracker(dht=dht, prefix=run_id, target_batch_size=target_batch_size, group=process_group,
                                        device=device, client_mode=client_mode, peer_id=peer_id, mode=tracker_mode)
         psgd = PowerSGD(flat_params, rank=powersgd_rank, group=process_group) if powersgd_rank else None
         self.grad_averager = GradientAverager(flat_params, arena=arena, group=process_group,
                                               reuse_grad_buffers=reuse_grad_buffers, compression=grad_compression,
-                                              powersgd=psgd, client_mode=client_mode)
+                                              powersgd=psgd, client_mode=client_mode,
+                                              averaging_timeout=averaging_timeout)
         self.state_averager = TrainingStateAverager(inner, sched, flat_params, arena=arena, group=process_group,
                                                     compression=state_averaging_compression,
                                                     average_state_every=average_state_every,
-                                                    master=self._master, delay=self._master is not None)
+                                                    master=self._master, delay=delay_optimizer_step and self._master is not None,
+                                                    averaging_timeout=averaging_timeout,
+                                                    skip_if_exact=skip_exact_state_averaging)
+        self.detached = False
         self.last_epoch_time = None
         if offload_optimizer and device.type == "cuda" and verbose:
-            logger.info("offload_optimizer=True: keeping the optimizer on-GPU (fused HIP LAMB; 288 GB HBM)")
+            where = "pinned host memory, CPU step" if (self._master is not None and self._master.offloaded) \
+                else "an HBM master copy (fused HIP LAMB; 288 GB HBM)"
+            logger.info(f"offload_optimizer=True: optimizer state in {where}")
         # torch.optim.Optimizer protocol (param_groups / state) for trainers and schedulers
         self.defaults = inner.defaults
         self._optimizer_step_pre_hooks = {}
@@ -390,20 +472,43 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             raise ValueError("batch_size_per_step (ctor) or batch_size (step) is required")
         self.grad_averager.accumulate_grads_(bs)
         if self.elastic is None:
-            self._collective_part(grad_scaler)
+            try:
+                self._collective_part(grad_scaler)
+            except Exception as e:  # noqa: BLE001 - the round's own collectives (boundary sync, resync)
+                logger.warning(f"{self.run_id}: collective failure ({e!r})")
+                self.grad_averager.comm_failed = True
+            if self._comm_failed():
+                self.detach()
             return loss
         try:
             self._collective_part(grad_scaler)
-            if not self.grad_averager.last_averaging_ok:
+            if self._comm_failed() or not self.grad_averager.last_averaging_ok:
                 raise RuntimeError("gradient averaging failed")
         except Exception as e:  # noqa: BLE001 - a member died / timed out: re-form the group and go on
             logger.warning(f"{self.run_id}: collective failure ({e!r}); regrouping")
             self._regroup()
         return loss
 
+    def _comm_failed(self) -> bool:
+        return self.grad_averager.comm_failed or self.state_averager.comm_failed
+
+    def detach(self):
+        """The communicator is broken (a peer died or missed the deadline): abort it -- never block in a
+        teardown -- and go on training alone; every later epoch is a local one (a failed
+        round falls back to local gradients and still advances the epoch)."""
+        if self.detached:
+            return
+        logger.warning(f"{self.run_id}: aborting the communicator; this peer continues without the collaboration")
+        abort_group(self.group)
+        self.detached = True
+        self.grad_averager.detached = self.state_averager.detached = True
+        self.grad_averager.comm_failed = self.state_averager.comm_failed = False
+        self.tracker.mode = "local"
+
     def _collective_part(self, grad_scaler):
         self.tracker.report_local_progress(self.local_epoch, self.grad_averager.local_samples_accumulated)
-        if self.tracker.max_epoch_seen > self.local_epoch + 1:
+        if self.tracker.mode in ("collective", "dht") and self.tracker.max_epoch_seen > self.local_epoch + 1:
+            # the lockstep tracker saw the epochs of all peers: the decision is identical on every rank
             logger.info(f"local epoch {self.local_epoch} lags the collaboration ({self.tracker.max_epoch_seen}); loading state")
             self.load_state_from_peers()
             self.grad_averager.reset_accumulated_grads_()
@@ -425,11 +530,44 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 self.grad_averager.powersgd.group = self.group
         self.grad_averager._shards = None
         self.grad_averager.last_averaging_ok = True
+        self.grad_averager.comm_failed = self.state_averager.comm_failed = False
         self.load_state_from_peers()
+
+    def _round_sync(self):
+        """Opening of an averaging round on the asynchronous tracker: ONE all-gather of every peer's
+        ``(samples accumulated, local epoch)``. Returns ``(total samples, min epoch, max epoch, peers)`` --
+        identical on every rank, so the weighting and the resync decision are collective."""
+        world, _ = (1, 0) if self.detached else _group_world(self.group)
+        s = float(self.grad_averager.local_samples_accumulated)
+        if world == 1 or self.tracker.mode not in ("store", "dht"):
+            gp = self.tracker.global_progress
+            total = gp.samples_accumulated if world > 1 else s
+            return total, self.local_epoch, self.local_epoch, max(1, gp.num_peers if world > 1 else 1)
+        dt = torch.float64 if self.device.type == "cpu" else torch.float32
+        mine = torch.tensor([s, float(self.local_epoch)], dtype=dt, device=self.device)
+        out = torch.empty(world * 2, dtype=dt, device=self.device)
+        deadline = Deadline(self.averaging_timeout)
+        if self.device.type == "cuda":
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+            wait_device(self.device, deadline, "round opening")
+        else:
+            work = dist.all_gather(list(out.chunk(world)), mine, group=self.group, async_op=True)
+            work.wait(timeout=__import__("datetime").timedelta(seconds=max(1.0, deadline.remaining())))
+        v = out.view(world, 2).tolist()
+        total = sum(r[0] for r in v)
+        epochs = [int(round(r[1])) for r in v]
+        return total, min(epochs), max(epochs), world
 
     def _update_global_epoch(self, grad_scaler=None):
         t0 = time.perf_counter()
-        total = self.tracker.global_progress.samples_accumulated
+        total, min_epoch, max_epoch, peers = self._round_sync()
+        if min_epoch < max_epoch - 1:
+            # some peer fell behind (e.g. restored an old local backup): everyone joins the resync
+            logger.info(f"{self.run_id}: epochs {min_epoch}..{max_epoch} diverged; resynchronising from the newest peer")
+            self.load_state_from_peers()
+            self.grad_averager.reset_accumulated_grads_()
+            self.tracker.update_epoch(self.local_epoch)
+            return
         if grad_scaler is not None and grad_scaler.is_enabled():
             # deferred AMP unscale + collaboration-wide overflow check (D28): skip the whole update
             # (and the averaging round) if any peer's accumulated grads overflowed
@@ -437,19 +575,22 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group):
                 logger.warning(f"{self.run_id}: non-finite scaled gradients at epoch {self.local_epoch}; skipping update")
                 self.grad_averager.reset_accumulated_grads_()
-                self.tracker.update_epoch(self.local_epoch + 1)
-                self.local_epoch = self.local_epoch + 1
+                self.local_epoch = max_epoch + 1
+                self.tracker.update_epoch(self.local_epoch)
                 return
-        self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
-        self.state_averager.step(optimizer_step=True, averaging_round=True)
+        ok = self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
+        exact = ok and self.grad_averager.last_round_exact and min_epoch == max_epoch
+        self.state_averager.step(optimizer_step=True, averaging_round=True, exact=exact)
+        if self.local_epoch < max_epoch + 1:  # a peer one epoch behind catches up on the count
+            self.local_epoch = max_epoch + 1
         if not self.state_averager.pending:
             faults.after_update(self.local_epoch, self._params)
         self.grad_averager.reset_accumulated_grads_()
         self.tracker.update_epoch(self.local_epoch)
         self.last_epoch_time = time.perf_counter() - t0
         if self.verbose:
-            logger.info(f"{self.run_id}: epoch {self.local_epoch} (averaged {total} samples across "
-                        f"{self.tracker.global_progress.num_peers} peers in {self.last_epoch_time * 1e3:.1f} ms)")
+            logger.info(f"{self.run_id}: epoch {self.local_epoch} (averaged {int(total)} samples across "
+                        f"{peers} peers in {self.last_epoch_time * 1e3:.1f} ms)")
 
     # -- delayed parameter update ---------------------------------------------------------------------
     def finish_pending(self) -> bool:
@@ -519,6 +660,36 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 self.scheduler.load_state_dict(sched[0])
         self.tracker.update_epoch(self.local_epoch)
         return rank != donor
+
+    def leave(self, poll: float = 0.02):
+        """A peer that finished training stays in the group until EVERY peer finished (asynchronous
+        peers finish at different times; a static communicator cannot lose a member mid-round): it
+        joins the remaining averaging rounds with zero samples -- receiving the averaged gradients and
+        applying the same update -- and exits once all peers announced the end. The end decision is
+        consistent: after the last peer announced, no peer adds samples, so the epoch counter is frozen."""
+        world, _ = (1, 0) if self.detached else _group_world(self.group)
+        if world == 1 or self.tracker.mode != "store":
+            return
+        store, done_key = self.tracker.store, f"{self.tracker._ns}/done"
+        self.grad_averager.reset_accumulated_grads_()
+        store.add(done_key, 1)
+        while not self.detached:
+            self.finish_pending()
+            if self._comm_failed():
+                self.detach()
+                break
+            self.tracker.report_local_progress(self.local_epoch, 0)
+            if self.tracker.ready_to_update_epoch:
+                try:
+                    self._update_global_epoch()
+                except Exception as e:  # noqa: BLE001
+                    logger.warning(f"{self.run_id}: collective failure while leaving ({e!r})")
+                    self.detach()
+                continue
+            if int(store.add(done_key, 0)) >= world:
+                break
+            time.sleep(poll)
+        self.finish_pending()
 
     def shutdown(self):
         self.apply_pending()

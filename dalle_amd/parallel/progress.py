@@ -4,15 +4,24 @@ Each peer reports ``(epoch, samples_accumulated, samples_per_second)``; the coll
 epoch advances when the peers of the current epoch together accumulated ``target_batch_size``
 samples.
 
-Two transports:
-* ``collective`` (peers are the ranks of a torch.distributed group -- one process per MI355X,
-  RCCL over xGMI): each local step does ONE tiny all-reduce of ``[samples, samples/s, peers,
-  clients, epoch]`` so every rank takes the identical "epoch is over" decision on the same step and
-  enters the gradient averaging round together (no matchmaking needed on a static communicator);
+Transports:
+* ``store`` (default for the ranks of a torch.distributed group -- one process per MI355X, RCCL over
+  xGMI): asynchronous progress records, no collective and no device sync per micro-step. Every peer
+  adds the samples it just accumulated to ONE atomic counter per epoch in the job's c10d key/value
+  store (``store.add``: one small TCP round trip, the reply is the collaboration-wide total). Peers
+  run at their own pace -- a faster GPU contributes more samples -- and each one enters the epoch's
+  averaging round as soon as the total it sees reaches ``target_batch_size`` (all peers see the same
+  monotone counter, so they arrive within one local step of each other). The exact per-peer sample
+  counts are exchanged by ONE tiny all-gather at the round itself (``CollaborativeOptimizer``).
+* ``static``: homogeneous peers with a fixed batch each step -- the global count is ``local * world``;
+  no communication at all (the headline benchmark).
+* ``collective``: one tiny all-reduce per local step (lockstep; kept for the elastic generations,
+  whose per-generation stores are short-lived).
 * ``dht`` (loosely coupled peers, e.g. the auxiliary monitor): records under ``{prefix}_progress``
   in the native key/value store, fetched periodically.
+* ``local``: a single peer.
 
-In both modes the local record is also published to the store for monitoring.
+In every mode the local record is also published to the key/value store (if any) for monitoring.
 """
 from __future__ import annotations
 
@@ -97,7 +106,15 @@ class ProgressTracker:
         self.device = device if device is not None else torch.device("cpu")
         self.client_mode = client_mode
         self.peer_id = peer_id
-        self.mode = mode if (mode != "collective" or (dist.is_available() and dist.is_initialized())) else "local"
+        grouped = dist.is_available() and dist.is_initialized()
+        if mode in ("collective", "store", "static") and not grouped:
+            mode = "local"
+        self.mode = mode
+        self.store = None
+        if mode == "store":
+            self.store = dist.distributed_c10d._get_default_store()
+            self._ns = f"collab/{prefix}"
+            self._reported = 0  # samples of the current epoch already added to the shared counter
         self.metadata_expiration = metadata_expiration
         self.report_period = report_period
         self.max_wait_time = max_wait_time
@@ -124,7 +141,9 @@ class ProgressTracker:
         self.local_progress = LocalTrainingProgress(self.peer_id, local_epoch, samples_accumulated,
                                                     self.performance_ema.samples_per_second, get_dht_time(),
                                                     self.client_mode)
-        if self.mode == "collective":
+        if self.mode == "store":
+            self._store_update(local_epoch, samples_accumulated)
+        elif self.mode == "collective":
             self._collective_update()
         elif self.mode == "static":
             # every rank contributes the same batch per step (asserted by the caller): the global count
@@ -146,6 +165,18 @@ class ProgressTracker:
         sps = self.performance_ema.samples_per_second * max(1, self.global_progress.num_peers)
         remaining = max(0, self.target_batch_size - samples)
         return get_dht_time() + (remaining / sps if sps > 0 else float("inf"))
+
+    def _store_update(self, local_epoch: int, samples_accumulated: int):
+        delta = max(0, int(samples_accumulated) - self._reported)
+        if self.max_wait_time is not None and time.perf_counter() - self._epoch_start > self.max_wait_time \
+                and samples_accumulated > 0:
+            delta += self.target_batch_size  # ETA deadline: close the epoch for everyone (the round counts exactly)
+        total = int(self.store.add(f"{self._ns}/e{local_epoch}/samples", delta))
+        self._reported = int(samples_accumulated)
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        self.max_epoch_seen = max(self.max_epoch_seen, local_epoch)
+        self.global_progress = GlobalTrainingProgress(local_epoch, total, self.target_batch_size, world,
+                                                      int(self.client_mode), self._eta(total), 0.0)
 
     def _collective_update(self):
         lp = self.local_progress
@@ -217,6 +248,8 @@ class ProgressTracker:
         return False
 
     def update_epoch(self, new_epoch: int):
+        if self.mode == "store":
+            self._reported = 0
         self.local_progress = LocalTrainingProgress(self.peer_id, new_epoch, 0, self.performance_ema.samples_per_second,
                                                     get_dht_time(), self.client_mode)
         self.global_progress = GlobalTrainingProgress(max(new_epoch, self.global_progress.epoch), 0, self.target_batch_size,

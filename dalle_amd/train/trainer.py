@@ -11,10 +11,13 @@ Reference behaviour (``lib/training/hf_trainer.py:15-85``, ``run_trainer.py:41-5
 * callbacks follow the ``TrainerCallback`` protocol: ``on_train_begin(args, state, control)``,
   ``on_step_end(args, state, control)`` with ``state.log_history[-1]["loss"]`` and
   ``control.should_log``.
+
+No host synchronisation per micro-step: the loss stays a device scalar (``DeferredScalar``: read --
+and synced -- only by whoever needs the number, e.g. the callback once per epoch), and the guarded
+``zero_grad`` zeroes non-finite accumulated gradients with a device-side flag.
 """
 from __future__ import annotations
 
-import math
 import os
 import time
 from dataclasses import dataclass, field
@@ -42,6 +45,24 @@ class TrainerControl:
     should_log: bool = False
     should_save: bool = False
     should_training_stop: bool = False
+
+
+class DeferredScalar:
+    """A device scalar that is read lazily: ``float()`` synchronises once and caches the value."""
+
+    __slots__ = ("tensor", "_value")
+
+    def __init__(self, tensor: torch.Tensor):
+        self.tensor = tensor.detach()
+        self._value = None
+
+    def __float__(self) -> float:
+        if self._value is None:
+            self._value = float(self.tensor)
+        return self._value
+
+    def __repr__(self):
+        return f"DeferredScalar({float(self):.6g})"
 
 
 class TrainerCallback:
@@ -97,11 +118,12 @@ class IgnoreGradManipulations(torch.nn.Module):
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         arena = getattr(self.module, "grad_arena", None)
-        if arena is not None:  # one fused finiteness check over the flat gradient arena
-            from ..ops import grads_finite
-            if self.override_zero_grad and grads_finite(arena.grad):
-                return
-            arena.zero_grad()
+        if arena is not None:  # one fused finiteness check over the flat gradient arena, on the device
+            if self.override_zero_grad:
+                from ..ops import zero_grads_if_nonfinite_
+                zero_grads_if_nonfinite_(arena.grad)
+            else:
+                arena.zero_grad()
             return
         params = [p for p in self.parameters() if p.requires_grad and p.grad is not None]
         if self.override_zero_grad and all(torch.isfinite(p.grad).all() for p in params):
@@ -175,7 +197,7 @@ class CollaborativeHFTrainer:
         max_steps = int(args.max_steps)
         t0 = time.perf_counter()
         while self.state.global_step < max_steps and not self.control.should_training_stop:
-            total = 0.0
+            total = None
             for _ in range(accum):
                 batch = next(loader)
                 batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
@@ -184,7 +206,7 @@ class CollaborativeHFTrainer:
                     loss = out["loss"] / accum
                 with prof_range("backward"):
                     (self.grad_scaler.scale(loss) if self.grad_scaler is not None else loss).backward()
-                total += float(loss.detach())
+                total = loss.detach() if total is None else total + loss.detach()
             self.model.clip_grad_norm_(args.max_grad_norm)
             with prof_range("collaborative_step"):
                 if self.grad_scaler is not None:
@@ -197,12 +219,13 @@ class CollaborativeHFTrainer:
             self.state.global_step += 1
             self.control.should_log = False
             # the collaborative callback forces should_log every step (callback.py:49): log every step
-            self.state.log_history.append({"loss": total, "step": self.state.global_step,
+            self.state.log_history.append({"loss": DeferredScalar(total), "step": self.state.global_step,
                                            "learning_rate": self.collaborative_optimizer.param_groups[0]["lr"],
                                            "elapsed": time.perf_counter() - t0})
             self._call("on_step_end")
-            if not math.isfinite(total):
-                logger.warning(f"non-finite loss at step {self.state.global_step}")
+        leave = getattr(self.collaborative_optimizer, "leave", None)
+        if leave is not None:  # asynchronous peers finish at different times: serve the others' last rounds
+            leave()
         apply_pending = getattr(self.collaborative_optimizer, "apply_pending", None)
         if apply_pending is not None:  # a delayed optimizer step still in flight lands in the model
             apply_pending()

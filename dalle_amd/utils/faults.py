@@ -10,6 +10,8 @@ optimizer and the trainer (all no-ops when unset):
 * ``DALLE_AMD_FAULT_FAIL_AVERAGING=<epoch>``  -- raise inside the averaging round of that epoch
                                               (exercises the fall-back-to-local-gradients path)
 * ``DALLE_AMD_FAULT_KILL_AT_EPOCH=<epoch>``  -- hard-exit the process (dead peer)
+* ``DALLE_AMD_FAULT_KILL_IN_AVERAGING=<epoch>`` -- hard-exit inside that epoch's averaging round, after the
+                                              round opened (the survivors are already in the collective)
 * ``DALLE_AMD_DEBUG_SYNC=1``                 -- synchronise the device after every fused op (debug mode;
                                               pairs with ``AMD_SERIALIZE_KERNEL=3`` / ``HIP_LAUNCH_BLOCKING=1``)
 """
@@ -35,6 +37,8 @@ def before_averaging(epoch: int):
     d = os.environ.get("DALLE_AMD_FAULT_DELAY_AVERAGING")
     if d:
         time.sleep(float(d))
+    if _int("DALLE_AMD_FAULT_KILL_IN_AVERAGING") == epoch:
+        os._exit(17)
     if _int("DALLE_AMD_FAULT_FAIL_AVERAGING") == epoch:
         raise RuntimeError(f"injected averaging failure at epoch {epoch}")
 

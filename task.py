@@ -174,6 +174,7 @@ class TrainingTask:
                 grad_compression=averaging_compression, state_averaging_compression=averaging_compression,
                 client_mode=self.peer_args.client_mode, verbose=True, process_group=group, arena=self._arena,
                 powersgd_rank=ta.powersgd_rank if ta.grad_averaging == "powersgd" else None, elastic=self._elastic,
+                offload_device="cpu" if getattr(ta, "offload_optimizer_to_host", False) else None,
                 **{k: v for k, v in vars(self.collab_args).items()})
         return self._collaborative_optimizer
 
@@ -188,13 +189,12 @@ class TrainingTask:
             {"params": [p for n, p in self.model.named_parameters() if any(nd in n for nd in no_decay) and p.requires_grad],
              "weight_decay": 0.0},
         ]
-        arena = self._arena
 
         def opt(params):
             return LAMB8bit(params, lr=training_args.learning_rate, betas=(training_args.adam_beta1, training_args.adam_beta2),
                             eps=training_args.adam_epsilon, weight_decay=training_args.weight_decay,
                             max_grad_norm=training_args.max_grad_norm, clamp_value=training_args.clamp_value,
-                            reuse_grad_buffers=True, optim_bits=training_args.optimizer_bits, arena=arena)
+                            reuse_grad_buffers=True, optim_bits=training_args.optimizer_bits)
 
         def scheduler(opt):
             return get_linear_schedule_with_warmup(opt, num_warmup_steps=training_args.warmup_steps,

@@ -1,0 +1,44 @@
+"""bench.py's multi-rank contract on CPU (gloo): ``--gpus N`` without a launcher spawns N ranks,
+each asserts the group size, the ranks stay bitwise identical, and only rank 0 prints one JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(tmp_path, *extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(BENCH_BACKEND="gloo", BENCH_DUMP_PARAMS=str(tmp_path / "params"), HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--model", "tiny", "--batch", "2", *extra], env=env, cwd=str(tmp_path), capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    p0 = torch.load(tmp_path / "params.rank0.pt", weights_only=True)
+    p1 = torch.load(tmp_path / "params.rank1.pt", weights_only=True)
+    return res, p0, p1
+
+
+@pytest.mark.parametrize("engine", ["step", "collab"])
+def test_bench_spawns_n_ranks(tmp_path, engine):
+    res, p0, p1 = _run(tmp_path, "--engine", engine)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 4
+    assert len(res["per_rank_ms_per_step"]) == 2 and res["value"] > 0
+    assert torch.equal(p0, p1)  # replicas stay bitwise identical
+    if engine == "collab":
+        assert res["config"]["engine"] == "CollaborativeOptimizer.step"
+        assert res["collab_performance_ema_samples_per_s"] > 0
+
+
+def test_bench_rejects_world_mismatch(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", BENCH_BACKEND="gloo", HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny"], env=env,
+                         cwd=str(tmp_path), capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

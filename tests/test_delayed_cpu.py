@@ -13,7 +13,7 @@ from dalle_amd.parallel.optimizer import CollaborativeOptimizer
 from test_collab_cpu import _init, _run
 
 
-def _make(delay: bool, use_arena: bool, shape=(300, 500), seed=0):
+def _make(delay: bool, use_arena: bool, shape=(300, 500), seed=0, tracker_mode="auto"):
     torch.manual_seed(seed)
     w = torch.nn.Parameter(torch.randn(*shape) * 0.1)
     b = torch.nn.Parameter(torch.zeros(shape[0]))
@@ -24,7 +24,7 @@ def _make(delay: bool, use_arena: bool, shape=(300, 500), seed=0):
                                                                weight_decay=0.045, max_grad_norm=4.0),
                                  scheduler=lambda o: get_linear_schedule_with_warmup(o, 0, 20),
                                  target_batch_size=4, batch_size_per_step=2, reuse_grad_buffers=True,
-                                 delay_optimizer_step=delay, offload_optimizer=True)
+                                 delay_optimizer_step=delay, offload_optimizer=True, tracker_mode=tracker_mode)
     return w, b, opt
 
 
@@ -92,7 +92,8 @@ def test_restore_drops_pending_update():
 def _delayed_dp_worker(rank, world, port, q, delay):
     try:
         _init(rank, world, port)
-        w, b, opt = _make(delay, True, shape=(64, 96), seed=0)
+        # homogeneous peers, one global step per local step: the static tracker (deterministic epochs)
+        w, b, opt = _make(delay, True, shape=(64, 96), seed=0, tracker_mode="static")
         for step in range(6):
             _const_grads(w, b, 10 * rank + step)
             opt.step()

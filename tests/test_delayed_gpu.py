@@ -10,7 +10,7 @@ from dalle_amd.parallel.optimizer import CollaborativeOptimizer
 pytestmark = pytest.mark.gpu
 
 
-def _make(delay, dev):
+def _make(delay, dev, offload_device=None):
     torch.manual_seed(0)
     w = torch.nn.Parameter(0.05 * torch.randn(1024, 3072, device=dev))
     b = torch.nn.Parameter(torch.zeros(1024, device=dev))
@@ -23,7 +23,7 @@ def _make(delay, dev):
                                                                clamp_value=10000.0, reuse_grad_buffers=True),
                                  scheduler=lambda o: get_linear_schedule_with_warmup(o, 0, 50),
                                  target_batch_size=4, batch_size_per_step=2, reuse_grad_buffers=True,
-                                 delay_optimizer_step=delay, offload_optimizer=True)
+                                 delay_optimizer_step=delay, offload_optimizer=True, offload_device=offload_device)
     return (w, b, s), arena, opt
 
 
@@ -51,3 +51,25 @@ def test_delayed_side_stream_matches_sync(cuda):
     torch.cuda.synchronize()
     assert torch.equal(ar_sync.data, ar_dly.data)
     assert sync.local_epoch == dly.local_epoch == 4
+
+
+@pytest.mark.parametrize("delay", [False, True])
+def test_host_offload_matches_hbm_optimizer(cuda, delay):
+    """offload_device="cpu": pinned host master + CPU LAMB step (thread when delayed) == the HBM fused
+    path up to fp32 rounding of the two LAMB implementations (8-bit moments: same block maps)."""
+    ps_ref, ar_ref, ref = _make(False, cuda)
+    ps_off, ar_off, off = _make(delay, cuda, offload_device="cpu")
+    assert off._master.offloaded and off._master.arena.data.is_pinned()
+    assert not off.state_averager.optimizer._get_fused()  # the CPU path
+    for step in range(8):
+        g = torch.Generator(device=cuda).manual_seed(7 + step)
+        noise = torch.randn(ar_ref.numel, device=cuda, generator=g)
+        ar_ref.grad.add_(noise)
+        ar_off.grad.add_(noise)
+        ref.step()
+        off.step()
+    off.apply_pending()
+    torch.cuda.synchronize()
+    rel = ((ar_ref.data - ar_off.data).norm() / ar_ref.data.norm()).item()
+    assert rel < 1e-4, rel
+    assert off.local_epoch == 4

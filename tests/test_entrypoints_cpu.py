@@ -58,8 +58,11 @@ def test_two_peers_plus_aux(tmp_path):
         raise
     assert trainer.returncode == 0, tout[-4000:]
     assert aux.returncode == 0, aux.stdout[-4000:]
-    # 2 peers x 2 samples per step, target 8 -> an epoch every 2 local steps
-    assert "cfg1: epoch 5 (averaged 8 samples across 2 peers" in tout, tout[-3000:]
+    # 2 peers x 2 samples per step, target 8 -> an epoch every ~2 local steps per peer (asynchronous
+    # progress: a peer may add one more micro-batch before it notices the target was reached)
+    import re
+    assert re.search(r"cfg1: epoch 5 \(averaged (8|10|12) samples across 2 peers", tout), tout[-3000:]
+    assert "aborting the communicator" not in tout, tout[-3000:]
     records = [json.loads(l) for l in metrics_log.read_text().splitlines()]
     assert records and max(r["alive peers"] for r in records) == 2
     assert all(r["performance"] > 0 for r in records)
@@ -70,7 +73,8 @@ def test_two_peers_plus_aux(tmp_path):
     osd = torch.load(tmp_path / "repo" / "optimizer_state.pt", weights_only=True)
     assert "local_epoch" in osd["state"]
     # backups written by the training callback
-    st = torch.load(tmp_path / "state.zip", weights_only=True)
+    st = torch.load(tmp_path / "state.rank0.zip", weights_only=True)  # one backup file per peer
+    assert (tmp_path / "state.rank1.zip").exists()
     assert set(st) == {"model", "training", "scheduler", "local_epoch"}
 
 

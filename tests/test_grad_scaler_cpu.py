@@ -29,7 +29,7 @@ def _worker(rank, world, port, q, overflow_rank):
         p = torch.nn.Parameter(torch.zeros(64))
         opt = CollaborativeOptimizer(run_id="gs", params=[p], optimizer=lambda ps: torch.optim.SGD(ps, lr=1.0),
                                      target_batch_size=8, batch_size_per_step=2, reuse_grad_buffers=True,
-                                     average_state_every=0)
+                                     average_state_every=0, tracker_mode="static")  # homogeneous: deterministic epochs
         scaler = CollaborativeGradScaler(init_scale=1024.0, growth_interval=1)
         scales, steps = [], 0
         while opt.local_epoch == 0:

@@ -242,3 +242,38 @@ def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type, monkeypatc
         grads.append(x.grad.float())
     # one bf16 rounding (fused) vs two (separate pass)
     assert _rel(grads[0], grads[1]) < 8e-3, attn_type
+
+
+def test_segmented_uniform8bit_matches_per_part(cuda):
+    """One segmented launch (one workgroup per part, csrc/kernels/quant.hip) == the per-part quantiser
+    (same indices up to rounding ties, same per-part codebooks), and the segmented dequantiser puts every
+    part back at its own offset (accumulating or not)."""
+    from dalle_amd.parallel.averaging import _seg_compress, _seg_dequant
+    from dalle_amd.parallel.compression import Uniform8BitQuantization
+
+    torch.manual_seed(0)
+    x = torch.randn(700_000, device=cuda)
+    x[200_000:400_000] *= 1e-3  # parts of very different scale
+    parts = [(0, 131072), (131072, 68928), (200_000, 131072), (331_072, 68928), (450_000, 5), (500_000, 200_000)]
+    x_off = torch.tensor([o for o, _ in parts], dtype=torch.int64, device=cuda)
+    lens = torch.tensor([n for _, n in parts], dtype=torch.int32, device=cuda)
+    q_off = torch.tensor([0] + list(torch.tensor([n for _, n in parts]).cumsum(0)[:-1].tolist()), dtype=torch.int64,
+                         device=cuda)
+    total = sum(n for _, n in parts)
+    q = torch.empty(total, dtype=torch.uint8, device=cuda)
+    cb = torch.empty(len(parts) * 256, dtype=torch.float32, device=cuda)
+    _seg_compress(x, x_off, q_off, lens, q, cb, 700_000, total)
+    quant = Uniform8BitQuantization()
+    for i, ((o, n), qo) in enumerate(zip(parts, q_off.tolist())):
+        ref = quant.compress(x[o:o + n].contiguous())
+        mism = (q[qo:qo + n] != ref["idx"]).float().mean().item()
+        assert mism < 2e-3, (i, mism)
+        used = torch.bincount(ref["idx"].long(), minlength=256) > 0
+        assert torch.allclose(cb[i * 256:(i + 1) * 256][used], ref["codebook"][used], rtol=1e-3, atol=1e-7), i
+    out = torch.zeros(700_000, device=cuda)
+    _seg_dequant(q, q_off, cb, x_off, lens, out, total, 700_000, accumulate=False)
+    _seg_dequant(q, q_off, cb, x_off, lens, out, total, 700_000, accumulate=True)
+    for o, n in parts:
+        rel = ((out[o:o + n] / 2 - x[o:o + n]).norm() / x[o:o + n].norm()).item()
+        assert rel < 0.05, (o, rel)
+    assert out[450_005:500_000].abs().max().item() == 0.0  # outside every part: untouched
