@@ -130,6 +130,7 @@ class CollaborativeCallback(TrainerCallback):
         if state.log_history:
             self.stats.add(state.log_history[-1]["loss"])
             if opt.local_epoch != self.stats.reported_epoch:
+                self.stats.samples = getattr(opt, "last_round_samples", self.stats.samples)
                 self._finish_epoch(opt)
         self.stats.samples = opt.grad_averager.local_samples_accumulated
         self.snapshots.poll()

@@ -410,6 +410,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                                                     averaging_timeout=averaging_timeout,
                                                     skip_if_exact=skip_exact_state_averaging)
         self.detached = False
+        self.last_round_samples = 0  # this peer's samples in the last averaging round
         self.last_epoch_time = None
         if offload_optimizer and device.type == "cuda" and verbose:
             where = "pinned host memory, CPU step" if (self._master is not None and self._master.offloaded) \
@@ -585,6 +586,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             self.local_epoch = max_epoch + 1
         if not self.state_averager.pending:
             faults.after_update(self.local_epoch, self._params)
+        self.last_round_samples = int(self.grad_averager.local_samples_accumulated)
         self.grad_averager.reset_accumulated_grads_()
         self.tracker.update_epoch(self.local_epoch)
         self.last_epoch_time = time.perf_counter() - t0
@@ -671,7 +673,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if world == 1 or self.tracker.mode != "store":
             return
         store, done_key = self.tracker.store, f"{self.tracker._ns}/done"
-        self.grad_averager.reset_accumulated_grads_()
+        # the samples accumulated so far are already in the shared counter: they stay this peer's
+        # contribution to the next round (dropping them would make the round's weights disagree with it)
         store.add(done_key, 1)
         while not self.detached:
             self.finish_pending()

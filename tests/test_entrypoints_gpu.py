@@ -55,4 +55,7 @@ def test_single_peer_rccl(cuda, tmp_path):
 
 def test_two_peers_share_the_gpu_over_gloo(cuda, tmp_path):
     out = _run(tmp_path, 2, ["--backend", "gloo", "--target_batch_size", "16", "--max_steps", "8"])
-    assert re.search(r"averaged 16 samples across 2 peers", out), out[-3000:]
+    # asynchronous progress: each round averages at least the target (a peer may add one more micro-batch)
+    totals = [int(m) for m in re.findall(r"averaged (\d+) samples across 2 peers", out)]
+    assert totals and all(16 <= t <= 16 + 2 * 4 for t in totals), out[-3000:]
+    assert "aborting the communicator" not in out
