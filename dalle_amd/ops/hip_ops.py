@@ -20,10 +20,31 @@ from ..models.rotary import rotary_tables
 _C = None
 
 
+class _SyncedExtension:
+    """``DALLE_AMD_DEBUG_SYNC=1``: every native op is followed by a device synchronisation,
+    so an asynchronous fault or a race surfaces at the op that caused it, with its name."""
+
+    def __init__(self, ext):
+        self._ext = ext
+
+    def __getattr__(self, name):
+        fn = getattr(self._ext, name)
+
+        def synced(*args, **kwargs):
+            out = fn(*args, **kwargs)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError(f"dalle_amd._C.{name} failed on the device: {e}") from e
+            return out
+        return synced
+
+
 def C():
     global _C
     if _C is None:
-        _C = load_extension(required=True)
+        ext = load_extension(required=True)
+        _C = _SyncedExtension(ext) if os.environ.get("DALLE_AMD_DEBUG_SYNC") == "1" else ext
     return _C
 
 

@@ -5,8 +5,9 @@ unpack copies. Buckets are sized for the xGMI mesh: each of the 8
 point-to-point links; RCCL splits an all-reduce into per-peer slices, and a 64 MB bucket keeps each
 per-link slice at >= 4 MB, past the latency-bound regime, while still pipelining several
 collectives. With weight sharing (5 blocks reused by every layer, tied embedding) no gradient is
-final before the end of backward, so the all-reduce runs after ``backward()`` on a side stream and
-overlaps the (tiny) optimizer prologue only.
+final before the end of backward, so all buckets are issued after ``backward()``: RCCL runs them on
+its own stream back to back, and the compute stream only waits for them (``Work.wait`` is a stream
+dependency, not a host block) before the optimizer kernels -- nothing overlaps the all-reduce itself.
 
 ``grad_dtype='bf16'`` halves the bytes on the wire (the averaged gradient is accumulated in fp32
 by RCCL's reduction of bf16 inputs is bf16 -- use for large worlds only).

@@ -27,25 +27,30 @@ from dalle_amd.utils.logging import get_logger
 logger = get_logger(__name__)
 
 
+def _keep_example(caption, nsfw, width, height) -> bool:
+    """The reference run's LAION filter: a caption of >= 3 characters, rated SFW, and an image with
+    positive dimensions whose long side is at most twice its short side."""
+    if caption is None or len(caption) < 3 or nsfw != "UNLIKELY":
+        return False
+    if not (width > 0 and height > 0):
+        return False
+    return max(width, height) <= 2 * min(width, height)
+
+
 def preprocess_batch(batch, tokenizer, max_sequence_length: int):
-    mask = [
-        (
-            caption is not None and len(caption) >= 3 and
-            nsfw == 'UNLIKELY' and
-            orig_width > 0 and orig_height > 0 and
-            max(orig_height / orig_width, orig_width / orig_height) <= 2
-        ) for caption, nsfw, orig_width, orig_height in
-        zip(batch['caption'], batch['NSFW'], batch['original_width'], batch['original_height'])
-    ]
-    logger.debug(f'{np.mean(mask) * 100:.1f}% of examples left after filtering')
-    if any(mask):
-        result = tokenizer(list(itertools.compress(batch['caption'], mask)),
-                           add_special_tokens=False, max_length=max_sequence_length, truncation=True)
+    """Filter a column batch, tokenise the kept captions (no special tokens, truncated) and decode the
+    kept VQGAN code bytes (int16) into int64 token ids."""
+    columns = zip(batch["caption"], batch["NSFW"], batch["original_width"], batch["original_height"])
+    kept = [i for i, row in enumerate(columns) if _keep_example(*row)]
+    logger.debug(f"filter kept {len(kept)} of {len(batch['caption'])} examples")
+    captions = [batch["caption"][i] for i in kept]
+    if captions:  # an empty list would make the tokenizer raise
+        enc = tokenizer(captions, add_special_tokens=False, max_length=max_sequence_length, truncation=True)
+        out = {"input_ids": list(enc["input_ids"]), "attention_mask": list(enc["attention_mask"])}
     else:
-        result = {'input_ids': [], 'attention_mask': []}
-    result['image'] = [np.frombuffer(encoded, np.int16).astype(np.int64)
-                       for encoded in itertools.compress(batch['code'], mask)]
-    return result
+        out = {"input_ids": [], "attention_mask": []}
+    out["image"] = [np.frombuffer(batch["code"][i], dtype=np.int16).astype(np.int64) for i in kept]
+    return out
 
 
 def _iter_rows(path: str) -> Iterator[dict]:

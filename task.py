@@ -64,7 +64,8 @@ def make_averaging_compression(kind: str):
 
 
 class TrainingTask:
-    """A container that defines the training config, model, tokenizer, optimizer and other local training utilities"""
+    """Everything one collaborative peer trains with, built lazily: the DALL-E recipe, tokenizer, key/value
+    store, process group, collaborative optimizer (fused 8-bit LAMB + schedule), dataset and collator."""
     _authorizer = _dht = _collaborative_optimizer = _training_dataset = _process_group = _arena = _elastic = None
 
     def __init__(self, peer_args: BasePeerArguments, trainer_args: HFTrainerArguments, collab_args: CollaborativeArguments):
@@ -87,15 +88,18 @@ class TrainingTask:
         vae = VQGanParams(num_layers=cfg.vae_num_layers, image_size=cfg.image_size, num_tokens=cfg.num_image_tokens)
         dalle = DALLE(cfg, vae=None)
         dalle.vae_params = vae
-        logger.info(f"Trainable parameters: {sum(param.numel() for param in dalle.parameters() if param.requires_grad)}")
+        n_trainable = sum(p.numel() for p in dalle.parameters() if p.requires_grad)
+        logger.info(f"{n_trainable / 1e6:.1f}M trainable parameters ({n_trainable})")
         self.model = ModelWrapper(dalle)
 
         output_dir = Path(trainer_args.output_dir)
-        logger.info(f'Checkpoint dir {output_dir}, contents {list(output_dir.glob("checkpoint*"))}')
-        latest_checkpoint_dir = max(output_dir.glob("checkpoint*"), default=None, key=os.path.getctime)
-        if latest_checkpoint_dir is not None and (latest_checkpoint_dir / "model_state.pt").exists():
-            logger.info(f"Loading model from {latest_checkpoint_dir}")
-            self.model.load_state_dict(torch.load(latest_checkpoint_dir / "model_state.pt", map_location="cpu", weights_only=True))
+        # resume: the newest checkpoint* directory (by creation time) that holds a model_state.pt
+        candidates = sorted(output_dir.glob("checkpoint*"), key=os.path.getctime)
+        newest = candidates[-1] if candidates else None
+        if newest is not None and (newest / "model_state.pt").exists():
+            logger.info(f"resuming model weights from {newest / 'model_state.pt'}")
+            state = torch.load(newest / "model_state.pt", map_location="cpu", weights_only=True)
+            self.model.load_state_dict(state)
 
     @property
     def authorizer(self):
@@ -154,7 +158,7 @@ class TrainingTask:
             )
             if self._dht is not None:
                 if self.peer_args.client_mode:
-                    logger.info(f"Created client mode peer with peer_id={self._dht.peer_id}")
+                    logger.info(f"client-mode peer {self._dht.peer_id} (no inbound connections)")
                 else:
                     utils.log_visible_maddrs(self._dht.get_visible_maddrs(), only_p2p=self.peer_args.use_ipfs)
         return self._dht

@@ -277,3 +277,18 @@ def test_segmented_uniform8bit_matches_per_part(cuda):
         rel = ((out[o:o + n] / 2 - x[o:o + n]).norm() / x[o:o + n].norm()).item()
         assert rel < 0.05, (o, rel)
     assert out[450_005:500_000].abs().max().item() == 0.0  # outside every part: untouched
+
+
+def test_debug_sync_mode_wraps_every_native_op(cuda, monkeypatch):
+    """DALLE_AMD_DEBUG_SYNC=1: the native ops run through a synchronising proxy."""
+    from dalle_amd.ops import hip_ops
+
+    monkeypatch.setenv("DALLE_AMD_DEBUG_SYNC", "1")
+    monkeypatch.setattr(hip_ops, "_C", None)
+    try:
+        C = hip_ops.C()
+        assert isinstance(C, hip_ops._SyncedExtension)
+        x = torch.randn(4096, device=cuda)
+        assert int(C.nonfinite(x).item()) == 0
+    finally:
+        monkeypatch.setattr(hip_ops, "_C", None)

@@ -136,3 +136,42 @@ def test_state_dict_roundtrip():
     opt.step()
     opt2.step()
     assert torch.allclose(p, p2)
+
+
+def test_monitor_summary_matches_reference_aggregation():
+    """Aux-peer aggregation (dalle_amd.utils.monitor.summarize): mean loss over all mini-steps, summed
+    samples and samples/s, alive peers = records."""
+    from types import SimpleNamespace as R
+
+    from dalle_amd.utils.monitor import summarize
+
+    recs = [R(step=7, loss=6.0, mini_steps=3, samples_accumulated=12, samples_per_second=10.0),
+            R(step=7, loss=2.0, mini_steps=1, samples_accumulated=4, samples_per_second=2.5)]
+    s = summarize(recs)
+    assert s.step == 7 and s.alive_peers == 2 and s.samples == 16
+    assert abs(s.loss - 2.0) < 1e-12 and abs(s.performance - 12.5) < 1e-12
+    assert s.as_record()["alive peers"] == 2
+    assert summarize([]) is None
+
+
+def test_preprocess_batch_filters_and_decodes():
+    import numpy as np
+
+    from data import preprocess_batch
+
+    class Tok:
+        def __call__(self, texts, add_special_tokens, max_length, truncation):
+            assert add_special_tokens is False and truncation
+            ids = [[len(t)] * min(len(t), max_length) for t in texts]
+            return {"input_ids": ids, "attention_mask": [[1] * len(i) for i in ids]}
+
+    code = np.arange(4, dtype=np.int16).tobytes()
+    batch = {"caption": ["a cat", "no", None, "a wide one", "nsfw", "ok caption"],
+             "NSFW": ["UNLIKELY", "UNLIKELY", "UNLIKELY", "UNLIKELY", "LIKELY", "UNLIKELY"],
+             "original_width": [100, 100, 100, 500, 100, 100], "original_height": [100, 100, 100, 100, 100, 200],
+             "code": [code] * 6}
+    out = preprocess_batch(batch, Tok(), 3)
+    assert out["input_ids"] == [[5, 5, 5], [10, 10, 10]]  # "a cat", "ok caption" (aspect exactly 2 is kept)
+    assert len(out["image"]) == 2 and out["image"][0].dtype == np.int64 and list(out["image"][1]) == [0, 1, 2, 3]
+    empty = preprocess_batch({k: v[1:3] for k, v in batch.items()}, Tok(), 3)
+    assert empty == {"input_ids": [], "attention_mask": [], "image": []}
