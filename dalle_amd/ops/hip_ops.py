@@ -19,6 +19,13 @@ from ..models.rotary import rotary_tables
 
 _C = None
 
+# how often each fused path ran (tests assert that the fast paths -- not a fallback -- were exercised)
+PATH_COUNTS: Dict[str, int] = {}
+
+
+def _count(path: str):
+    PATH_COUNTS[path] = PATH_COUNTS.get(path, 0) + 1
+
 
 class _SyncedExtension:
     """``DALLE_AMD_DEBUG_SYNC=1``: every native op is followed by a device synchronisation,
@@ -423,6 +430,7 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
         # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
         q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
+        _count("qkv_rope")
     else:
         qkv = torch.mm(h2, wq.t()).view(B, n, -1)
         q, k, v = C().rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
@@ -483,6 +491,7 @@ def _ff_core_bwd(saved, params, dy, sk):
     if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
         da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
+        _count("ff_dgrad_geglu")
         dw2 = _wgrad(w2, dy, u)
     else:
         du = torch.mm(dy, w2b)
@@ -598,6 +607,7 @@ class _FFSublayer(torch.autograd.Function):
 class _ReversibleFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blocks, recompute, *params):
+        _count("reversible_stack")
         x1 = x2 = x.contiguous()
         stored = None if recompute else []
         with torch.no_grad():
@@ -695,6 +705,7 @@ def _ln_meta(kind, args):
 class _SequentialFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, subs, *params):
+        _count("sequential_stack")
         x = x.contiguous()
         saved_all = []
         kind, args, prm = subs[0]

@@ -217,3 +217,43 @@ def test_fused_lamb_restore_before_first_step(cuda):
     opt2.step()
     assert opt2._fused
     assert torch.equal(arena2.data, ref)
+
+
+@pytest.mark.parametrize("reversible", [False, True])
+def test_reference_geometry_end_to_end(cuda, reversible):
+    """The bench / reference geometry (d=1024, 16 heads, 256 text + 32x32 image tokens, the attention /
+    sharing cycle of the recipe) with the flat arena attached, B=2 (M = 2560 = 10 x 256), so every fused
+    path runs: QKV GEMM + rotary epilogue, FF dgrad + GEGLU-backward epilogue, the fused sequential /
+    reversible stack. Loss and EVERY arena gradient vs the fp32 PyTorch model on the CPU."""
+    from dalle_amd.config import DALLEConfig, reference_attn_types, reference_shared_ids
+    from dalle_amd.data.synthetic import synthetic_batch
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = DALLEConfig(depth=4, attn_types=reference_attn_types(4), shared_attn_ids=reference_shared_ids(4),
+                      shared_ff_ids=reference_shared_ids(4), reversible=reversible)
+    assert cfg.dim == 1024 and cfg.text_len == 257 and cfg.image_fmap_size == 32
+    m_ref = DALLE(cfg)
+    m_hip = copy.deepcopy(m_ref).to(cuda)
+    arena = FlatArena(m_hip.parameters(), device=cuda)
+    b = synthetic_batch(2, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens, cfg.num_image_tokens,
+                        torch.Generator().manual_seed(3))
+    hip_ops.PATH_COUNTS.clear()
+    loss = m_hip(b["input_ids"].to(cuda), b["image"].to(cuda), mask=b["attention_mask"].to(cuda), return_loss=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    stack = "reversible_stack" if reversible else "sequential_stack"
+    for path in ("qkv_rope", "ff_dgrad_geglu", stack):
+        assert hip_ops.PATH_COUNTS.get(path, 0) > 0, (path, hip_ops.PATH_COUNTS)
+    torch.set_num_threads(16)
+    loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
+    loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 5e-3 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
+    ref = dict(m_ref.named_parameters())
+    worst = 0.0
+    for name, p in m_hip.named_parameters():
+        g, gr = p.grad.float().cpu(), ref[name].grad
+        rel = ((g - gr).norm() / (gr.norm() + 1e-12)).item()
+        worst = max(worst, rel)
+        assert rel < 0.05, (name, rel)
+    print(f"reference geometry: loss {loss.item():.5f} vs {loss_ref.item():.5f}, worst grad rel err {worst:.4f}")
