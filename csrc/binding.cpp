@@ -42,6 +42,11 @@ void splitk_accum(const float*, float*, long, int, int, hipStream_t);
 void psgd_orthonormalize(float*, const long*, const int*, int, int, float, hipStream_t);
 bool psgd_reconstruct(float*, float*, const float*, const float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
+void embed_fwd(const int64_t*, const int64_t*, const float*, float*, int*, int*, int, int, int, int, int, int, int, int,
+               hipStream_t);
+bool xent_colsum(void*, const int64_t*, float*, float*, long, int, float, hipStream_t);
+long xent_colsum_blocks(long);
+void embed_bwd(const float*, const int*, const int*, const int*, float*, float*, int, int, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
                      hipStream_t);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
@@ -593,6 +598,56 @@ Tensor nonfinite(Tensor x) {
   return flag;
 }
 
+// K1 + K2: token ids (BOS, unique pad ids, offset image codes) and the gather of their rows of the
+// fp32 table into the fp32 residual stream. Returns {tokens (B, n, d), ids (B*n) int32, bad flag}.
+std::vector<Tensor> embed_fwd(Tensor text, Tensor image, Tensor table, int64_t pad_base, int64_t Vt) {
+  CHECK_IN(text, torch::kInt64); CHECK_IN(image, torch::kInt64); CHECK_IN(table, torch::kFloat32);
+  TORCH_CHECK(text.dim() == 2 && image.dim() == 2 && table.dim() == 2, "embed_fwd: text (B, T), image (B, I), table (V, d)");
+  const int B = text.size(0), Ttxt = text.size(1), Timg = image.size(1), V = table.size(0), d = table.size(1);
+  TORCH_CHECK(image.size(0) == B || Timg == 0, "embed_fwd: batch mismatch");
+  TORCH_CHECK(d % 4 == 0, "embed_fwd: d must be a multiple of 4");
+  TORCH_CHECK(pad_base >= 0 && pad_base + Ttxt <= V && Vt >= 0 && Vt <= V, "embed_fwd: id ranges exceed the table");
+  const int n = Timg > 0 ? Ttxt + Timg : Ttxt + 1;  // BOS + text + image, the last image token dropped
+  auto out = torch::empty({B, n, d}, table.options());
+  auto ids = torch::empty({(long)B * n}, table.options().dtype(torch::kInt32));
+  auto bad = torch::zeros({1}, table.options().dtype(torch::kInt32));
+  if (B * n > 0)
+    dalle::embed_fwd(text.data_ptr<int64_t>(), image.data_ptr<int64_t>(), table.data_ptr<float>(), out.data_ptr<float>(),
+                     ids.data_ptr<int>(), bad.data_ptr<int>(), B, n, Ttxt, Timg, d, (int)pad_base, (int)Vt, V, cur_stream());
+  return {out, ids, bad};
+}
+
+// grad[sorted_ids[r]] += sum of dout rows order[...] over each run of equal ids (deterministic order).
+// order / sorted_ids / head come from a stable sort of the forward's ids (values < N, < V, < N).
+void embed_bwd_(Tensor dout, Tensor order, Tensor sorted_ids, Tensor head, Tensor grad) {
+  CHECK_IN(dout, torch::kFloat32); CHECK_IN(order, torch::kInt32); CHECK_IN(sorted_ids, torch::kInt32);
+  CHECK_IN(head, torch::kInt32); CHECK_IN(grad, torch::kFloat32);
+  TORCH_CHECK(dout.dim() == 2 && grad.dim() == 2 && dout.size(1) == grad.size(1) && dout.size(1) % 4 == 0, "embed_bwd: shapes");
+  const long N = dout.size(0);
+  TORCH_CHECK(order.numel() == N && sorted_ids.numel() == N && head.numel() == N, "embed_bwd: table sizes");
+  if (N == 0) return;
+  auto partial = torch::empty_like(dout);
+  dalle::embed_bwd(dout.data_ptr<float>(), order.data_ptr<int>(), sorted_ids.data_ptr<int>(), head.data_ptr<int>(),
+                   partial.data_ptr<float>(), grad.data_ptr<float>(), (int)N, (int)dout.size(1), cur_stream());
+}
+
+// Cross entropy + in-place dlogits + their column sums accumulated into `dbias` (fp32, += ) through
+// per-workgroup partial rows and the fixed-order column_sum reducer. Returns the per-row losses.
+Tensor xent_colsum_(Tensor logits, Tensor labels, double gscale, Tensor dbias) {
+  CHECK_IN(logits, torch::kBFloat16); CHECK_IN(labels, torch::kInt64); CHECK_IN(dbias, torch::kFloat32);
+  TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0) && dbias.numel() == logits.size(1), "xent_colsum: shapes");
+  const long R = logits.size(0);
+  const int V = logits.size(1);
+  auto loss = torch::empty({R}, logits.options().dtype(torch::kFloat32));
+  if (R == 0) return loss;
+  auto part = torch::empty({dalle::xent_colsum_blocks(R), V}, logits.options().dtype(torch::kFloat32));
+  TORCH_CHECK(dalle::xent_colsum(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), part.data_ptr<float>(),
+                                 R, V, (float)gscale, cur_stream()), "xent_colsum: vocabulary split too wide for LDS");
+  dalle::GradSink sink{dbias.data_ptr<float>(), nullptr, nullptr, V, 1};
+  dalle::column_sum(part.data_ptr<float>(), (int)part.size(0), V, sink, cur_stream());
+  return loss;
+}
+
 Tensor xent_fwd_bwd_(Tensor logits, Tensor labels, double gscale) {
   CHECK_IN(logits, torch::kBFloat16); CHECK_IN(labels, torch::kInt64);
   TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0));
@@ -794,6 +849,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("xent_colsum_", &xent_colsum_);
+  m.def("embed_bwd_", &embed_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);
   m.def("decode_rope_", &decode_rope_);
   m.def("decode_attn_", &decode_attn_);

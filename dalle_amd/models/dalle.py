@@ -272,9 +272,15 @@ class DALLE(nn.Module):
             assert self.vae is not None, "raw images need a VAE"
             image = self.vae.get_codebook_indices(image)
         ops.begin_forward()
-        tokens = self.embed(text_bos, image)
-        # fp32 residual stream, bf16 (or input dtype) compute inside the branches
-        x = tokens.float() if tokens.is_cuda else tokens
+        x = None
+        if self.cfg.share_input_output_emb and image is not None and image.numel() > 0:
+            # one HIP gather kernel for pad remap + BOS + both tied tables, straight into the fp32 stream
+            x = ops.embed_tokens(text, image, self.to_logits[1].weight, self.num_text_tokens - self.text_seq_len,
+                                 self.num_text_tokens)
+        if x is None:
+            tokens = self.embed(text_bos, image)
+            # fp32 residual stream, bf16 (or input dtype) compute inside the branches
+            x = tokens.float() if tokens.is_cuda else tokens
         out = self.transformer(x)
         norm, head = self.to_logits[0], self.to_logits[1]
         if not return_loss:

@@ -164,6 +164,13 @@ def grads_finite(buf: torch.Tensor) -> bool:
     return bool(torch.isfinite(buf).all())
 
 
+def embed_tokens(text, image, weight, pad_base: int, Vt: int):
+    """K1 + K2 on the HIP path (tied table); None on other backends (the caller gathers with F.embedding)."""
+    if text.is_cuda and backend_for(text) == "hip" and weight.dtype == torch.float32:
+        return _hip().embed_tokens(text, image, weight, pad_base, Vt)
+    return None
+
+
 def zero_grads_if_nonfinite_(buf: torch.Tensor) -> torch.Tensor:
     """Zero a flat fp32 gradient buffer iff it holds a NaN/Inf, entirely on the device (no host sync):
     the trainer's guarded ``zero_grad`` (``lib/training/hf_trainer.py:73-78``). Returns the flag tensor."""

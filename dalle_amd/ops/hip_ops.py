@@ -324,6 +324,46 @@ def linear(x, w, b=None):
 
 
 # ---------------------------------------------------------------------------------------------
+# K1 + K2: token ids + gather from the tied fp32 table; backward = deterministic segmented row sums
+# straight into the table's arena gradient (csrc/kernels/embed.hip)
+# ---------------------------------------------------------------------------------------------
+class _Embed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, text, image, weight, pad_base: int, Vt: int):
+        out, ids, bad = C().embed_fwd(text.contiguous(), image.contiguous(), weight.detach().contiguous(), int(pad_base),
+                                      int(Vt))
+        ctx.save_for_backward(ids)
+        ctx.w = weight
+        ctx.bad = bad  # device flag: an id outside the table was clamped (checked by tests / debug tools)
+        _count("embed")
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        w = ctx.w
+        g2 = g.reshape(-1, g.shape[-1]).float().contiguous()
+        sorted_ids, order = torch.sort(ids, stable=True)
+        n = ids.numel()
+        pos = torch.arange(n, device=ids.device, dtype=torch.int64)
+        start = torch.ones(n, dtype=torch.bool, device=ids.device)
+        start[1:] = sorted_ids[1:] != sorted_ids[:-1]
+        head = torch.cummax(torch.where(start, pos, torch.zeros_like(pos)), 0).values.to(torch.int32)
+        sink = grad_sink(w, ctx.needs_input_grad[2])
+        if sink is not None:
+            C().embed_bwd_(g2, order.to(torch.int32), sorted_ids.contiguous(), head, sink.view(w.shape))
+            return None, None, None, None, None
+        dw = torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+        C().embed_bwd_(g2, order.to(torch.int32), sorted_ids.contiguous(), head, dw)
+        return None, None, dw, None, None
+
+
+def embed_tokens(text, image, weight, pad_base: int, Vt: int):
+    """fp32 tokens (B, n, d) of [BOS | text (0 -> unique pad id) | image codes + Vt][:-1] from ``weight``."""
+    return _Embed.apply(text, image, weight, pad_base, Vt)
+
+
+# ---------------------------------------------------------------------------------------------
 # K3+K4: LayerNorm + token shift
 # ---------------------------------------------------------------------------------------------
 class _LNShift(torch.autograd.Function):
@@ -860,51 +900,78 @@ def scale_residual(x, y, scale):
 # K12: final LayerNorm + split-vocabulary logits + fused softmax cross entropy
 # ---------------------------------------------------------------------------------------------
 class _SplitXent(torch.autograd.Function):
+    """K12: final-LN output -> split-vocabulary logits (text rows x 32356 text columns, image rows x 8192
+    image columns: the static logits mask makes every other column -inf, so it is skipped exactly) ->
+    fused log-softmax + NLL, loss = (CE_text + w * CE_img) / (1 + w).
+
+    Logits are never materialised for the whole batch: the rows are processed in chunks of
+    ``HEAD_CHUNK_ROWS``, and each chunk's backward runs right away in the forward (the loss is the last
+    op, so its gradient is known up to the upstream scalar g): the xent kernel turns the chunk's logits
+    into dlogits in place, dh = dlogits W and dW += dlogits^T h (fp32) are computed, and the chunk's
+    logits buffer is reused. ``backward`` only scales by g: dh * g, arena dW += g * dW, db += g * db.
+    Peak head memory drops from B*n*V/2 bf16 logits (1.6 GB at B48) to one chunk."""
+
     @staticmethod
     def forward(ctx, h, w, b, labels, text_seq_len, Vt, img_w):
-        # h: (B, n, d) bf16 normed hidden; w/b fp32 master head
         B, n, d = h.shape
         wb, bb = bf16_weight(w), bf16_weight(b)
-        ht = h[:, :text_seq_len].reshape(-1, d).contiguous()
-        hi = h[:, text_seq_len:].reshape(-1, d).contiguous()
-        lt = labels[:, :text_seq_len].reshape(-1).contiguous()
-        li = (labels[:, text_seq_len:] - Vt).reshape(-1).contiguous()
-        Nt, Ni = ht.shape[0], hi.shape[0]
         den = 1.0 + img_w
-        logit_t = torch.addmm(bb[:Vt], ht, wb[:Vt].t())
-        logit_i = torch.addmm(bb[Vt:], hi, wb[Vt:].t())
-        loss_t = C().xent_fwd_bwd_(logit_t, lt, 1.0 / (den * Nt))  # logits now hold dL/dlogits
-        loss_i = C().xent_fwd_bwd_(logit_i, li, img_w / (den * Ni))
-        loss = (loss_t.mean() + img_w * loss_i.mean()) / den
-        ctx.save_for_backward(ht, hi, logit_t, logit_i, wb)
-        ctx.meta = (B, n, d, text_seq_len, Vt)
+        segs = ((h[:, :text_seq_len], labels[:, :text_seq_len], 0, Vt, 1.0),
+                (h[:, text_seq_len:], labels[:, text_seq_len:] - Vt, Vt, w.shape[0], img_w))
+        eager = any(ctx.needs_input_grad[:3])  # the backward will be asked for: do its work now
+        dh = torch.empty(B, n, d, dtype=torch.bfloat16, device=h.device)
+        dW = torch.zeros(w.shape, dtype=torch.float32, device=h.device)
+        db = torch.zeros(b.shape, dtype=torch.float32, device=h.device)
+        loss = torch.zeros((), dtype=torch.float32, device=h.device)
+        col0 = 0
+        for hs, ls, v0, v1, wt in segs:
+            rows = hs.shape[1]
+            hs2 = hs.reshape(-1, d).contiguous()
+            ls2 = ls.reshape(-1).contiguous()
+            N = hs2.shape[0]
+            gscale = wt / (den * N)
+            dh_seg = dh[:, col0:col0 + rows].view(-1, d) if dh[:, col0:col0 + rows].is_contiguous() else None
+            dh_parts = []
+            for r0 in range(0, N, HEAD_CHUNK_ROWS):
+                r1 = min(N, r0 + HEAD_CHUNK_ROWS)
+                hc = hs2[r0:r1]
+                logit = torch.addmm(bb[v0:v1], hc, wb[v0:v1].t())
+                if eager:  # logit -> dL/dlogits in place, their column sums -> db (the bias gradient)
+                    lc = C().xent_colsum_(logit, ls2[r0:r1], gscale, db[v0:v1])
+                else:
+                    lc = C().xent_fwd_bwd_(logit, ls2[r0:r1], gscale)
+                loss = loss + lc.sum() * gscale
+                if eager:
+                    part = torch.mm(logit, wb[v0:v1])
+                    if dh_seg is not None:
+                        dh_seg[r0:r1].copy_(part)
+                    else:
+                        dh_parts.append(part)
+                    torch.addmm(dW[v0:v1], logit.t(), hc, out_dtype=torch.float32, out=dW[v0:v1])
+                del logit
+            if eager and dh_seg is None:
+                dh[:, col0:col0 + rows] = torch.cat(dh_parts).view(B, rows, d)
+            col0 += rows
+        ctx.save_for_backward(dh, dW, db)
         ctx.params = (w, b)
         return loss
 
     @staticmethod
     def backward(ctx, gl):
-        ht, hi, dt, di, wb = ctx.saved_tensors
-        B, n, d, tsl, Vt = ctx.meta
+        dh, dW, db = ctx.saved_tensors
         g = gl.float()
-        dh = torch.empty(B, n, d, dtype=torch.bfloat16, device=ht.device)
-        dh[:, :tsl] = (torch.mm(dt, wb[:Vt]) * g).view(B, tsl, d)
-        dh[:, tsl:] = (torch.mm(di, wb[Vt:]) * g).view(B, n - tsl, d)
         w, b = ctx.params
         gw, gb = grad_sink(w, ctx.needs_input_grad[1]), grad_sink(b, ctx.needs_input_grad[2])
-        if gw is not None and gb is not None:
-            # accumulate into the arena: the upstream scalar is folded into the (small) activations
-            gw = gw.view(wb.shape)
-            torch.addmm(gw[:Vt], dt.t(), ht * g, out_dtype=torch.float32, out=gw[:Vt])
-            torch.addmm(gw[Vt:], di.t(), hi * g, out_dtype=torch.float32, out=gw[Vt:])
-            gb[:Vt].add_(torch.sum(dt, 0, dtype=torch.float32) * g)
-            gb[Vt:].add_(torch.sum(di, 0, dtype=torch.float32) * g)
+        dh = (dh * g.to(dh.dtype)) if g.numel() else dh
+        if gw is not None and gb is not None:  # accumulate into the arena, no host read of g
+            gw.view(w.shape).addcmul_(dW, g)
+            gb.view(b.shape).addcmul_(db, g)
             return dh, None, None, None, None, None, None
-        dw = torch.empty(wb.shape, dtype=torch.float32, device=wb.device)
-        dw[:Vt] = torch.mm(dt.t(), ht, out_dtype=torch.float32)
-        dw[Vt:] = torch.mm(di.t(), hi, out_dtype=torch.float32)
-        dw.mul_(g)
-        db = torch.cat([torch.sum(dt, 0, dtype=torch.float32), torch.sum(di, 0, dtype=torch.float32)]) * g
-        return dh, dw, db, None, None, None, None
+        return dh, dW * g, db * g, None, None, None, None
+
+
+# rows of one head chunk (logits of 4096 text rows: 265 MB bf16, image rows: 67 MB)
+HEAD_CHUNK_ROWS = int(os.environ.get("DALLE_AMD_HEAD_CHUNK_ROWS", "4096"))
 
 
 def logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len: int, num_text_tokens: int, loss_img_weight: float):

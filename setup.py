@@ -26,6 +26,7 @@ hip_sources = [
     "csrc/kernels/skinny.hip",
     "csrc/kernels/sample.hip",
     "csrc/kernels/powersgd.hip",
+    "csrc/kernels/embed.hip",
     "csrc/optim/lamb.hip",
 ]
 
