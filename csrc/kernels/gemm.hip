@@ -14,6 +14,13 @@
 //
 // Epilogues (template EPI): 0 = bf16 store (+bias); further epilogues fuse the GEGLU forward /
 // backward into the FF GEMMs (see gemm_epilogue).
+//
+// Measured and rejected (profiles/r2_gemm_persistent_vs_8ph_vs_hipblaslt.jsonl): a persistent form
+// (one workgroup per CU walking the tiles, the next tile's first K-tile DMA issued before the current
+// tile's epilogue, which staged through the other buffer in two 64-row halves) was 1-7 % SLOWER than
+// this one-tile-per-workgroup kernel on every training shape and on both fused epilogues: keeping the
+// loop-invariant fragment / DMA offsets live across the epilogue pushed it past 256 VGPRs (40-56
+// spilled, reloaded once per tile), and the exposed prologue was not the bottleneck.
 #include "common.h"
 
 namespace dalle {
