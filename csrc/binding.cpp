@@ -45,6 +45,13 @@ void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void embed_fwd(const int64_t*, const int64_t*, const float*, float*, int*, int*, int, int, int, int, int, int, int, int,
                hipStream_t);
 bool xent_colsum(void*, const int64_t*, float*, float*, long, int, float, hipStream_t);
+bool conv3x3(const ConvArgs&, hipStream_t);
+bool gn_stats(const void*, float*, float*, float*, int, int, int, float, hipStream_t);
+size_t gn_part_floats(int);
+void gn_apply(const void*, const float*, const float*, const float*, const float*, void*, int, int, int, hipStream_t);
+bool conv_out(const void*, const void*, const float*, const float*, const float*, const float*, const float*, float*, int, int,
+              int, int, hipStream_t);
+void softmax_rows(const float*, void*, long, int, float, hipStream_t);
 long xent_colsum_blocks(long);
 void embed_bwd(const float*, const int*, const int*, const int*, float*, float*, int, int, hipStream_t);
 void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
@@ -648,6 +655,93 @@ Tensor xent_colsum_(Tensor logits, Tensor labels, double gscale, Tensor dbias) {
   return loss;
 }
 
+// ---------------------------------------------------------------------------------------------
+// VQGAN decoder (K20): NHWC bf16 activations
+static const float* opt_f32(const c10::optional<Tensor>& t, long n, const char* what) {
+  if (!t.has_value()) return nullptr;
+  CHECK_IN((*t), torch::kFloat32);
+  TORCH_CHECK(t->numel() == n, what, ": wrong size");
+  return t->data_ptr<float>();
+}
+
+// y (N, H, W, Cout) = conv3x3(silu(GN(x)) or x, upsampled 2x if ups) + bias (+ res)
+Tensor conv3x3(Tensor x, Tensor w, c10::optional<Tensor> bias, c10::optional<Tensor> res, c10::optional<Tensor> mean,
+               c10::optional<Tensor> rstd, c10::optional<Tensor> gamma, c10::optional<Tensor> beta, bool ups) {
+  CHECK_IN(x, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv3x3: x (N, H, W, Cin) NHWC, w (Cout, 9 * Cin)");
+  const int N = x.size(0), Hs = x.size(1), Ws = x.size(2), Cin = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(w.size(1) == 9 * Cin, "conv3x3: weight / input channels mismatch");
+  const int H = ups ? 2 * Hs : Hs, W = ups ? 2 * Ws : Ws;
+  auto y = torch::empty({N, H, W, Cout}, x.options());
+  dalle::ConvArgs a{};
+  a.x = x.data_ptr();
+  a.w = w.data_ptr();
+  a.bias = opt_f32(bias, Cout, "conv3x3 bias");
+  if (res.has_value()) {
+    CHECK_IN((*res), torch::kBFloat16);
+    TORCH_CHECK(res->numel() == (long)N * H * W * Cout, "conv3x3: residual shape");
+    a.res = res->data_ptr();
+  }
+  a.gn = mean.has_value() ? 1 : 0;
+  if (a.gn) {
+    a.mean = opt_f32(mean, (long)N * 32, "conv3x3 mean");
+    a.rstd = opt_f32(rstd, (long)N * 32, "conv3x3 rstd");
+    a.gamma = opt_f32(gamma, Cin, "conv3x3 gamma");
+    a.beta = opt_f32(beta, Cin, "conv3x3 beta");
+    TORCH_CHECK(a.rstd && a.gamma && a.beta, "conv3x3: GroupNorm needs mean, rstd, gamma, beta");
+  }
+  a.y = y.data_ptr();
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.ups = ups ? 1 : 0;
+  TORCH_CHECK(dalle::conv3x3(a, cur_stream()), "conv3x3: unsupported shape (Cin % 64, Cout % 128, H*W % 128, Cin <= 1024)");
+  return y;
+}
+
+std::vector<Tensor> gn_stats(Tensor x, double eps) {
+  CHECK_IN(x, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4, "gn_stats: x (N, H, W, C)");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto opts = x.options().dtype(torch::kFloat32);
+  auto part = torch::empty({(long)dalle::gn_part_floats(N)}, opts);
+  auto mean = torch::empty({N, 32}, opts), rstd = torch::empty({N, 32}, opts);
+  TORCH_CHECK(dalle::gn_stats(x.data_ptr(), part.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), N, HW, C,
+                              (float)eps, cur_stream()), "gn_stats: unsupported channel count");
+  return {mean, rstd};
+}
+
+Tensor gn_apply(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta) {
+  CHECK_IN(x, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 32 == 0 && x.size(3) % 8 == 0, "gn_apply: x (N, H, W, C)");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  const float* m = opt_f32(mean, (long)N * 32, "gn_apply mean");
+  const float* r = opt_f32(rstd, (long)N * 32, "gn_apply rstd");
+  const float* g = opt_f32(gamma, C, "gn_apply gamma");
+  const float* b = opt_f32(beta, C, "gn_apply beta");
+  auto y = torch::empty_like(x);
+  dalle::gn_apply(x.data_ptr(), m, r, g, b, y.data_ptr(), N, HW, C, cur_stream());
+  return y;
+}
+
+// final GN + SiLU + conv3x3 (C -> 3) + clamp / (x + 1) / 2: NCHW fp32 images; w (3, 9 * C) bf16
+Tensor conv_out(Tensor x, Tensor w, Tensor bias, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta) {
+  CHECK_IN(x, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2 && w.size(0) == 3 && w.size(1) == 9 * x.size(3), "conv_out: shapes");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  auto img = torch::empty({N, 3, H, W}, x.options().dtype(torch::kFloat32));
+  TORCH_CHECK(dalle::conv_out(x.data_ptr(), w.data_ptr(), opt_f32(bias, 3, "conv_out bias"), opt_f32(mean, (long)N * 32, "mean"),
+                              opt_f32(rstd, (long)N * 32, "rstd"), opt_f32(gamma, C, "gamma"), opt_f32(beta, C, "beta"),
+                              img.data_ptr<float>(), N, H, W, C, cur_stream()), "conv_out: C must be <= 128 and a multiple of 8");
+  return img;
+}
+
+Tensor softmax_rows(Tensor s, double scale) {
+  CHECK_IN(s, torch::kFloat32);
+  const int L = s.size(-1);
+  const long R = s.numel() / L;
+  auto p = torch::empty(s.sizes(), s.options().dtype(torch::kBFloat16));
+  if (R > 0) dalle::softmax_rows(s.data_ptr<float>(), p.data_ptr(), R, L, (float)scale, cur_stream());
+  return p;
+}
+
 Tensor xent_fwd_bwd_(Tensor logits, Tensor labels, double gscale) {
   CHECK_IN(logits, torch::kBFloat16); CHECK_IN(labels, torch::kInt64);
   TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0));
@@ -851,6 +945,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("embed_fwd", &embed_fwd);
   m.def("xent_colsum_", &xent_colsum_);
+  m.def("conv3x3", &conv3x3, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("res") = py::none(),
+        py::arg("mean") = py::none(), py::arg("rstd") = py::none(), py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
+        py::arg("ups") = false);
+  m.def("gn_stats", &gn_stats);
+  m.def("gn_apply", &gn_apply);
+  m.def("conv_out", &conv_out);
+  m.def("softmax_rows", &softmax_rows);
   m.def("embed_bwd_", &embed_bwd_);
   m.def("decode_ln_shift_", &decode_ln_shift_);
   m.def("decode_rope_", &decode_rope_);

@@ -31,6 +31,20 @@ struct ShiftGeom {
   int S;      // image side
   int shift;  // 0 = plain LayerNorm
 };
+// VQGAN decoder 3x3 convolution (conv.hip): bf16 tensors passed as void pointers (host-compiled header)
+struct ConvArgs {
+  const void* x;       // [N, Hs, Ws, Cin] NHWC (Hs = H / 2 when ups)
+  const void* w;       // [Cout, 9 * Cin] tap-major, channel-contiguous
+  const float* bias;   // [Cout] or nullptr
+  const void* res;     // [N, H, W, Cout] or nullptr
+  void* y;             // [N, H, W, Cout]
+  const float* mean;   // [N, 32] GroupNorm statistics (gn)
+  const float* rstd;   // [N, 32]
+  const float* gamma;  // [Cin]
+  const float* beta;   // [Cin]
+  int N, H, W, Cin, Cout, ups, gn;
+};
+
 // Destination of a column-reduced parameter gradient (see column_sum_kernel)
 struct GradSink {
   float* out0;        // columns [0, split)

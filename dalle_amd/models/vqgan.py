@@ -233,9 +233,40 @@ class VQGanVAE(nn.Module):
 
     @torch.no_grad()
     def decode(self, img_seq: torch.Tensor) -> torch.Tensor:
+        if img_seq.is_cuda and self.use_hip_decoder():
+            # K20 on the hand-written HIP kernels (models/vqgan_hip.py): NHWC bf16 from the codebook gather on
+            hip = self._hip_decoder
+            b, n = img_seq.shape
+            side = int(round(n ** 0.5))
+            cb = self._codebook_bf16()
+            z = F.embedding(img_seq.long(), cb).view(b, side, side, cb.shape[1])
+            return hip(z)
         z = self.embed_codes(img_seq)
         img = self.decoder(self.post_quant_conv(z))
         return (img.clamp(-1.0, 1.0) + 1) * 0.5
+
+    def use_hip_decoder(self) -> bool:
+        """True when the decoder runs on the HIP kernels (MI355X, supported channel layout, not disabled by
+        ``DALLE_AMD_VQGAN_TORCH=1``)."""
+        import os
+
+        if os.environ.get("DALLE_AMD_VQGAN_TORCH") == "1":
+            return False
+        if getattr(self, "_hip_decoder", None) is None:
+            from .vqgan_hip import HipDecoder, supported
+
+            if not supported(self.decoder):
+                return False
+            self._hip_decoder = HipDecoder(self.post_quant_conv, self.decoder)
+        return True
+
+    def _codebook_bf16(self) -> torch.Tensor:
+        cb = self.codebook
+        key = (cb.data_ptr(), cb._version)
+        if getattr(self, "_cb_key", None) != key:
+            self._cb_bf16 = cb.detach().to(torch.bfloat16).contiguous()
+            self._cb_key = key
+        return self._cb_bf16
 
     @torch.no_grad()
     def get_codebook_indices(self, images: torch.Tensor, gumbel_tau: float = 0.0, generator=None) -> torch.Tensor:

@@ -27,6 +27,7 @@ hip_sources = [
     "csrc/kernels/sample.hip",
     "csrc/kernels/powersgd.hip",
     "csrc/kernels/embed.hip",
+    "csrc/kernels/conv.hip",
     "csrc/optim/lamb.hip",
 ]
 

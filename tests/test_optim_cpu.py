@@ -175,3 +175,32 @@ def test_preprocess_batch_filters_and_decodes():
     assert len(out["image"]) == 2 and out["image"][0].dtype == np.int64 and list(out["image"][1]) == [0, 1, 2, 3]
     empty = preprocess_batch({k: v[1:3] for k, v in batch.items()}, Tok(), 3)
     assert empty == {"input_ids": [], "attention_mask": [], "image": []}
+
+
+def test_delegating_optimizer():
+    from dalle_amd.optim.wrapper import OptimizerWrapper
+
+    class Counting(OptimizerWrapper):
+        _own = ("inner", "steps")
+
+        def __init__(self, inner):
+            super().__init__(inner)
+            self.steps = 0
+
+        def step(self, closure=None):
+            self.steps += 1
+            return super().step(closure)
+
+    p = torch.nn.Parameter(torch.ones(3))
+    opt = Counting(torch.optim.SGD([p], lr=0.5))
+    p.grad = torch.ones(3)
+    opt.step()
+    assert opt.steps == 1 and torch.allclose(p.detach(), torch.full((3,), 0.5))
+    assert opt.param_groups[0]["lr"] == 0.5 and opt.defaults["lr"] == 0.5
+    opt.param_groups[0]["lr"] = 0.1  # protocol objects are the inner optimizer's
+    assert opt.inner.param_groups[0]["lr"] == 0.1
+    sd = opt.state_dict()
+    opt.load_state_dict(sd)
+    opt.zero_grad()
+    assert p.grad is None
+    assert "Counting(" in repr(opt)
