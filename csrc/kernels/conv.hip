@@ -174,65 +174,40 @@ __global__ __launch_bounds__(CV_THREADS, 2) void conv3x3_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// GroupNorm statistics: grid (N, GN_CHUNKS); thread t owns channel chunk t % (C / 8) of every
-// (256 / (C / 8))-th pixel of the workgroup's pixel range; partial (sum, sumsq) per group.
+// GroupNorm statistics: grid (N, GN_CHUNKS); thread t owns channel chunk t % (C / 8) (8 channels) of
+// every (256 / (C / 8))-th pixel of the workgroup's pixel range and keeps per-CHANNEL partial sums;
+// the workgroup then folds them into per-group partials (any channels-per-group that divides C).
 constexpr int GN_CHUNKS = 64;
 
 __global__ __launch_bounds__(256) void gn_partial_kernel(const __bf16* __restrict__ x, float* __restrict__ part, int HW, int C) {
-  __shared__ float red[256 * 2];
+  __shared__ float red[256 * 16];
   const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
-  const int cpr = C / 8;                 // 16-byte chunks per pixel (<= 64 for C <= 512)
-  const int ppass = 256 / cpr;           // pixels per pass
+  const int cpr = C / 8;        // 16-byte chunks per pixel (<= 256)
+  const int ppass = 256 / cpr;  // pixels per pass
   const int cc = tid % cpr, pr = tid / cpr;
   const int per = (HW + GN_CHUNKS - 1) / GN_CHUNKS;
   const int p0 = chunk * per, p1 = min(HW, p0 + per);
-  float s = 0.f, q = 0.f;
-  for (int p = p0 + pr; p < p1; p += ppass) {
-    float f[8];
-    unpack8(*reinterpret_cast<const s16x8*>(x + ((size_t)n * HW + p) * C + cc * 8), f);
+  float s[8] = {}, q[8] = {};
+  if (pr < ppass) {
+    for (int p = p0 + pr; p < p1; p += ppass) {
+      float f[8];
+      unpack8(*reinterpret_cast<const s16x8*>(x + ((size_t)n * HW + p) * C + cc * 8), f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { s += f[j]; q += f[j] * f[j]; }
-  }
-  red[tid] = s;
-  red[256 + tid] = q;
-  __syncthreads();
-  // group g = channels [g * C/32, (g+1) * C/32): chunks [g * cpg, (g+1) * cpg) with cpg = cpr / 32 (>= 1 for
-  // C >= 256); for C = 128 a chunk holds two groups -- then the chunk's 8 channels are split by halves
-  if (tid < GN_GROUPS) {
-    const int g = tid;
-    const int cg = C / GN_GROUPS;  // channels per group
-    double S = 0.0, Q = 0.0;
-    if (cg >= 8) {
-      const int c_lo = g * cg / 8, c_hi = (g + 1) * cg / 8;
-      for (int r = 0; r < ppass; ++r)
-        for (int c = c_lo; c < c_hi; ++c) { S += red[r * cpr + c]; Q += red[256 + r * cpr + c]; }
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
     }
-    part[(((size_t)n * GN_CHUNKS + chunk) * GN_GROUPS + g) * 2] = (float)S;
-    part[(((size_t)n * GN_CHUNKS + chunk) * GN_GROUPS + g) * 2 + 1] = (float)Q;
   }
-}
-
-// C = 128 (4 channels per group, two groups per 16-byte chunk): per-group sums directly
-__global__ __launch_bounds__(256) void gn_partial_small_kernel(const __bf16* __restrict__ x, float* __restrict__ part, int HW, int C) {
-  __shared__ float red[256 * 4];
-  const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
-  const int cpr = C / 8, ppass = 256 / cpr;
-  const int cc = tid % cpr, pr = tid / cpr;
-  const int per = (HW + GN_CHUNKS - 1) / GN_CHUNKS;
-  const int p0 = chunk * per, p1 = min(HW, p0 + per);
-  float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
-  for (int p = p0 + pr; p < p1; p += ppass) {
-    float f[8];
-    unpack8(*reinterpret_cast<const s16x8*>(x + ((size_t)n * HW + p) * C + cc * 8), f);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { s0 += f[j]; q0 += f[j] * f[j]; s1 += f[4 + j]; q1 += f[4 + j] * f[4 + j]; }
-  }
-  red[tid * 4] = s0; red[tid * 4 + 1] = q0; red[tid * 4 + 2] = s1; red[tid * 4 + 3] = q1;
+  for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = s[j]; red[tid * 16 + 8 + j] = q[j]; }
   __syncthreads();
   if (tid < GN_GROUPS) {
-    const int g = tid, c = g >> 1, half = g & 1;  // group g = half `half` of chunk c
+    const int g = tid, cg = C / GN_GROUPS;
     double S = 0.0, Q = 0.0;
-    for (int r = 0; r < ppass; ++r) { S += red[(r * cpr + c) * 4 + 2 * half]; Q += red[(r * cpr + c) * 4 + 2 * half + 1]; }
+    for (int r = 0; r < ppass; ++r)
+      for (int c = g * cg; c < (g + 1) * cg; ++c) {
+        const int t = r * cpr + (c >> 3);
+        S += red[t * 16 + (c & 7)];
+        Q += red[t * 16 + 8 + (c & 7)];
+      }
     part[(((size_t)n * GN_CHUNKS + chunk) * GN_GROUPS + g) * 2] = (float)S;
     part[(((size_t)n * GN_CHUNKS + chunk) * GN_GROUPS + g) * 2 + 1] = (float)Q;
   }
@@ -353,12 +328,7 @@ bool conv3x3(const ConvArgs& a, hipStream_t st) {
 
 bool gn_stats(const void* x, float* part, float* mean, float* rstd, int N, int HW, int C, float eps, hipStream_t st) {
   if (C % GN_GROUPS || C % 8 || C / 8 > 256) return false;
-  if (C / GN_GROUPS >= 8)
-    hipLaunchKernelGGL(gn_partial_kernel, dim3(N, GN_CHUNKS), dim3(256), 0, st, (const __bf16*)x, part, HW, C);
-  else if (C / GN_GROUPS == 4)
-    hipLaunchKernelGGL(gn_partial_small_kernel, dim3(N, GN_CHUNKS), dim3(256), 0, st, (const __bf16*)x, part, HW, C);
-  else
-    return false;
+  hipLaunchKernelGGL(gn_partial_kernel, dim3(N, GN_CHUNKS), dim3(256), 0, st, (const __bf16*)x, part, HW, C);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((N * GN_GROUPS + 255) / 256), dim3(256), 0, st, part, mean, rstd, N, HW, C, eps);
   return true;
 }
