@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include <stdlib.h>
 #include "geom.h"
 
 namespace dalle {
@@ -515,12 +516,17 @@ __device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* 
 // phases as the forward: (A) the text key tiles, staged cooperatively two per barrier step with the
 // next pair's loads in flight; (B) each image query block streams ITS OWN local key tiles through a
 // private LDS slot (no workgroup barrier, no wave idling on the other blocks' tiles).
-template <int MINB>
+// FUSE_LOCAL (axial row / col, rotary-fused output only): an image key tile is attended by exactly one
+// query tile -- its own row's (column's) -- so that tile's dK / dV are produced right here, by the wave
+// that owns the query tile, from the K / V it already staged and the Q / dO it already holds: the
+// separate image-key dK/dV kernel (a launch that re-read Q, dO, K and V of every local tile) disappears.
+template <int MINB, bool FUSE_LOCAL>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
                                                              __bf16* __restrict__ dQ, AttnGeom g, RopeOut ro) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
+  __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   int grp, bh;
   xcd_remap(grp, bh);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
@@ -608,6 +614,71 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
       dq_tile(dq0, dq1, P, P + TILE, t, qf, dof, lq, dl, g, qb, qs, lane);
       __builtin_amdgcn_wave_barrier();
     }
+  }
+  if (FUSE_LOCAL && active && qb >= ntext && ro.dqkv) {
+    // key-centric pass over the diagonal tile: K / V rows of the tile's keys (lane = key) from the slot,
+    // then the slot is refilled with this wave's Q / dO tile (lane = query row) and the row stats
+    __bf16* P = smem + wave * (2 * TILE);
+    const int c32 = lane & 31;
+    bf16x8 kf[4], vf[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      kf[s2] = ld16(P + lds_idx(c32, 16 * s2 + 8 * hl));
+      vf[s2] = ld16(P + TILE + lds_idx(c32, 16 * s2 + 8 * hl));
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is read before it is rewritten
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      *reinterpret_cast<bf16x8*>(P + lds_idx(c32, 16 * s2 + 8 * hl)) = qf[s2];
+      *reinterpret_cast<bf16x8*>(P + TILE + lds_idx(c32, 16 * s2 + 8 * hl)) = dof[s2];
+    }
+    if (hl == 0) {
+      fstats[FUSE_LOCAL ? wave : 0][0][c32] = lq;
+      fstats[FUSE_LOCAL ? wave : 0][1][c32] = dl;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    const float(*st)[32] = fstats[FUSE_LOCAL ? wave : 0];
+    const int ks = qb * 32 + c32;
+    f32x16 sc = {}, dp = {};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      sc = MFMA32(row_operand(P, s2, c32, hl), kf[s2], sc);
+      dp = MFMA32(row_operand(P + TILE, s2, c32, hl), vf[s2], dp);
+    }
+    f32x16 ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = acc_row(r, hl);
+      const float pr = fast_exp2(fmaf(sc[r], LOG2E, -st[0][ql]));
+      sc[r] = pr;
+      ds[r] = pr * (dp[r] - st[1][ql]);
+    }
+    const uint32_t mh = query_mask(g, ks, qb) >> (4 * hl);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool on = mask_bit(mh, r);
+      sc[r] = on ? sc[r] : 0.f;
+      ds[r] = on ? ds[r] : 0.f;
+    }
+    const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
+    const bf16x8 e0 = cvt8(ds, 0), e1 = cvt8(ds, 8);
+    f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+    dv0 = MFMA32(tr_operand(P + TILE, 0, 0, lane), p0, dv0);
+    dv0 = MFMA32(tr_operand(P + TILE, 1, 0, lane), p1, dv0);
+    dv1 = MFMA32(tr_operand(P + TILE, 0, 1, lane), p0, dv1);
+    dv1 = MFMA32(tr_operand(P + TILE, 1, 1, lane), p1, dv1);
+    dk0 = MFMA32(tr_operand(P, 0, 0, lane), e0, dk0);
+    dk0 = MFMA32(tr_operand(P, 1, 0, lane), e1, dk0);
+    dk1 = MFMA32(tr_operand(P, 0, 1, lane), e0, dk1);
+    dk1 = MFMA32(tr_operand(P, 1, 1, lane), e1, dk1);
+    // the MFMAs consumed the slot's operands: it now stages this wave's dK / dV stores
+    float* stage = reinterpret_cast<float*>(P);
+    rope_bwd_store_half(ro, g, bh, qb * 32, 1, 0, dk0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, qb * 32, 1, 1, dk1, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, qb * 32, 2, 0, dv0, 1.0f, stage, lane);
+    rope_bwd_store_half(ro, g, bh, qb * 32, 2, 1, dv1, 1.0f, stage, lane);
   }
   // the epilogue's per-wave staging slot (4 KB at wave * 4 KB) overlaps other waves' phase-B slots
   __syncthreads();
@@ -959,14 +1030,30 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st, (const __bf16*)dout,
                      (const __bf16*)out, (__bf16*)do_st, delta, g, BH);
   dim3 grid((g.Np / 32 + 3) / 4, BH);
-  ATTN_LAUNCH(attn_bwd_dq_kernel, 1, grid, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)do_st,
-              lse, delta, (__bf16*)dq, g, ro);
+  // axial row / col: every image key tile is attended by exactly its own query tile -> dK / dV of the
+  // image keys inside the dQ kernel (rotary-fused output path; DALLE_AMD_ATTN_FUSE_LOCAL=0 disables)
+  const char* fl = getenv("DALLE_AMD_ATTN_FUSE_LOCAL");
+  const bool fuse_local = dqkv != nullptr && (g.pattern == 1 || g.pattern == 2) && !(fl && fl[0] == '0');
+  if (fuse_local) {
+    if (attn_occ(1) == 3)
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                         (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                         (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+  } else if (attn_occ(1) == 3) {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+  }
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
   // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
   ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
               (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
-  // image key blocks (short, local patterns): four blocks per workgroup
-  ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+  // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
+  if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
               (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
 }
 

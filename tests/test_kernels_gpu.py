@@ -248,6 +248,35 @@ def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type, monkeypatc
     assert _rel(grads[0], grads[1]) < 8e-3, attn_type
 
 
+@pytest.mark.parametrize("S", [16, 32])
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
+def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S, monkeypatch):
+    """Axial patterns: the image keys' dK / dV computed inside the dQ kernel (default) must equal the
+    separate key-centric kernel's (DALLE_AMD_ATTN_FUSE_LOCAL=0), and both the fp32 reference."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(5)
+    T, B, H = 65, 2, 2
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
+    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DALLE_AMD_ATTN_FUSE_LOCAL", flag)
+        x = qkv.clone().requires_grad_(True)
+        hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+        torch.cuda.synchronize()
+        grads.append(x.grad.float())
+    assert torch.isfinite(grads[0]).all()
+    assert _rel(grads[0], grads[1]) < 1e-6, attn_type
+    xr = qkv.float().requires_grad_(True)
+    cos, sin = rotary_tables(T, S, 64, device=cuda)
+    q, k, v = ref.qkv_rotary(xr, H, cos, sin)
+    ref.sparse_attention_core(q, k, v, geom, attn_type).backward(g.float())
+    assert _rel(grads[0], xr.grad) < 3e-2, attn_type
+
+
 def test_segmented_uniform8bit_matches_per_part(cuda):
     """One segmented launch (one workgroup per part, csrc/kernels/quant.hip) == the per-part quantiser
     (same indices up to rounding ties, same per-part codebooks), and the segmented dequantiser puts every
