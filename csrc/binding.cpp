@@ -10,7 +10,7 @@
 namespace dalle {
 
 void attn_fwd(const void*, const void*, const void*, void*, float*, const AttnGeom&, int, hipStream_t);
-void attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*, void*, void*,
+void attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
               void*, const AttnGeom&, int, hipStream_t, const float*, const float*, void*, float);
 void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
 void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
@@ -281,13 +281,12 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor do
   TORCH_CHECK(k.sizes() == q.sizes() && v.sizes() == q.sizes());
   TORCH_CHECK(out.size(0) == B && out.size(1) == n && out.size(2) == H * 64 && dout.sizes() == out.sizes());
   TORCH_CHECK(lse.numel() == B * H * g.Np);
-  auto do_st = torch::empty_like(q);
   auto delta = torch::empty({B * H, g.Np}, lse.options());
   auto dq = torch::empty_like(q);
   auto dk = torch::empty_like(q);
   auto dv = torch::empty_like(q);
   dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                  do_st.data_ptr(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), g, B * H,
+                  delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), g, B * H,
                   cur_stream(), nullptr, nullptr, nullptr, 0.f);
   return {dq, dk, dv};
 }
@@ -306,11 +305,10 @@ Tensor attn_bwd_rope(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tens
   TORCH_CHECK(lse.numel() == B * H * g.Np);
   TORCH_CHECK(cosT.dim() == 2 && cosT.size(0) >= n && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes(),
               "attn_bwd_rope: rotary tables must be (>= n, 64)");
-  auto do_st = torch::empty_like(q);
   auto delta = torch::empty({B * H, g.Np}, lse.options());
   auto dqkv = torch::empty({B, n, 3 * H * 64}, q.options());
   dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                  do_st.data_ptr(), delta.data_ptr<float>(), nullptr, nullptr, nullptr, g, B * H, cur_stream(),
+                  delta.data_ptr<float>(), nullptr, nullptr, nullptr, g, B * H, cur_stream(),
                   cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(), (float)qscale);
   return dqkv;
 }

@@ -43,6 +43,15 @@ __device__ __forceinline__ int st2seq(const AttnGeom& g, int s) {
   return p < g.n ? p : -1;
 }
 
+// 16 bytes (columns col .. col+7) of storage row s of (b, h) from a token-major [B, n, H*64] tensor
+// (the attention output / its gradient); zeros for padding rows
+__device__ __forceinline__ s16x8 ld_tok(const __bf16* __restrict__ x, const AttnGeom& g, int bh, int s, int col) {
+  const int p = st2seq(g, s);
+  if (p < 0) return s16x8{};
+  const int b = bh / g.H, h = bh - b * g.H;
+  return *reinterpret_cast<const s16x8*>(x + ((size_t)b * g.n + p) * (g.H * 64) + h * 64 + col);
+}
+
 // bits [lo, hi] of a 32-bit word (empty when hi < lo; bounds clipped to [0, 31])
 __device__ __forceinline__ uint32_t range_bits(int lo, int hi) {
   lo = max(lo, 0);
@@ -454,37 +463,6 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
 }
 
 // ------------------------------------------------------------------------------------------------
-// Backward preprocessing: dO -> storage layout, delta = rowsum(dO * O) (fp32)
-// ------------------------------------------------------------------------------------------------
-__global__ void attn_bwd_prep_kernel(const __bf16* __restrict__ dout, const __bf16* __restrict__ out,
-                                     __bf16* __restrict__ do_st, float* __restrict__ delta, AttnGeom g, int BH) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (bh, row, 8-chunk)
-  const int chunk = gid & 7;
-  const int row_g = gid >> 3;
-  if (row_g >= BH * g.Np) return;
-  const int bh = row_g / g.Np, s = row_g - bh * g.Np;
-  const int b = bh / g.H, h = bh - b * g.H;
-  const int p = st2seq(g, s);
-  s16x8 d = {};
-  float acc = 0.f;
-  if (p >= 0) {
-    const size_t off = ((size_t)b * g.n + p) * (g.H * 64) + h * 64 + chunk * 8;
-    d = *reinterpret_cast<const s16x8*>(dout + off);
-    const s16x8 o = *reinterpret_cast<const s16x8*>(out + off);
-    float fd[8], fo[8];
-    unpack8(d, fd);
-    unpack8(o, fo);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc += fd[i] * fo[i];
-  }
-  *reinterpret_cast<s16x8*>(do_st + (size_t)row_g * 64 + chunk * 8) = d;
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  if (chunk == 0) delta[row_g] = acc;
-}
-
-// ------------------------------------------------------------------------------------------------
 // Backward dQ (query-centric)
 // ------------------------------------------------------------------------------------------------
 // dS for one key tile of the wave's 32 queries -> dQ^T += K^T dS^T (S^T layout as in the forward).
@@ -522,9 +500,10 @@ __device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* 
 // separate image-key dK/dV kernel (a launch that re-read Q, dO, K and V of every local tile) disappears.
 template <int MINB, bool FUSE_LOCAL>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
-                                                             const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
-                                                             const float* __restrict__ lse, const float* __restrict__ delta,
-                                                             __bf16* __restrict__ dQ, AttnGeom g, RopeOut ro) {
+                                                             const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
+                                                             const __bf16* __restrict__ out, const float* __restrict__ lse,
+                                                             float* __restrict__ delta, __bf16* __restrict__ dQ, AttnGeom g,
+                                                             RopeOut ro) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   int grp, bh;
@@ -541,15 +520,29 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   const int my_text_end = active ? min(qb + 1, ntext) : 0;
   const int qs = qb * 32 + (lane & 31);
   const int qrow = active ? qs : 0;
+  // Q from the storage layout; dO and O gathered from the token-major tensors (the former backward
+  // prologue pass is folded in here): delta = rowsum(dO * O) of the wave's rows, published for the
+  // dK/dV kernels that run next on the stream
   bf16x8 qf[4], dof[4];
+  float dl = 0.f;
   {
     const __bf16* qp = Q + base + (size_t)qrow * 64 + 8 * hl;
-    const __bf16* dp = dO + base + (size_t)qrow * 64 + 8 * hl;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) { qf[s] = ld16(qp + 16 * s); dof[s] = ld16(dp + 16 * s); }
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = ld16(qp + 16 * s);
+      const s16x8 d = ld_tok(dout, g, bh, qrow, 16 * s + 8 * hl);
+      const s16x8 o = ld_tok(out, g, bh, qrow, 16 * s + 8 * hl);
+      float fd[8], fo[8];
+      unpack8(d, fd);
+      unpack8(o, fo);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dl = fmaf(fd[i], fo[i], dl);
+      dof[s] = __builtin_bit_cast(bf16x8, d);
+    }
+    dl += __shfl_xor(dl, 32, 64);
+    if (active && hl == 0) delta[(size_t)bh * g.Np + qrow] = dl;
   }
   const float lq = lse[(size_t)bh * g.Np + qrow];
-  const float dl = delta[(size_t)bh * g.Np + qrow];
   f32x16 dq0 = {}, dq1 = {};
 
   // ---- phase A: shared text tiles, two per step ----
@@ -713,7 +706,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
 // ------------------------------------------------------------------------------------------------
 template <int MINB>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
-                                                               const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
+                                                               const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                                const float* __restrict__ lse, const float* __restrict__ delta,
                                                                __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g,
                                                                RopeOut ro) {
@@ -745,7 +738,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
       const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
       const size_t off = base + (size_t)(qt * 32 + row) * 64 + col;
       qr[j] = *reinterpret_cast<const s16x8*>(Q + off);
-      dr[j] = *reinterpret_cast<const s16x8*>(dO + off);
+      dr[j] = ld_tok(dout, g, bh, qt * 32 + row, col);
     }
     sv = (hl ? delta : lse)[(size_t)bh * g.Np + qt * 32 + c32];
   };
@@ -833,7 +826,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
 // ------------------------------------------------------------------------------------------------
 template <int MINB>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
-                                                                    const __bf16* __restrict__ V, const __bf16* __restrict__ dO,
+                                                                    const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                                     __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g,
                                                                     RopeOut ro) {
@@ -870,7 +863,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
       const int qt = min(kb0 + 2 * i + pp, nqb - 1);
       const size_t off = base + (size_t)(qt * 32 + st_row) * 64 + st_col;
       sreg[2 * pp] = *reinterpret_cast<const s16x8*>(Q + off);
-      sreg[2 * pp + 1] = *reinterpret_cast<const s16x8*>(dO + off);
+      sreg[2 * pp + 1] = ld_tok(dout, g, bh, qt * 32 + st_row, st_col);
     }
     if (tid < 128) {  // lse / delta rows of both tiles: 2 parities x 2 stats x 32
       const int pp = tid >> 6, which = (tid >> 5) & 1, r = tid & 31;
@@ -1023,12 +1016,9 @@ void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse
 }
 
 void attn_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
-              void* do_st, float* delta, void* dq, void* dk, void* dv, const AttnGeom& g, int BH, hipStream_t st,
+              float* delta, void* dq, void* dk, void* dv, const AttnGeom& g, int BH, hipStream_t st,
               const float* cosT, const float* sinT, void* dqkv, float qscale) {
   const RopeOut ro{cosT, sinT, static_cast<__bf16*>(dqkv), qscale};
-  const int rows = BH * g.Np;
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st, (const __bf16*)dout,
-                     (const __bf16*)out, (__bf16*)do_st, delta, g, BH);
   dim3 grid((g.Np / 32 + 3) / 4, BH);
   // axial row / col: every image key tile is attended by exactly its own query tile -> dK / dV of the
   // image keys inside the dQ kernel (rotary-fused output path; DALLE_AMD_ATTN_FUSE_LOCAL=0 disables)
@@ -1037,24 +1027,24 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   if (fuse_local) {
     if (attn_occ(1) == 3)
       hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
     else
       hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
   } else if (attn_occ(1) == 3) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
   } else {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dq, g, ro);
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
   }
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
   // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
   ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
-              (const __bf16*)v, (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+              (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
   // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
   if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-              (const __bf16*)do_st, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+              (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
 }
 
 }  // namespace dalle
