@@ -47,6 +47,15 @@ def wgrad_sweep(M):
                 part = torch.bmm(g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
                 C.splitk_accum_(acc, part, True)
             res[f"s{s}_TF"] = round(fl / timeit(f) / 1e9)
+        # hand-written MN-major MFMA kernel (gemm_wgrad_), every split count that tiles the tokens
+        ref = g.float().t() @ x.float()
+        for s in (1, 2, 4, 5, 8, 16):
+            if M % (64 * s):
+                continue
+            out = torch.zeros(N, K, device=dev)
+            C.gemm_wgrad_(g, x, out, s, True)
+            res[f"own_s{s}_relerr"] = float((out - ref).norm() / ref.norm())
+            res[f"own_s{s}_TF"] = round(fl / timeit(lambda s=s: C.gemm_wgrad_(g, x, acc, s, True)) / 1e9)
         print(json.dumps(res), flush=True)
 
 

@@ -27,6 +27,7 @@ void scale_residual_bwd(const float*, const void*, const float*, void*, float*, 
 void nonfinite(const float*, long, int*, hipStream_t);
 void zero_if_flag(float*, long, const int*, hipStream_t);
 bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
+bool gemm_wgrad(const void*, const void*, float*, float*, int, int, int, int, int, hipStream_t);
 void uq8_compress(const float*, long, uint8_t*, float*, void*, hipStream_t);
 size_t uq8_workspace_bytes();
 void uq8_dequant(const uint8_t*, const float*, float*, long, float, int, hipStream_t);
@@ -441,6 +442,21 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
   auto C = torch::empty({M, N}, A.options());
   TORCH_CHECK(dalle::gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, (int)variant, cur_stream()));
   return C;
+}
+
+// dW (N, K) fp32 (+)= G^T X: G (M, N), X (M, K) bf16 row-major (tokens on the rows of both), the
+// hand-written MN-major MFMA GEMM split `splits` ways over the tokens (deterministic fold)
+void gemm_wgrad_(Tensor G, Tensor X, Tensor out, int64_t splits, bool accumulate) {
+  CHECK_IN(G, torch::kBFloat16); CHECK_IN(X, torch::kBFloat16); CHECK_IN(out, torch::kFloat32);
+  TORCH_CHECK(G.dim() == 2 && X.dim() == 2 && G.size(0) == X.size(0), "gemm_wgrad: G (M, N), X (M, K)");
+  const int M = G.size(0), N = G.size(1), K = X.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == N && out.size(1) == K, "gemm_wgrad: out must be (N, K)");
+  TORCH_CHECK(N % 256 == 0 && K % 256 == 0, "gemm_wgrad: N, K multiples of 256");
+  TORCH_CHECK(splits >= 1 && M % (splits * 64) == 0, "gemm_wgrad: M must be a multiple of 64 * splits");
+  Tensor ws;
+  if (splits > 1) ws = torch::empty({splits, N, K}, out.options());
+  TORCH_CHECK(dalle::gemm_wgrad(G.data_ptr(), X.data_ptr(), out.data_ptr<float>(), splits > 1 ? ws.data_ptr<float>() : nullptr, M,
+                                N, K, (int)splits, accumulate ? 1 : 0, cur_stream()));
 }
 
 // ---- decode-step skinny GEMMs (M <= 64): one launch each, epilogue fused ----
@@ -940,6 +956,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zero_if_nonfinite_", &zero_if_nonfinite_);
   m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
+  m.def("gemm_wgrad_", &gemm_wgrad_, py::arg("G"), py::arg("X"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("embed_fwd", &embed_fwd);
   m.def("xent_colsum_", &xent_colsum_);

@@ -189,6 +189,9 @@ struct RopeEpi {
   __bf16* gdh;
   float* gpart;
   int F;
+  // EPI 3 / 4 (weight gradients, MN-major operands): fp32 tile stored into slab blockIdx.y of fout
+  // (3) or accumulated into fout (4)
+  float* fout;
 };
 
 __device__ __forceinline__ int rope_epi_seq2st(const RopeEpi& e, int p) {
@@ -229,6 +232,48 @@ __device__ __forceinline__ void stage_half(const __bf16* __restrict__ src, int l
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
                                      (void __attribute__((address_space(3)))*)(lds_half + piece * 512), 16, 0, 0);
   }
+}
+
+// ---- MN-major operands (weight gradients: dW[N, K] = G^T X with G (tokens, N), X (tokens, K) both
+// row-major, the reduction running over tokens = the slow axis of both) ----
+// A half-tile image is 64 tokens x 128 columns (256 B rows). Fragments are read with
+// ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses token row q, columns 4p..4p+3 and
+// receives its own column's 4 consecutive tokens, i.e. exactly an MFMA operand fragment (M / N index
+// on the lane, tokens along K). The 16-byte chunk index is XOR-swizzled by token row so the 4 rows x
+// 2 chunks of a 16-lane group, and the two groups of a half-wave (rows 8 apart), hit 16 distinct
+// 16-byte bank groups.
+__device__ __forceinline__ int mn_swz(int t) { return ((t & 3) << 1) | (((t >> 3) & 1) << 3); }
+
+// In MN mode a half-tile is 128 CONTIGUOUS tile columns (off = 0 or 128: 256 B per token row), so
+// the waves' output columns interleave accordingly (see the EPI 3 / 4 store): wave (wm, wn) owns
+// rows {wm*64 + 0..63, 128 + wm*64 + 0..63} and columns {wn*32 + 0..31, 128 + wn*32 + 0..31}.
+__device__ __forceinline__ void stage_half_mn(const __bf16* __restrict__ src, int ld, int col0, int t0, __bf16* lds_half,
+                                              int wave, int lane, int off) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;           // 0..15: token rows 4*piece .. 4*piece+3
+    const int tr = piece * 4 + (lane >> 4);   // this lane's token row in the image
+    const int lchunk = (lane & 15) ^ mn_swz(tr);
+    const __bf16* g = src + (size_t)(t0 + tr) * ld + col0 + off + lchunk * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                     (void __attribute__((address_space(3)))*)(lds_half + piece * 512), 16, 0, 0);
+  }
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+
+__device__ __forceinline__ bf16x8 frag_mn(const __bf16* img, int c_img, int kk, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int t1 = kk * 32 + g * 8 + q, t2 = t1 + 4;
+  const int chunk = (c_img >> 3) + (p >> 1), sub = (p & 1) * 4;
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(img + t1 * 128 + ((chunk ^ mn_swz(t1)) << 3) + sub));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(img + t2 * 128 + ((chunk ^ mn_swz(t2)) << 3) + sub));
+  s16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // Shared epilogue of the phased kernels: stage each wave's 128 x 64 accumulator tile (bf16) through
@@ -477,12 +522,18 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_phased_kernel(const __bf
 //     so K-tile t+1 is complete for every wave before any wave's phase-5 reads (RAW), even for the
 //     lagging wave row.
 // ------------------------------------------------------------------------------------------------
-template <int EPI, int OPT>
+// MN = 1: MN-major operands (see stage_half_mn): A = G (tokens, M), B = X (tokens, N), K = tokens per
+// split; blockIdx.y selects the split (tokens [y K, (y + 1) K)).
+template <int EPI, int OPT, int MN = 0>
 __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                    __bf16* __restrict__ C, const __bf16* __restrict__ bias,
                                                                    int M, int N, int K, RopeEpi rope, int group) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];  // [buf][A-lo | B-lo | B-hi | A-hi]
   constexpr bool STAGGER = !(OPT & 1);
+  if (MN) {
+    A += (size_t)blockIdx.y * K * M;
+    B += (size_t)blockIdx.y * K * N;
+  }
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   int tm, tn;
@@ -500,10 +551,22 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
   // which: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
   auto stage = [&](int t, int which) {
     const int buf = t & 1, k0 = t * GBK;
-    if (which == 0) stage_half(A, K, row0, k0, slot(buf, 0), wave, lane, 64, 0);
-    else if (which == 1) stage_half(B, K, col0, k0, slot(buf, 1), wave, lane, 32, 0);
-    else if (which == 2) stage_half(B, K, col0, k0, slot(buf, 2), wave, lane, 32, 32);
-    else stage_half(A, K, row0, k0, slot(buf, 3), wave, lane, 64, 64);
+    if constexpr (MN) {
+      if (which == 0) stage_half_mn(A, M, row0, k0, slot(buf, 0), wave, lane, 0);
+      else if (which == 1) stage_half_mn(B, N, col0, k0, slot(buf, 1), wave, lane, 0);
+      else if (which == 2) stage_half_mn(B, N, col0, k0, slot(buf, 2), wave, lane, 128);
+      else stage_half_mn(A, M, row0, k0, slot(buf, 3), wave, lane, 128);
+    } else {
+      if (which == 0) stage_half(A, K, row0, k0, slot(buf, 0), wave, lane, 64, 0);
+      else if (which == 1) stage_half(B, K, col0, k0, slot(buf, 1), wave, lane, 32, 0);
+      else if (which == 2) stage_half(B, K, col0, k0, slot(buf, 2), wave, lane, 32, 32);
+      else stage_half(A, K, row0, k0, slot(buf, 3), wave, lane, 64, 64);
+    }
+  };
+  // operand fragment: image rows (NT) / image columns (MN) r0 .. r0+15, k-half kk
+  auto frag = [&](const __bf16* img, int r0, int kk) {
+    if constexpr (MN) return frag_mn(img, r0, kk, lane);
+    else return gemm_frag(img, r0 + fr, kk * 4 + fq);
   };
 
   const int nk = K / GBK;
@@ -530,14 +593,16 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b0[j][kk] = gemm_frag(Blo, wn * 32 + j * 16 + fr, kk * 4 + fq);
+      for (int kk = 0; kk < 2; ++kk) b0[j][kk] = frag(Blo, wn * 32 + j * 16, kk);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Alo, wm * 64 + i * 16 + fr, kk * 4 + fq);
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag(Alo, wm * 64 + i * 16, kk);
     if (s1) stage(t + 1, 3);
-    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the 4 B reads (issued first) have retired
+    // the B reads (issued first: 4 fragments, 8 tr-reads in MN mode) have retired
+    if constexpr (MN) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -555,7 +620,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b1[j][kk] = gemm_frag(Bhi, wn * 32 + j * 16 + fr, kk * 4 + fq);
+      for (int kk = 0; kk < 2; ++kk) b1[j][kk] = frag(Bhi, wn * 32 + j * 16, kk);
     if (s2) stage(t + 2, 1);
     asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -575,7 +640,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = gemm_frag(Ahi, wm * 64 + i * 16 + fr, kk * 4 + fq);
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag(Ahi, wm * 64 + i * 16, kk);
     if (s2) stage(t + 2, 0);
     asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -613,7 +678,24 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
   if (STAGGER && wm == 0) asm volatile("s_barrier" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  gemm_store_epilogue<EPI>(acc, smem, C, bias, N, row0, col0, wave, lane, rope);
+  if constexpr (EPI == 3 || EPI == 4) {
+    // fp32 tile straight from the accumulators: 16 lanes store 16 consecutive floats of a row
+    float* Cf = rope.fout + (EPI == 3 ? (size_t)blockIdx.y * M * N : 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = (i < 4 ? wm * 64 + i * 16 : 128 + wm * 64 + (i - 4) * 16) + fq * 4 + r;
+          const int cc = (j < 2 ? wn * 32 + j * 16 : 128 + wn * 32 + (j - 2) * 16) + fr;
+          float* dst = Cf + (size_t)(row0 + rr) * N + col0 + cc;
+          if (EPI == 3) *dst = acc[i][j][r];
+          else *dst += acc[i][j][r];
+        }
+  } else {
+    gemm_store_epilogue<EPI>(acc, smem, C, bias, N, row0, col0, wave, lane, rope);
+  }
 }
 
 // zero the storage rows that have no sequence position (text padding [T, Tp) and the last image slot)
@@ -681,6 +763,36 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   const int nwg = (M / GBM) * (F / GBN);
   hipLaunchKernelGGL((gemm_nt_8ph_kernel<2, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
                      (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);
+  return true;
+}
+
+// Weight gradient dW (N_out, K_in) fp32 = G^T X over Mtok tokens, G (Mtok, N_out) and X (Mtok, K_in)
+// bf16 row-major: the MN-major 8-phase kernel, token range split `splits` ways over blockIdx.y. One
+// split accumulates (or stores) straight into `out`; more write fp32 slabs to `ws` (splits x N x K)
+// that splitk_accum folds in split order (deterministic).
+void splitk_accum(const float* part, float* acc, long n, int s, int accumulate, hipStream_t st);
+bool gemm_wgrad(const void* G, const void* X, float* out, float* ws, int Mtok, int Nout, int Kin, int splits, int accumulate,
+                hipStream_t st) {
+  if (Nout % GBM || Kin % GBN || splits < 1 || Mtok % (splits * GBK)) return false;
+  if (splits > 1 && ws == nullptr) return false;
+  RopeEpi e{};
+  const int tiles = (Nout / GBM) * (Kin / GBN);
+  const int kt = Mtok / splits;
+  dim3 grid(tiles, splits);
+  if (splits == 1) {
+    e.fout = out;
+    if (accumulate)
+      hipLaunchKernelGGL((gemm_nt_8ph_kernel<4, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
+                         (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
+    else
+      hipLaunchKernelGGL((gemm_nt_8ph_kernel<3, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
+                         (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
+    return true;
+  }
+  e.fout = ws;
+  hipLaunchKernelGGL((gemm_nt_8ph_kernel<3, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
+                     (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
+  splitk_accum(ws, out, (long)Nout * Kin, splits, accumulate, st);
   return true;
 }
 

@@ -130,6 +130,8 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
 
 
 SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
+# weight grads on the hand-written MN-major GEMM (gemm_wgrad_) instead of hipBLASLt (opt-in, see weight_grad)
+OWN_WGRAD = int(os.environ.get("DALLE_AMD_OWN_WGRAD", "0"))
 # QKV projection through the hand-written GEMM with the rotary in its epilogue (csrc/kernels/gemm.hip)
 FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "1"))
 # rotary backward fused into the attention-backward epilogues (csrc/kernels/attention.hip RopeOut)
@@ -146,6 +148,16 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
     gw = w.grad
     fused = FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape
     M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
+    if OWN_WGRAD and N % 256 == 0 and K % 256 == 0 and g2.is_contiguous() and x2.is_contiguous():
+        # hand-written MN-major MFMA kernel; 15-20 % slower than hipBLASLt on the training shapes
+        # (profiles/r2_wgrad_mn_major_vs_hipblaslt.jsonl), so opt-in only
+        s = max(1, min(16, 256 // ((N // 256) * (K // 256))))
+        while s > 1 and M % (64 * s):
+            s -= 1
+        if M % 64 == 0:
+            out = gw if fused else torch.zeros(N, K, dtype=torch.float32, device=g2.device)
+            C().gemm_wgrad_(g2, x2, out, s, True)
+            return None if fused else out
     s = wgrad_splits(M, N, K)
     if s > 1:
         part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
