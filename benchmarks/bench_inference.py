@@ -38,9 +38,10 @@ def main():
         model.vae = VQGanVAE().to(dev).eval()
     text = torch.randint(2, cfg.num_text_tokens, (args.batch, cfg.text_seq_len), device=dev)
     use_graph = not args.no_graph
-    from dalle_amd.models.generation import DecodeEngine
-    eng = DecodeEngine(model, args.batch, device=dev)
+    from dalle_amd.models.generation import make_decode_engine
+    eng = make_decode_engine(model, args.batch, device=dev)
     model._decode_engine = eng
+    parts = getattr(eng, "nparts", 1)
     t = time.perf_counter()
     eng.prefill(model.prepare_text(text))
     torch.cuda.synchronize()
@@ -71,6 +72,11 @@ def main():
         torch.cuda.synchronize()
         print(f"# generate {i}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
     el = (time.perf_counter() - t0) / args.iters
+    # sampling alone (no VAE): the average decode step over all positions
+    t2 = time.perf_counter()
+    model.generate_images(text, top_k=args.top_k, use_graph=use_graph, return_codes=True)
+    torch.cuda.synchronize()
+    codes_s = time.perf_counter() - t2
     eng = model._decode_engine
     # decode-only timing (graph replays) from a fresh start: positions 0..63 -- never past seq_len
     eng._start(model.prepare_text(text))
@@ -87,6 +93,8 @@ def main():
     print(json.dumps({"metric": "text->image generation throughput (batch 64, top-k, hipGraph decode)",
                       "value": round(args.batch / el, 3), "unit": "images/s", "n_gpus": 1,
                       "seconds_per_batch": round(el, 3), "ms_per_decode_step": round(per_tok * 1e3, 3),
+                      "ms_per_step_all_positions": round(codes_s / cfg.seq_len * 1e3, 3),
+                      "sampling_seconds": round(codes_s, 3), "decode_parts": parts,
                       "batch": args.batch, "model": args.model, "depth": cfg.depth, "graph": use_graph,
                       "vae": not args.no_vae, "out_shape": list(out.shape), "dtype": "bf16",
                       "data": "random-init weights, synthetic captions"}), flush=True)

@@ -298,14 +298,14 @@ class DALLE(nn.Module):
                         return_codes: bool = False, use_graph=None):
         """Sample 1024 image tokens per caption with the KV-cache decoder (hipGraph-replayed on MI355X)
         and decode them with ``self.vae`` to (b, 3, H, W) images in [0, 1] (codes if no VAE)."""
-        from .generation import DecodeEngine
+        from .generation import make_decode_engine
 
         if filter_thres is not None and not top_k:
             top_k = max(1, int((1 - filter_thres) * self.num_image_tokens))
         text_bos = self.prepare_text(text)
         eng = getattr(self, "_decode_engine", None)
         if eng is None or eng.B != text.shape[0] or eng.device != text.device:
-            eng = DecodeEngine(self, text.shape[0], device=text.device)
+            eng = make_decode_engine(self, text.shape[0], device=text.device)
             self._decode_engine = eng
         codes = eng.generate(text_bos, temperature=temperature, top_k=top_k, top_p=top_p, use_graph=use_graph)
         if return_codes or self.vae is None:

@@ -91,12 +91,15 @@ class DecodeEngine:
             self._w[id(p)] = ent
         return ent[1]
 
+    _refresh_weights = True
+
     def reset(self):
         """Zero position/caches and refresh the compute-dtype weight copies IN PLACE (a captured graph
         keeps pointing at the same buffers, so weight updates between calls are still seen)."""
         self.pos.zero_()
-        for p, w in self._w.values():
-            w.copy_(p.detach().reshape(w.shape))
+        if self._refresh_weights:
+            for p, w in self._w.values():
+                w.copy_(p.detach().reshape(w.shape))
         for k in self.kc + self.vc:
             k.zero_()
 
@@ -326,3 +329,117 @@ class DecodeEngine:
                 self.tok.copy_(image[:, i] + self.Vt)
                 self.pos.add_(1)
         return torch.stack(outs, dim=1)
+
+
+class SplitDecodeEngine:
+    """The batch split into ``parts`` independent :class:`DecodeEngine` s whose steps run on separate
+    HIP streams inside ONE captured graph. At batch 64 a decode step is a chain of short kernels
+    whose time is mostly fixed latency (a skinny GEMM takes 8-10 us whether it streams 2 or 16 MB of
+    weights), so two half-batch chains interleaved on the GPU overlap one chain's latency with the
+    other's work. The parts share the bf16 weight copies; each has its own KV caches, LN histories,
+    device position and sampler seed (``seed + part``), so the parts never touch the same buffer."""
+
+    def __init__(self, model, batch_size: int, device=None, parts: int = 2):
+        if batch_size % parts:
+            raise ValueError(f"batch {batch_size} is not divisible into {parts} parts")
+        self.model, self.B, self.nparts = model, batch_size, parts
+        self.parts = [DecodeEngine(model, batch_size // parts, device=device) for _ in range(parts)]
+        for p in self.parts[1:]:
+            p._w = self.parts[0]._w  # one bf16 copy of every weight, refreshed by part 0 only
+            p._refresh_weights = False
+        self.device = self.parts[0].device
+        self.use_hip = self.parts[0].use_hip
+        self.graph = None
+        self._graph_cfg = None
+
+    @property
+    def codes(self) -> torch.Tensor:
+        return torch.cat([p.codes for p in self.parts])
+
+    def _start_all(self, text_bos: torch.Tensor):
+        b = self.B // self.nparts
+        for i, p in enumerate(self.parts):
+            p._start(text_bos[i * b:(i + 1) * b])
+
+    _start = _start_all
+
+    def _step(self):
+        for p in self.parts:
+            p._step()
+
+    _image_step = _step
+
+    @torch.no_grad()
+    def prefill(self, text_bos: torch.Tensor):
+        b = self.B // self.nparts
+        for i, p in enumerate(self.parts):
+            p.prefill(text_bos[i * b:(i + 1) * b])
+
+    def _capture(self):
+        if self.graph is not None and self._graph_cfg == (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p):
+            return
+        main = torch.cuda.current_stream()
+        streams = [torch.cuda.Stream() for _ in self.parts[1:]]
+        warm = torch.cuda.Stream()
+        warm.wait_stream(main)
+        with torch.cuda.stream(warm):
+            for _ in range(2):
+                for p in self.parts:
+                    p._step()
+        main.wait_stream(warm)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            cap = torch.cuda.current_stream()
+            for s in streams:
+                s.wait_stream(cap)
+            self.parts[0]._step()
+            for p, s in zip(self.parts[1:], streams):
+                with torch.cuda.stream(s):
+                    p._step()
+            for s in streams:
+                cap.wait_stream(s)
+        self.graph = g
+        self._streams = streams
+        self._graph_cfg = (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p)
+
+    @torch.no_grad()
+    def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                 use_graph: Optional[bool] = None, seed: Optional[int] = None) -> torch.Tensor:
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        for i, p in enumerate(self.parts):
+            p.temperature, p.top_k, p.top_p = temperature, top_k, top_p
+            p.seed.fill_(int(seed) + i)
+        use_graph = self.use_hip if use_graph is None else use_graph
+        n = self.parts[0].n
+        self._start_all(text_bos)
+        if use_graph:
+            self._capture()
+            self._start_all(text_bos)
+            for _ in range(n):
+                self.graph.replay()
+        else:
+            for _ in range(n):
+                for p in self.parts:
+                    p._step()
+        return self.codes.clone()
+
+
+def decode_parts(batch_size: int, device) -> int:
+    """How many concurrent batch-slice chains a decode engine uses: ``DALLE_AMD_DECODE_PARTS`` (default
+    1). Measured on the reference model at batch 64 (profiles/r2_decode_split_parts.txt): 2 parts
+    3.96 ms per position vs 4.01 for one chain, 4 parts 6.43 -- the half-batch chains do overlap (a
+    batch-32 chain alone takes 3.16 ms), but each skinny-GEMM workgroup occupies a whole CU, so two
+    concurrent kernels mostly run one after the other at CU granularity."""
+    n = max(1, int(os.environ.get("DALLE_AMD_DECODE_PARTS", "1")))
+    return n if batch_size % n == 0 else 1
+
+
+def make_decode_engine(model, batch_size: int, device=None):
+    device = device or next(model.parameters()).device
+    parts = decode_parts(batch_size, device)
+    if parts > 1:
+        eng = SplitDecodeEngine(model, batch_size, device=device, parts=parts)
+        if eng.use_hip:
+            return eng
+    return DecodeEngine(model, batch_size, device=device)

@@ -4,6 +4,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/r2_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r2_pytest.log; exit 1; }
 tail -1 gpurun_out/r2_pytest.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r2_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/r2_smoke.log; exit 1; }
+echo smoke ok
 timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 > gpurun_out/r2_bench_step.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/r2_bench_step.log; exit 1; }
 grep '^{' gpurun_out/r2_bench_step.log | cut -c1-400
 timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --engine collab > gpurun_out/r2_bench_collab.log 2>&1 || { echo "bench collab failed"; tail -20 gpurun_out/r2_bench_collab.log; exit 1; }

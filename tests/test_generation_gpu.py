@@ -48,6 +48,29 @@ def test_graph_replay_matches_eager(cuda):
     assert torch.equal(eager, graph)
 
 
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_split_decode_engine_matches_single(cuda, use_graph):
+    """Two half-batch chains on separate streams (one captured graph) == one full-batch engine under
+    greedy sampling (top-k 1: the sampler's noise, which differs per part, cannot change the pick)."""
+    from dalle_amd.models.generation import SplitDecodeEngine
+
+    torch.manual_seed(0)
+    cfg = _cfg(False)
+    m = DALLE(cfg).eval().to(cuda)
+    B = 4
+    text = torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len), device=cuda)
+    tb = m.prepare_text(text)
+    single = DecodeEngine(m, B, device=cuda).generate(tb, top_k=1, use_graph=use_graph, seed=5)
+    split = SplitDecodeEngine(m, B, device=cuda, parts=2)
+    assert len(split.parts) == 2 and split.parts[1]._w is split.parts[0]._w
+    got = split.generate(tb, top_k=1, use_graph=use_graph, seed=5)
+    assert got.shape == single.shape
+    assert (got == single).float().mean().item() > 0.98
+    # a second call reuses the captured graph and the shared weights
+    again = split.generate(tb, top_k=1, use_graph=use_graph, seed=7)
+    assert torch.equal(again, got)
+
+
 def test_vq_embed_kernel(cuda):
     vae = VQGanVAE(n_embed=64, embed_dim=32, ddconfig=dict(ch=32, out_ch=3, ch_mult=(1, 2), num_res_blocks=1,
                                                            attn_resolutions=(8,), resolution=16, z_channels=32)).to(cuda)
