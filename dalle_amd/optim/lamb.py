@@ -25,8 +25,11 @@ from typing import Optional
 
 import torch
 
+from ..utils.logging import get_logger
 from . import quant
 from .flat import FlatArena
+
+_logger = get_logger(__name__)
 
 
 class LAMB8bit(torch.optim.Optimizer):
@@ -146,7 +149,11 @@ class LAMB8bit(torch.optim.Optimizer):
             from .fused import FusedLambEngine
             self._fused = FusedLambEngine.maybe_create(self) or False
             if self._fused is False:
+                if any(p.is_cuda for g in self.param_groups for p in g["params"]):
+                    _logger.info("LAMB: per-tensor PyTorch path (parameters outside a flat arena)")
                 return None
+            _logger.info(f"LAMB: fused HIP engine over the flat arena ({self.defaults['optim_bits']}-bit state, "
+                         f"{self._fused.state_bytes() / 2 ** 20:.1f} MiB)")
         return self._fused
 
     @torch.no_grad()

@@ -51,6 +51,9 @@ def test_single_peer_rccl(cuda, tmp_path):
     epochs = [int(m) for m in re.findall(r"epoch (\d+): contributed", out)]
     assert epochs and max(epochs) >= 5, out[-3000:]
     assert "cuda" in out
+    # the delayed step runs LAMB over the master copies: the fused HIP engine, never the per-tensor path
+    assert "LAMB: fused HIP engine over the flat arena" in out, out[-3000:]
+    assert "per-tensor PyTorch path" not in out
 
 
 def test_two_peers_share_the_gpu_over_gloo(cuda, tmp_path):
