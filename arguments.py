@@ -57,8 +57,9 @@ class HFTrainerArguments:
 
     # --- engine-only flags
     model_preset: str = flag("reference", "engine only: dalle_amd.config preset (reference, bench24, tiny, dalle-1.3b)")
-    reversible_recompute: bool = flag(True, "engine only: reversible blocks rebuild activations in backward (False: "
-                                            "keep them; ~30% faster for the 64-layer recipe, ~4 GB per sample of HBM)")
+    reversible_recompute: str = flag("auto", "engine only: reversible blocks rebuild activations in backward (true), "
+                                           "keep them (false: ~30% faster for the 64-layer recipe, ~4 GB per sample "
+                                           "of HBM) or keep as many blocks as the free HBM holds (auto)")
     dataset_path: Optional[str] = flag(None, "engine only: directory of LAION-VQGAN parquet/jsonl shards (default: synthetic)")
     optimizer_bits: int = flag(8, "engine only: LAMB moment storage, 8 (CPULAMB8Bit layout) or 32")
     grad_averaging: str = flag("size_adaptive", "engine only: none | fp16 | 8bit | size_adaptive | powersgd")

@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--trace", default="", help="chrome trace path for the --profile-steps pass")
     ap.add_argument("--no-recompute", action="store_true",
                     help="reversible presets: keep the activations instead of rebuilding them in backward")
+    ap.add_argument("--recompute", default=None, choices=["true", "false", "auto"],
+                    help="reversible presets: rebuild activations in backward (true, the reference regime), keep them "
+                         "(false) or keep as many blocks as the free HBM holds (auto)")
     ap.add_argument("--tunable", default="off", choices=["auto", "use", "tune", "off"],
                     help="hipBLASLt solution selection for the library GEMMs (dalle_amd/utils/tuning.py)")
     return ap.parse_args()
@@ -180,6 +183,8 @@ def run_rank(args) -> None:
     cfg = get_config(args.model)
     if args.no_recompute:
         cfg.reversible_recompute = False
+    if args.recompute is not None:
+        cfg.reversible_recompute = "auto" if args.recompute == "auto" else args.recompute == "true"
     bits = args.optim_bits if args.optim_bits is not None else (8 if args.engine == "collab" else 32)
     torch.manual_seed(1234)
     model = DALLE(cfg).to(device)
@@ -313,7 +318,8 @@ def run_rank(args) -> None:
                        "engine": "CollaborativeOptimizer.step" if args.engine == "collab" else "GradSync + fused LAMB",
                        "optimizer": f"LAMB ({bits}-bit moments) + global clip 4.0",
                        "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning,
-                       "reversible": ("recompute" if cfg.reversible_recompute else "stored activations") if cfg.reversible else "no",
+                       "reversible": ({True: "recompute", False: "stored activations"}.get(cfg.reversible_recompute, "auto: stored while HBM allows")
+                                      if cfg.reversible else "no"),
                        "grad_compression": args.compression if args.compression != "powersgd"
                        else f"powersgd-rank{args.powersgd_rank}"},
             "rccl_world": world if backend == "nccl" else None,

@@ -60,7 +60,7 @@ class DALLEConfig:
     reversible: bool = True
     # reversible blocks rebuild their inputs in backward (the reference's O(1)-in-depth activation memory);
     # False keeps the activations instead -- same coupling math, one forward less per step (HBM permitting)
-    reversible_recompute: bool = True
+    reversible_recompute: Union[bool, str] = True  # True | False | "auto" (keep what fits in HBM)
     share_input_output_emb: bool = True
     loss_img_weight: float = 7.0
     conv_kernel_size: int = 5
@@ -131,7 +131,7 @@ class DALLEConfig:
         t, i = self.text_len, self.image_seq_len
         per_layer += 4 * self.heads * self.dim_head * (t * t / 2 + i * (t + self.image_fmap_size))
         head = 2 * (self.text_seq_len * self.total_text_tokens + self.image_seq_len * self.num_image_tokens) * d
-        layer_mult = 4.0 if (self.reversible and self.reversible_recompute and include_recompute) else 3.0
+        layer_mult = 4.0 if (self.reversible and self.reversible_recompute is True and include_recompute) else 3.0
         return layer_mult * self.depth * per_layer + 3.0 * head
 
 

@@ -656,18 +656,53 @@ class _FFSublayer(torch.autograd.Function):
 #   x1 = y1 - f(x2); dy2 += f'(x2)^T dy1   (same with the attention sublayer)
 # so the recompute costs exactly one forward per block and no autograd graph is built.
 # ---------------------------------------------------------------------------------------------
+REV_STATS: Dict[str, float] = {}  # last reversible forward: blocks kept / total / bytes kept ("auto" only)
+
+
+def rev_store_budget(device) -> float:
+    """Bytes of block activations the reversible stack may keep from the forward ("auto" policy): what
+    the device can still hold -- free HBM plus the caching allocator's idle reserve -- minus a margin
+    for the backward's own working set (max(6 GB, 8 % of HBM)). ``DALLE_AMD_REV_STORE_GB`` overrides."""
+    env = os.environ.get("DALLE_AMD_REV_STORE_GB")
+    if env is not None:
+        return float(env) * 2 ** 30
+    if device.type != "cuda":
+        return 0.0
+    free, total = torch.cuda.mem_get_info(device)
+    idle = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    return max(0.0, free + idle - max(6 * 2 ** 30, 0.08 * total))
+
+
 class _ReversibleFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blocks, recompute, *params):
+        """``recompute``: True rebuilds every block in backward, False keeps every block's activations,
+        "auto" keeps the FIRST blocks' activations while they fit rev_store_budget (the backward, newest
+        block first, rebuilds the rest from the outputs and then runs on the stored ones)."""
         _count("reversible_stack")
         x1 = x2 = x.contiguous()
-        stored = None if recompute else []
+        if recompute == "auto":
+            budget = rev_store_budget(x.device)
+        else:
+            budget = 0.0 if recompute else float("inf")
+        stored, used, storing = [], 0.0, budget > 0
+        cuda = x.is_cuda
         with torch.no_grad():
             for fa, ga in blocks:
-                x1, sf = _attn_fwd(x1, x2, *fa[0], save=not recompute)
-                x2, sg = _ff_fwd(x2, x1, *ga[0], save=not recompute)
-                if stored is not None:
+                before = torch.cuda.memory_allocated(x.device) if (cuda and storing and budget != float("inf")) else 0
+                x1, sf = _attn_fwd(x1, x2, *fa[0], save=storing)
+                x2, sg = _ff_fwd(x2, x1, *ga[0], save=storing)
+                if storing:
+                    if budget != float("inf") and cuda:
+                        # this block's retained bytes; keep a second block's worth free for the backward
+                        delta = torch.cuda.memory_allocated(x.device) - before
+                        if used + 2 * delta > budget:
+                            del sf, sg
+                            storing = False
+                            continue
+                        used += delta
                     stored.append((sf, sg))
+        REV_STATS.update(stored=len(stored), blocks=len(blocks), stored_bytes=used)
         ctx.blocks = blocks
         ctx.params = params
         ctx.stored = stored
@@ -694,7 +729,8 @@ class _ReversibleFused(torch.autograd.Function):
                 fa, ga = blocks[bi]
                 g_args, g_params = ga
                 f_args, f_params = fa
-                if stored is None:  # rebuild this block's inputs (and activations) from its outputs
+                rebuild = bi >= len(stored)  # blocks past the stored prefix are rebuilt from their outputs
+                if rebuild:
                     x2, saved_g = _ff_fwd(y2, y1, *g_args, save=True, sign=-1.0)
                 else:
                     saved_f, saved_g = stored.pop()
@@ -702,7 +738,7 @@ class _ReversibleFused(torch.autograd.Function):
                 del saved_g
                 dy1 = res[0]
                 collect(g_params, res[1:])
-                if stored is None:
+                if rebuild:
                     x1, saved_f = _attn_fwd(y1, x2, *f_args, save=True, sign=-1.0)
                     y1, y2 = x1, x2
                 res = _attn_bwd(saved_f, f_params, [p.requires_grad for p in f_params], dy1, dy2)
@@ -713,11 +749,12 @@ class _ReversibleFused(torch.autograd.Function):
         return (dx, None, None, *[pending.get(id(p)) for p in ctx.params])
 
 
-def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int, recompute: bool = True):
+def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int, recompute=True):
     """``layers``: per block ((ln_w, ln_b, w_qkv, w_out, b_out, scale, heads, attn_type, shift),
     (ln_w, ln_b, w1, b1, w2, b2, scale, shift)). Returns mean(y1, y2) of the reversible stack.
     ``recompute=False`` keeps every block's activations from the forward instead of rebuilding them
-    in backward (same coupling math; one forward less per step for ~depth x the activation memory)."""
+    in backward (same coupling math; one forward less per step for ~depth x the activation memory);
+    ``"auto"`` keeps as many blocks as the HBM left over holds (see _ReversibleFused.forward)."""
     blocks, uniq, seen = [], [], set()
     for (aln_w, aln_b, w_qkv, w_out, b_out, ascale, heads, attn_type, ashift), (fln_w, fln_b, w1, b1, w2, b2, fscale, fshift) in layers:
         dim_head = w_qkv.shape[0] // 3 // heads
@@ -732,7 +769,7 @@ def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: i
             if id(p) not in seen:
                 seen.add(id(p))
                 uniq.append(p)
-    return _ReversibleFused.apply(x, blocks, bool(recompute), *uniq)
+    return _ReversibleFused.apply(x, blocks, recompute if recompute == "auto" else bool(recompute), *uniq)
 
 
 # ---------------------------------------------------------------------------------------------

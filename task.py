@@ -81,7 +81,8 @@ class TrainingTask:
         self.tokenizer.pad_token = self.tokenizer.eos_token
         if cfg.text_seq_len != trainer_args.text_seq_length:
             cfg = type(cfg)(**{**cfg.to_dict(), "text_seq_len": trainer_args.text_seq_length})
-        cfg.reversible_recompute = bool(trainer_args.reversible_recompute)
+        rr = str(trainer_args.reversible_recompute).lower()
+        cfg.reversible_recompute = "auto" if rr == "auto" else rr not in ("false", "0", "no")
         self.config = cfg
 
         logger.info(f"Creating model ({trainer_args.model_preset}: depth {cfg.depth}, dim {cfg.dim})")

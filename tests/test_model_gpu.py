@@ -96,6 +96,50 @@ def test_fused_reversible_matches_unfused(cuda, arena, monkeypatch):
         assert rel < 2e-2, (name, rel)
 
 
+@pytest.mark.parametrize("budget_gb", [None, "0", "tiny"])
+def test_reversible_auto_partial_storage(cuda, budget_gb, monkeypatch):
+    """recompute="auto": the first blocks keep their activations while the HBM budget allows, the rest
+    are rebuilt in backward -- loss bitwise equal, grads equal to the full-recompute path; a zero budget
+    stores nothing and an unconstrained one (288 GB card, tiny model) stores every block."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = _cfg(True)
+    m = DALLE(cfg).to(cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+
+    def run(policy):
+        m.cfg.reversible_recompute = policy
+        m.zero_grad(set_to_none=True)
+        loss = m(text, img, return_loss=True)
+        loss.backward()
+        return loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    l_ref, g_ref = run(True)
+    if budget_gb == "tiny":
+        # room for about one and a half blocks: measure one block's bytes with an unconstrained run first
+        monkeypatch.delenv("DALLE_AMD_REV_STORE_GB", raising=False)
+        run("auto")
+        per_block = hip_ops.REV_STATS["stored_bytes"] / max(hip_ops.REV_STATS["stored"], 1)
+        monkeypatch.setenv("DALLE_AMD_REV_STORE_GB", str(3.5 * per_block / 2 ** 30))
+    elif budget_gb is not None:
+        monkeypatch.setenv("DALLE_AMD_REV_STORE_GB", budget_gb)
+    l_auto, g_auto = run("auto")
+    m.cfg.reversible_recompute = True
+    stored, blocks = hip_ops.REV_STATS["stored"], hip_ops.REV_STATS["blocks"]
+    if budget_gb is None:
+        assert stored == blocks
+    elif budget_gb == "0":
+        assert stored == 0
+    else:
+        assert 0 < stored < blocks, (stored, blocks)
+    assert l_auto == l_ref
+    for n, g in g_ref.items():
+        rel = ((g - g_auto[n]).norm() / (g.norm() + 1e-8)).item()
+        assert rel < 2e-2, (n, rel)
+
+
 def test_reversible_stored_activations_match_recompute(cuda):
     """reversible_recompute=False (activations kept from the forward) == the rebuild-in-backward path:
     same loss bitwise, gradients equal up to the reconstruction rounding of the recompute."""
