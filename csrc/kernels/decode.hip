@@ -18,32 +18,19 @@ __global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __rest
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   const float* xr = x + (size_t)b * D;
-  f32x4 v[PER];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    v[j] = *reinterpret_cast<const f32x4*>(xr + 4 * (lane + 64 * j));
-    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
-  }
-  const float mean = wave_sum(s) * (1.0f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int j = 0; j < PER; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
-  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
   __bf16* hb = hist + (size_t)b * g.n * D;
+  // every load is independent of the row statistics -- the row, the LN parameters and the shifted
+  // history rows (earlier positions, written by earlier steps) -- so all of them are issued before
+  // the first reduction: one memory round trip per step instead of three
+  f32x4 v[PER], wv[PER], bv[PER];
+  s16x4 sh[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = 4 * (lane + 64 * j);
-    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[i] + bv[i];
-    const s16x4 packed = pack4(o);
-    *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
-    s16x4 outv = packed;
+    v[j] = *reinterpret_cast<const f32x4*>(xr + c);
+    wv[j] = *reinterpret_cast<const f32x4*>(w + c);
+    bv[j] = *reinterpret_cast<const f32x4*>(bias + c);
+    sh[j] = s16x4{};
     if (shift && c < D / 2) {
       int src = -1;
       if (pos < g.T) {
@@ -53,10 +40,28 @@ __global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __rest
         if (c < D / 4) src = (k >= g.S) ? pos - g.S : -1;
         else src = (k % g.S) ? pos - 1 : -1;
       }
-      if (src >= 0) outv = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
-      else outv = s16x4{};
+      if (src >= 0) sh[j] = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
     }
-    *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = outv;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[j][i] + bv[j][i];
+    const s16x4 packed = pack4(o);
+    *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
+    *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = (shift && c < D / 2) ? sh[j] : packed;
   }
 }
 
