@@ -194,7 +194,16 @@ __global__ void splitk_accum_kernel(const float* __restrict__ part, float* __res
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= n) return;
   f32x4 v = accumulate ? *reinterpret_cast<const f32x4*>(acc + i) : f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < s; ++k) {
+  // the partial loads of up to 8 slabs are issued together (one memory round trip per 8 slabs)
+  int k = 0;
+  for (; k + 8 <= s; k += 8) {
+    f32x4 p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = *reinterpret_cast<const f32x4*>(part + (size_t)(k + u) * n + i);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { v[0] += p[u][0]; v[1] += p[u][1]; v[2] += p[u][2]; v[3] += p[u][3]; }
+  }
+  for (; k < s; ++k) {
     const f32x4 p = *reinterpret_cast<const f32x4*>(part + (size_t)k * n + i);
     v[0] += p[0]; v[1] += p[1]; v[2] += p[2]; v[3] += p[3];
   }

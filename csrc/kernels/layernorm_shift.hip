@@ -220,30 +220,35 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 }
 
 // sum `nrows` partial rows of width `width` (column-parallel, fixed order)
-// 256 threads = 64 columns x 4 row groups; 8 independent loads in flight per thread
+// 256 threads = 16 columns x 16 row groups (width / 16 workgroups: 128 for the 2 x 1024 LN partials,
+// enough to keep every row group's loads in flight at once); 8 independent loads per thread per round;
+// the 16 row-group sums are added in a fixed order through LDS, so the result is deterministic.
 // The result goes to a GradSink: columns [0, split) -> out0, [split, width) -> out1 (optionally
 // multiplied per column by mul1), written or ACCUMULATED into the destination -- the destinations
 // are the parameters' fp32 .grad views in the flat arena, so no autograd add kernel follows.
+constexpr int CS_COLS = 16, CS_RG = 16;
 __global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part, int nrows, int width, GradSink sink) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[CS_RG][CS_COLS];
+  const int cl = threadIdx.x % CS_COLS, rg = threadIdx.x / CS_COLS;
+  const int c = blockIdx.x * CS_COLS + cl;
   float s = 0.f;
   if (c < width) {
     int r = rg;
-    for (; r + 28 < nrows; r += 32) {
+    for (; r + 7 * CS_RG < nrows; r += 8 * CS_RG) {
       float t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = part[(size_t)(r + 4 * u) * width + c];
+      for (int u = 0; u < 8; ++u) t[u] = part[(size_t)(r + CS_RG * u) * width + c];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += t[u];
     }
-    for (; r < nrows; r += 4) s += part[(size_t)r * width + c];
+    for (; r < nrows; r += CS_RG) s += part[(size_t)r * width + c];
   }
   red[rg][cl] = s;
   __syncthreads();
   if (rg == 0 && c < width) {
-    float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_RG; ++k) v += red[k][cl];
     float* dst;
     if (c < sink.split) {
       dst = sink.out0 + c;
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict
 }
 
 void column_sum(const float* part, int nrows, int width, const GradSink& sink, hipStream_t st) {
-  hipLaunchKernelGGL(column_sum_kernel, dim3((width + 63) / 64), dim3(256), 0, st, part, nrows, width, sink);
+  hipLaunchKernelGGL(column_sum_kernel, dim3((width + CS_COLS - 1) / CS_COLS), dim3(256), 0, st, part, nrows, width, sink);
 }
 void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st) {
   column_sum(part, nrows, width, GradSink{out, nullptr, nullptr, width, 0}, st);
