@@ -97,15 +97,16 @@ void xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, long R, int 
 // one partial row per workgroup, reduced over workgroups in a fixed order by column_sum -- so the
 // separate column-reduction pass over the logits disappears, deterministically.
 constexpr int XENT_RB = 16;
-constexpr int XENT_MAXV = 40000;  // (V + 16) floats of dynamic LDS must fit the 160 KiB per workgroup
+constexpr int XENT_T = 1024;  // 16 waves: one workgroup per CU when the vocabulary fills the LDS
+constexpr int XENT_MAXV = 40000;  // (V + 32) floats of dynamic LDS must fit the 160 KiB per workgroup
 
-__global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ logits, const int64_t* __restrict__ labels,
+__global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict__ logits, const int64_t* __restrict__ labels,
                                                           float* __restrict__ loss, float* __restrict__ part, long R, int V,
                                                           float gscale) {
   extern __shared__ float colacc[];  // V floats (+16 for the reductions)
   float* red = colacc + ((V + 3) & ~3);
   const int tid = threadIdx.x;
-  for (int c = tid; c < V; c += 256) colacc[c] = 0.f;
+  for (int c = tid; c < V; c += XENT_T) colacc[c] = 0.f;
   const long r0 = (long)blockIdx.x * XENT_RB;
   for (long row = r0; row < r0 + XENT_RB && row < R; ++row) {
     __bf16* lrow = logits + row * (long)V;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
       m = bf2f(reinterpret_cast<const bf16_raw*>(lrow)[tid]);
       s = 1.0f;
     }
-    for (int i = tid; i < nvec; i += 256) {
+    for (int i = tid; i < nvec; i += XENT_T) {
       float f[8];
       unpack8(*reinterpret_cast<const s16x8*>(lr + 8 * i), f);
       float mx = f[0];
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
       m = mn;
       s = acc;
     }
-    for (int i = nvec * 8 + tid; i < Vb; i += 256) {
+    for (int i = nvec * 8 + tid; i < Vb; i += XENT_T) {
       const float f = bf2f(reinterpret_cast<const bf16_raw*>(lr)[i]);
       const float mn = fmaxf(m, f);
       s = s * __expf(m - mn) + __expf(f - mn);
@@ -141,12 +142,16 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
     const float wm = wave_max(m);
     const float ws = wave_sum(s * __expf(m - wm));
     const int w = tid >> 6, l = tid & 63;
+    constexpr int NW = XENT_T / 64;
     __syncthreads();  // the previous row's users of `red` are done
-    if (l == 0) { red[w] = wm; red[4 + w] = ws; }
+    if (l == 0) { red[w] = wm; red[NW + w] = ws; }
     __syncthreads();
-    const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    const float Ssum = red[4] * __expf(red[0] - M) + red[5] * __expf(red[1] - M) + red[6] * __expf(red[2] - M) +
-                       red[7] * __expf(red[3] - M);
+    float M = red[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) M = fmaxf(M, red[k]);
+    float Ssum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) Ssum += red[NW + k] * __expf(red[k] - M);
     const float lse = M + __logf(Ssum);
     const int64_t lab = labels[row];
     if (tid == 0) loss[row] = lse - bf2f(reinterpret_cast<const bf16_raw*>(lrow)[lab]);
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
       colacc[tid] += bf2f(q);
     }
     const int64_t labb = lab - head;
-    for (int i = tid; i < nvec; i += 256) {
+    for (int i = tid; i < nvec; i += XENT_T) {
       float f[8];
       s16x8* p = reinterpret_cast<s16x8*>(lr + 8 * i);
       unpack8(*p, f);
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
 #pragma unroll
       for (int j = 0; j < 8; ++j) colacc[head + 8 * i + j] += f[j];
     }
-    for (int i = nvec * 8 + tid; i < Vb; i += 256) {
+    for (int i = nvec * 8 + tid; i < Vb; i += XENT_T) {
       bf16_raw* p = reinterpret_cast<bf16_raw*>(lr) + i;
       float g = __expf(bf2f(*p) - lse);
       if (i == labb) g -= 1.0f;
@@ -187,19 +192,19 @@ __global__ __launch_bounds__(256) void xent_colsum_kernel(__bf16* __restrict__ l
     __syncthreads();  // the next row may map a column to another thread
   }
   float* prow = part + (size_t)blockIdx.x * V;
-  for (int c = tid; c < V; c += 256) prow[c] = colacc[c];
+  for (int c = tid; c < V; c += XENT_T) prow[c] = colacc[c];
 }
 
 bool xent_colsum(void* logits, const int64_t* labels, float* loss, float* part, long R, int V, float gscale, hipStream_t st) {
   if (V > XENT_MAXV) return false;
   const long nblk = (R + XENT_RB - 1) / XENT_RB;
-  const size_t lds = (size_t)(((V + 3) & ~3) + 16) * sizeof(float);
+  const size_t lds = (size_t)(((V + 3) & ~3) + 2 * (XENT_T / 64)) * sizeof(float);
   static bool attr = false;
   if (!attr) {  // dynamic LDS beyond the default cap needs an explicit per-kernel limit
     (void)hipFuncSetAttribute((const void*)xent_colsum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(xent_colsum_kernel, dim3(nblk), dim3(256), lds, st, (__bf16*)logits, labels, loss, part, R, V, gscale);
+  hipLaunchKernelGGL(xent_colsum_kernel, dim3(nblk), dim3(XENT_T), lds, st, (__bf16*)logits, labels, loss, part, R, V, gscale);
   return true;
 }
 
