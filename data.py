@@ -5,7 +5,9 @@ tokenisation (no special tokens, truncation to ``max_sequence_length``) and int1
 decoding as the reference's ``preprocess_batch``. Sources, in order of preference:
 
 * ``dataset_path``: a local directory of parquet / jsonl shards with the
-  ``laion/laion_100m_vqgan_f8`` columns (``caption, NSFW, original_width, original_height, code``);
+  ``laion/laion_100m_vqgan_f8`` columns (``caption, NSFW, original_width, original_height, code``),
+  streamed record batch by record batch; or a ``datasets`` streaming source -- the reference's Hub id
+  (network needed) or ``parquet:<glob>`` / ``json:<glob>``;
 * otherwise synthetic LAION-shaped pairs (there is no network for the streamed dataset).
 
 Per-peer shuffling uses a seeded shuffle buffer (``shuffle_buffer_size``, ``shuffle_seed``).
@@ -53,6 +55,9 @@ def preprocess_batch(batch, tokenizer, max_sequence_length: int):
     return out
 
 
+_COLUMNS = ("caption", "NSFW", "original_width", "original_height", "code")
+
+
 def _iter_rows(path: str) -> Iterator[dict]:
     files = sorted(glob.glob(os.path.join(path, "*.parquet")) + glob.glob(os.path.join(path, "*.jsonl")))
     if not files:
@@ -61,9 +66,10 @@ def _iter_rows(path: str) -> Iterator[dict]:
         if f.endswith(".parquet"):
             import pyarrow.parquet as pq
 
-            table = pq.read_table(f)
-            cols = table.column_names
-            for batch in table.to_batches(1024):
+            # streamed record batch by record batch: a shard is never materialised whole
+            pf = pq.ParquetFile(f)
+            cols = [c for c in _COLUMNS if c in pf.schema_arrow.names]
+            for batch in pf.iter_batches(batch_size=1024, columns=cols):
                 d = batch.to_pydict()
                 for i in range(batch.num_rows):
                     yield {c: d[c][i] for c in cols}
@@ -107,6 +113,30 @@ class LocalLAIONDataset(IterableDataset):
         yield from buf
 
 
+class HFStreamingLAION(IterableDataset):
+    """The reference's source (``data.py:34-47``): a ``datasets`` streaming dataset -- a Hub id such as
+    ``laion/laion_100m_vqgan_f8`` (needs network) or ``parquet:<glob>`` / ``json:<glob>`` for local
+    shards -- shuffled with a seeded buffer and mapped through :func:`preprocess_batch` in batches."""
+
+    def __init__(self, spec: str, tokenizer, shuffle_buffer_size, shuffle_seed, preprocessing_batch_size, max_sequence_length):
+        import datasets
+
+        builder, _, files = spec.partition(":")
+        if builder in ("parquet", "json") and files:
+            ds = datasets.load_dataset(builder, data_files=sorted(glob.glob(files)), split="train", streaming=True)
+        else:
+            ds = datasets.load_dataset(spec, split="train", streaming=True)
+        ds = ds.shuffle(seed=shuffle_seed, buffer_size=shuffle_buffer_size)
+        keep = [c for c in _COLUMNS]
+        self.ds = ds.map(lambda b: preprocess_batch(b, tokenizer, max_sequence_length), batched=True,
+                         batch_size=preprocessing_batch_size, remove_columns=[c for c in (ds.column_names or keep)])
+
+    def __iter__(self):
+        for ex in self.ds:
+            yield {"input_ids": torch.as_tensor(ex["input_ids"]), "attention_mask": torch.as_tensor(ex["attention_mask"]),
+                   "image": torch.as_tensor(np.asarray(ex["image"], dtype=np.int64))}
+
+
 def make_dataset(
     tokenizer,
     *,
@@ -118,9 +148,12 @@ def make_dataset(
     image_seq_len: int = 1024,
     num_image_tokens: int = 8192,
 ):
-    if dataset_path:
+    if dataset_path and os.path.isdir(dataset_path):
         return LocalLAIONDataset(dataset_path, tokenizer, shuffle_buffer_size, shuffle_seed,
                                  preprocessing_batch_size, max_sequence_length)
+    if dataset_path:  # a `datasets` streaming source (Hub id, or parquet:/json: globs)
+        return HFStreamingLAION(dataset_path, tokenizer, shuffle_buffer_size, shuffle_seed,
+                                preprocessing_batch_size, max_sequence_length)
     logger.info("no dataset_path given: streaming synthetic LAION-shaped pairs")
     return SyntheticLAION(text_seq_len=max_sequence_length, image_seq_len=image_seq_len,
                           vocab_size=getattr(tokenizer, "vocab_size", 32100), num_image_tokens=num_image_tokens,

@@ -177,6 +177,40 @@ def test_preprocess_batch_filters_and_decodes():
     assert empty == {"input_ids": [], "attention_mask": [], "image": []}
 
 
+def test_local_and_datasets_streaming_sources(tmp_path):
+    """Parquet shards in the laion_100m_vqgan_f8 column layout: the local directory reader (streamed
+    record batches) and the `datasets` streaming source (`parquet:<glob>`, the reference's
+    load_dataset(..., streaming=True) path) yield the same filtered, tokenised examples."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    from data import make_dataset
+
+    class Tok:
+        def __call__(self, texts, add_special_tokens, max_length, truncation):
+            ids = [[len(t) % 7 + 1] * min(len(t), max_length) for t in texts]
+            return {"input_ids": ids, "attention_mask": [[1] * len(i) for i in ids]}
+
+    rng = np.random.default_rng(0)
+    for shard in range(2):
+        n = 40
+        caps = [f"caption number {shard}-{i}" if i % 5 else "no" for i in range(n)]
+        tbl = pa.table({"caption": caps, "NSFW": ["UNLIKELY" if i % 7 else "LIKELY" for i in range(n)],
+                        "original_width": [256] * n, "original_height": [256] * n,
+                        "code": [rng.integers(0, 8192, 16, dtype=np.int16).tobytes() for _ in range(n)]})
+        pq.write_table(tbl, tmp_path / f"part-{shard}.parquet")
+    kw = dict(shuffle_buffer_size=1, shuffle_seed=0, preprocessing_batch_size=16, max_sequence_length=8)
+    local = list(make_dataset(Tok(), dataset_path=str(tmp_path), **kw))
+    kept = sum(1 for s in range(2) for i in range(40) if i % 5 and i % 7)
+    assert len(local) == kept
+    assert all(ex["image"].dtype == torch.int64 and ex["image"].shape == (16,) for ex in local)
+    streamed = list(make_dataset(Tok(), dataset_path=f"parquet:{tmp_path}/*.parquet", **kw))
+    assert len(streamed) == kept
+    key = lambda ex: tuple(ex["image"].tolist())  # noqa: E731
+    assert sorted(map(key, streamed)) == sorted(map(key, local))
+
+
 def test_delegating_optimizer():
     from dalle_amd.optim.wrapper import OptimizerWrapper
 
