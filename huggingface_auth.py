@@ -26,15 +26,20 @@ logger = get_logger(__name__)
 
 
 def call_with_retries(func, n_retries: int = 10, initial_delay: float = 1.0):
-    for i in range(n_retries):
+    """``func()`` with exponential backoff (initial_delay * 2^attempt seconds between attempts); the
+    last attempt's exception propagates."""
+    attempt = 0
+    while True:
         try:
             return func()
-        except Exception as e:  # noqa: BLE001
-            if i == n_retries - 1:
+        except Exception as err:  # noqa: BLE001 - any transport / server error is retried
+            attempt += 1
+            if attempt >= n_retries:
                 raise
-            delay = initial_delay * (2 ** i)
-            logger.warning(f"Failed to call `{getattr(func, '__name__', func)}` with exception: {e!r}. Retrying in {delay:.1f} sec")
-            time.sleep(delay)
+            wait = initial_delay * 2 ** (attempt - 1)
+            name = getattr(func, "__name__", repr(func))
+            logger.warning(f"{name} failed ({err!r}); attempt {attempt + 1}/{n_retries} in {wait:.1f} s")
+            time.sleep(wait)
 
 
 @dataclass
