@@ -106,3 +106,31 @@ def test_vqgan_checkpoint_naming(tmp_path):
     assert torch.allclose(d.decode(codes), src.decode(codes))
     with pytest.raises(RuntimeError):
         d.get_codebook_indices(img)
+
+
+@pytest.mark.parametrize("reversible", [False, True])
+def test_parallel_prefill_matches_sequential_steps(reversible):
+    """The batched caption prefill fills the KV caches and LN histories as the T-1 decode steps do and
+    leaves the engine at the same position: the next step's logits agree."""
+    torch.manual_seed(0)
+    cfg = _cfg(reversible)
+    m = DALLE(cfg).eval()
+    B = 3
+    text = torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len))
+    text[:, 40:] = 0  # padding -> the unique per-position pad ids
+    tb = m.prepare_text(text)
+    seq = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False)
+    par = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False)
+    with torch.no_grad():
+        seq.prefill(tb)
+        par.prefill_parallel(tb)
+        P = cfg.text_len - 1
+        assert int(seq.pos) == int(par.pos) == P and torch.equal(seq.tok, par.tok)
+        for li in range(len(seq.kc)):
+            for a, b in ((seq.kc[li], par.kc[li]), (seq.vc[li], par.vc[li])):
+                assert torch.allclose(a[:, :P], b[:, :P], atol=1e-4, rtol=1e-4)
+                assert not b[:, P:].any()
+            for j in range(2):
+                assert torch.allclose(seq.hist[li][j][:, :P], par.hist[li][j][:, :P], atol=1e-4, rtol=1e-4)
+        l_seq, l_par = seq._forward_position(), par._forward_position()
+    assert torch.allclose(l_seq, l_par, atol=2e-4, rtol=1e-4), (l_seq - l_par).abs().max()

@@ -71,6 +71,19 @@ def test_split_decode_engine_matches_single(cuda, use_graph):
     assert torch.equal(again, got)
 
 
+def test_parallel_prefill_generation_matches_sequential(cuda):
+    """Greedy generation with the batched caption prefill == with the T-1 sequential decode steps."""
+    torch.manual_seed(0)
+    cfg = _cfg(True)
+    m = DALLE(cfg).eval().to(cuda)
+    text = torch.randint(2, cfg.num_text_tokens, (4, cfg.text_seq_len), device=cuda)
+    tb = m.prepare_text(text)
+    eng = DecodeEngine(m, 4, device=cuda)
+    seq = eng.generate(tb, top_k=1, seed=3, parallel_prefill=False)
+    par = eng.generate(tb, top_k=1, seed=3, parallel_prefill=True)
+    assert (seq == par).float().mean().item() > 0.98
+
+
 def test_vq_embed_kernel(cuda):
     vae = VQGanVAE(n_embed=64, embed_dim=32, ddconfig=dict(ch=32, out_ch=3, ch_mult=(1, 2), num_res_blocks=1,
                                                            attn_resolutions=(8,), resolution=16, z_channels=32)).to(cuda)
