@@ -40,6 +40,7 @@ std::vector<int> skinny_shape_info(int, int, int, int);
 bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
                    float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
+void splitk_accum_t(const float*, float*, int, int, int, int, hipStream_t);
 void psgd_orthonormalize(float*, const long*, const int*, int, int, float, hipStream_t);
 bool psgd_reconstruct(float*, float*, const float*, const float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
@@ -425,6 +426,17 @@ void splitk_accum_(Tensor acc, Tensor part, bool accumulate) {
   const long n = acc.numel();
   TORCH_CHECK(part.dim() >= 1 && part.numel() == part.size(0) * n && n % 4 == 0, "splitk_accum: shape mismatch");
   dalle::splitk_accum(part.data_ptr<float>(), acc.data_ptr<float>(), n, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
+}
+
+// acc (R, C) (+)= sum_k part[k]^T with part (s, C, R): the weight-gradient fold of the transposed
+// split-K product (x^T g is the faster hipBLASLt problem for N_out > K_in)
+void splitk_accum_t_(Tensor acc, Tensor part, bool accumulate) {
+  CHECK_IN(acc, torch::kFloat32); CHECK_IN(part, torch::kFloat32);
+  TORCH_CHECK(acc.dim() == 2 && part.dim() == 3 && part.size(1) == acc.size(1) && part.size(2) == acc.size(0),
+              "splitk_accum_t: part (s, C, R) for acc (R, C)");
+  const int R = acc.size(0), C = acc.size(1);
+  TORCH_CHECK(R % 32 == 0 && C % 32 == 0, "splitk_accum_t: R, C multiples of 32");
+  dalle::splitk_accum_t(part.data_ptr<float>(), acc.data_ptr<float>(), R, C, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
 }
 
 // C = A . B^T (+ bias): A (M, K), B (N, K) bf16, both K-contiguous; M, N multiples of 256, K of 64
@@ -947,6 +959,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
+  m.def("splitk_accum_t_", &splitk_accum_t_);
   m.def("psgd_orthonormalize_", &psgd_orthonormalize_);
   m.def("psgd_reconstruct_", &psgd_reconstruct_);
   m.def("qkv_rope", &qkv_rope);

@@ -130,6 +130,8 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
 
 
 SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
+# split-K weight grads as x^T g + a transposing fold when N_out > K_in
+WGRAD_TRANSPOSED = int(os.environ.get("DALLE_AMD_WGRAD_T", "0"))
 # weight grads on the hand-written MN-major GEMM (gemm_wgrad_) instead of hipBLASLt (opt-in, see weight_grad)
 OWN_WGRAD = int(os.environ.get("DALLE_AMD_OWN_WGRAD", "0"))
 # QKV projection through the hand-written GEMM with the rotary in its epilogue (csrc/kernels/gemm.hip)
@@ -160,9 +162,16 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
             return None if fused else out
     s = wgrad_splits(M, N, K)
     if s > 1:
-        part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
         out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
-        C().splitk_accum_(out, part, fused)
+        if WGRAD_TRANSPOSED and N > K and N % 32 == 0 and K % 32 == 0:
+            # x^T g is the faster hipBLASLt problem in isolation when N_out > K_in (3072x1024: 961 vs 836
+            # TF/s, 8192x1024: 1192 vs 1111 at M = 61440, profiles/r2_wgrad_layouts.jsonl) but the full
+            # step measured the same (185.7 / 185.9 vs 185.0 / 186.1 ms, same box): opt-in
+            part = torch.bmm(x2.view(s, M // s, K).transpose(1, 2), g2.view(s, M // s, N), out_dtype=torch.float32)
+            C().splitk_accum_t_(out, part, fused)
+        else:
+            part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
+            C().splitk_accum_(out, part, fused)
         return None if fused else out
     if fused:
         torch.addmm(gw, g2.t(), x2, out_dtype=torch.float32, out=gw)
