@@ -472,6 +472,32 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
 }
 
 // ------------------------------------------------------------------------------------------------
+// delta = rowsum(dO * O) per storage row, for the concurrent backward (the dK/dV kernels start before
+// the dQ kernel, which otherwise publishes it): one thread per (row, 16-byte chunk)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restrict__ dout, const __bf16* __restrict__ out,
+                                                         float* __restrict__ delta, AttnGeom g, int BH) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = gid & 7;
+  const long row_g = gid >> 3;
+  if (row_g >= (long)BH * g.Np) return;
+  const int bh = row_g / g.Np, srow = row_g - (long)bh * g.Np;
+  const int off = tok_row(g, srow);
+  float acc = 0.f;
+  if (off >= 0) {
+    float fd[8], fo[8];
+    unpack8(ld_tok(tok_base(dout, g, bh), off, chunk * 8), fd);
+    unpack8(ld_tok(tok_base(out, g, bh), off, chunk * 8), fo);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = fmaf(fd[i], fo[i], acc);
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (chunk == 0) delta[row_g] = acc;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Backward dQ (query-centric)
 // ------------------------------------------------------------------------------------------------
 // dS for one key tile of the wave's 32 queries -> dQ^T += K^T dS^T (S^T layout as in the forward).
@@ -512,7 +538,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                              const __bf16* __restrict__ out, const float* __restrict__ lse,
                                                              float* __restrict__ delta, __bf16* __restrict__ dQ, AttnGeom g,
-                                                             RopeOut ro) {
+                                                             RopeOut ro, int delta_ready) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   int grp, bh;
@@ -543,16 +569,22 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
     for (int s = 0; s < 4; ++s) {
       qf[s] = ld16(qp + 16 * s);
       const s16x8 d = ld_tok(dob, qoff, 16 * s + 8 * hl);
-      const s16x8 o = ld_tok(outb, qoff, 16 * s + 8 * hl);
-      float fd[8], fo[8];
-      unpack8(d, fd);
-      unpack8(o, fo);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dl = fmaf(fd[i], fo[i], dl);
       dof[s] = __builtin_bit_cast(bf16x8, d);
+      if (!delta_ready) {
+        const s16x8 o = ld_tok(outb, qoff, 16 * s + 8 * hl);
+        float fd[8], fo[8];
+        unpack8(d, fd);
+        unpack8(o, fo);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dl = fmaf(fd[i], fo[i], dl);
+      }
     }
-    dl += __shfl_xor(dl, 32, 64);
-    if (active && hl == 0) delta[(size_t)bh * g.Np + qrow] = dl;
+    if (delta_ready) {
+      dl = delta[(size_t)bh * g.Np + qrow];
+    } else {
+      dl += __shfl_xor(dl, 32, 64);
+      if (active && hl == 0) delta[(size_t)bh * g.Np + qrow] = dl;
+    }
   }
   const float lq = lse[(size_t)bh * g.Np + qrow];
   f32x16 dq0 = {}, dq1 = {};
@@ -1038,27 +1070,61 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   // image keys inside the dQ kernel (rotary-fused output path; DALLE_AMD_ATTN_FUSE_LOCAL=0 disables)
   const char* fl = getenv("DALLE_AMD_ATTN_FUSE_LOCAL");
   const bool fuse_local = dqkv != nullptr && (g.pattern == 1 || g.pattern == 2) && !(fl && fl[0] == '0');
+  // DALLE_AMD_ATTN_BWD_CONC=1: delta by its own small kernel, then the dK/dV kernels on a side stream
+  // run concurrently with the dQ kernel (both latency / VALU bound, each ~50 % of wave-cycles waiting)
+  static const bool conc = [] { const char* e = getenv("DALLE_AMD_ATTN_BWD_CONC"); return e && e[0] == '1'; }();
+  const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
+  hipStream_t kst = st;
+  static hipStream_t side[64] = {};
+  static hipEvent_t ev_in[64] = {}, ev_out[64] = {};
+  int dev = 0;
+  if (conc) {
+    (void)hipGetDevice(&dev);
+    if (side[dev] == nullptr) {
+      (void)hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
+      (void)hipEventCreateWithFlags(&ev_in[dev], hipEventDisableTiming);
+      (void)hipEventCreateWithFlags(&ev_out[dev], hipEventDisableTiming);
+    }
+    const long rows = (long)BH * g.Np;
+    hipLaunchKernelGGL(attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st, (const __bf16*)dout,
+                       (const __bf16*)out, delta, g, BH);
+    (void)hipEventRecord(ev_in[dev], st);
+    (void)hipStreamWaitEvent(side[dev], ev_in[dev], 0);
+    kst = side[dev];
+  }
+  auto launch_dkdv = [&](hipStream_t s2) {
+    // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
+    hipStream_t st = s2;
+    ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
+                (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+    // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
+    if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+                (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+  };
+  if (conc) launch_dkdv(kst);
+  const int dr = conc ? 1 : 0;
   if (fuse_local) {
     if (attn_occ(1) == 3)
       hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
+                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
     else
       hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
+                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
   } else if (attn_occ(1) == 3) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
   } else {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro);
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
   }
-  const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
-  // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
-  ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
-              (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
-  // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
-  if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-              (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+  if (conc) {
+    // the caller's stream resumes only after the side-stream kernels: every later use of the outputs,
+    // and every reuse of the inputs' memory by the caching allocator, is ordered after them
+    (void)hipEventRecord(ev_out[dev], kst);
+    (void)hipStreamWaitEvent(st, ev_out[dev], 0);
+  } else {
+    launch_dkdv(st);
+  }
 }
 
 }  // namespace dalle
