@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Median time of the two fused-epilogue GEMMs at the bench24 B48 shapes (M = 61440 tokens):
 FF-out dgrad + GEGLU backward (ff_dgrad_geglu) and QKV + rotary into the attention layout (qkv_rope).
-One JSON line; environment knobs (e.g. DALLE_AMD_GEMM_STAGGER) are read once per process."""
+One JSON line."""
 import json
 import os
 import sys
@@ -39,8 +39,7 @@ def main():
     x = torch.randn(M, D, device=dev).bfloat16()
     wq = (torch.randn(3 * H * 64, D, device=dev) * 0.03).bfloat16()
     cos, sin = rotary_tables(T, S, 64, device=dev)
-    res = {"stagger": os.environ.get("DALLE_AMD_GEMM_STAGGER", "0"),
-           "stagger_qkv": os.environ.get("DALLE_AMD_GEMM_STAGGER_QKV", "0")}
+    res = {}
     res["ff_dgrad_geglu_us"] = round(timeit(lambda: C.ff_dgrad_geglu(dy, w2t, h)), 1)
     res["qkv_rope_us"] = round(timeit(lambda: C.qkv_rope(x, wq, cos, sin, T, S, H, n, False, 0.125)), 1)
     print(json.dumps(res), flush=True)
