@@ -56,11 +56,17 @@ bool conv_out(const void*, const void*, const float*, const float*, const float*
 void softmax_rows(const float*, void*, long, int, float, hipStream_t);
 long xent_colsum_blocks(long);
 void embed_bwd(const float*, const int*, const int*, const int*, float*, float*, int, int, hipStream_t);
-void decode_ln_shift(const float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int,
-                     hipStream_t);
+void decode_ln_shift(float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int, hipStream_t,
+                     const float*, const void*, const float*, int);
+void residual_from_partials(float*, const float*, const void*, const float*, int, int, int, hipStream_t);
+void decode_attn_part(const float*, int, const float*, const float*, float, void*, void*, void*, const int*, const DecodeGeom&, int,
+                      hipStream_t);
+bool skinny_partials(SkinnyArgs, hipStream_t);
+int skinny_partials_ks(int, int, int);
+void skinny_partials_config(int);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
                  hipStream_t);
-void decode_attn(const void*, const void*, const void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
+void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
 void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 bool sample_step(const SampleArgs&, hipStream_t);
 bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
@@ -509,6 +515,21 @@ Tensor skinny_linear(Tensor X, Tensor W, c10::optional<Tensor> bias, bool out_f3
   return out;
 }
 
+// split-K partial slabs (KS, M, N) fp32 of Y = X W^T for a consumer that sums them (no bias)
+Tensor skinny_partials(Tensor X, Tensor W) {
+  CHECK_CUDA(X); CHECK_DT(X, torch::kBFloat16); CHECK_IN(W, torch::kBFloat16);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && W.dim() == 2 && X.size(1) == W.size(1), "skinny_partials: X (M, K), W (N, K)");
+  const int M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && N % 16 == 0 && K % 128 == 0 && X.stride(0) % 8 == 0, "skinny_partials: shapes");
+  const int KS = dalle::skinny_partials_ks(M, N, K);
+  auto part = torch::empty({KS, M, N}, X.options().dtype(torch::kFloat32));
+  dalle::SkinnyArgs a{};
+  a.X = X.data_ptr(); a.W = W.data_ptr(); a.M = M; a.N = N; a.K = K; a.ldx = X.stride(0); a.KS = KS;
+  a.out = part.data_ptr();
+  TORCH_CHECK(dalle::skinny_partials(a, cur_stream()), "skinny_partials: unsupported shape");
+  return part;
+}
+
 Tensor skinny_geglu(Tensor X, Tensor W, c10::optional<Tensor> bias, Tensor cnt) {
   TORCH_CHECK(W.size(0) % 2 == 0, "skinny_geglu: W holds the value and gate halves");
   Tensor ws;
@@ -786,15 +807,62 @@ static dalle::DecodeGeom make_decode_geom(int T, int S, int n, int H, int K, int
   return g;
 }
 
-void decode_ln_shift_(Tensor x, Tensor w, Tensor b, Tensor hist, Tensor y, Tensor pos, int64_t T, int64_t S, bool shift) {
+// pending: (part (KS, B, D) fp32, bias (D) bf16 or None, scale (D) fp32) applied to x before the LN
+void decode_ln_shift_(Tensor x, Tensor w, Tensor b, Tensor hist, Tensor y, Tensor pos, int64_t T, int64_t S, bool shift,
+                      c10::optional<Tensor> part, c10::optional<Tensor> pbias, c10::optional<Tensor> pscale) {
   CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(b, torch::kFloat32);
   CHECK_IN(hist, torch::kBFloat16); CHECK_IN(y, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
   const int B = x.size(0), D = x.size(-1);
   TORCH_CHECK(x.numel() == (long)B * D && hist.size(0) == B && hist.size(2) == D && y.numel() == (long)B * D);
   TORCH_CHECK(D == 256 || D == 512 || D == 1024 || D == 2048, "decode_ln_shift: unsupported hidden size");
   auto g = make_decode_geom(T, S, hist.size(1), 1, 1, 0);
+  const float* pp = nullptr;
+  const void* pb = nullptr;
+  const float* ps = nullptr;
+  int KS = 0;
+  if (part.has_value() && part->defined()) {
+    CHECK_IN((*part), torch::kFloat32); TORCH_CHECK(pscale.has_value() && pscale->defined(), "decode_ln_shift: pending needs a scale");
+    CHECK_IN((*pscale), torch::kFloat32);
+    TORCH_CHECK(part->dim() == 3 && part->size(1) == B && part->size(2) == D && pscale->numel() == D, "decode_ln_shift: pending shapes");
+    pp = part->data_ptr<float>();
+    ps = pscale->data_ptr<float>();
+    KS = part->size(0);
+    if (pbias.has_value() && pbias->defined()) {
+      CHECK_IN((*pbias), torch::kBFloat16); TORCH_CHECK(pbias->numel() == D);
+      pb = pbias->data_ptr();
+    }
+  }
   dalle::decode_ln_shift(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), hist.data_ptr(), y.data_ptr(),
-                         pos.data_ptr<int>(), g, B, D, shift ? 1 : 0, cur_stream());
+                         pos.data_ptr<int>(), g, B, D, shift ? 1 : 0, cur_stream(), pp, pb, ps, KS);
+}
+
+void residual_from_partials_(Tensor x, Tensor part, c10::optional<Tensor> pbias, Tensor pscale) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(part, torch::kFloat32); CHECK_IN(pscale, torch::kFloat32);
+  const int B = x.size(0), D = x.size(-1);
+  TORCH_CHECK(x.numel() == (long)B * D && D % 4 == 0 && part.dim() == 3 && part.size(1) == B && part.size(2) == D &&
+              pscale.numel() == D, "residual_from_partials: shapes");
+  const void* pb = nullptr;
+  if (pbias.has_value() && pbias->defined()) {
+    CHECK_IN((*pbias), torch::kBFloat16); TORCH_CHECK(pbias->numel() == D);
+    pb = pbias->data_ptr();
+  }
+  dalle::residual_from_partials(x.data_ptr<float>(), part.data_ptr<float>(), pb, pscale.data_ptr<float>(), part.size(0), B, D,
+                                cur_stream());
+}
+
+// attention of the new token whose q / k / v are still split-K partials of the QKV projection
+void decode_attn_part_(Tensor part, Tensor cosT, Tensor sinT, double qscale, Tensor kc, Tensor vc, Tensor out, Tensor pos,
+                       int64_t T, int64_t S, int64_t H, int64_t K, int64_t pattern) {
+  CHECK_IN(part, torch::kFloat32); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(out, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  const int BH = kc.size(0), B = BH / H;
+  TORCH_CHECK(BH % H == 0 && out.numel() == (long)BH * 64 && vc.sizes() == kc.sizes() && kc.size(2) == 64);
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == B && part.size(2) == 3 * H * 64, "decode_attn_part: part (KS, B, 3*H*64)");
+  TORCH_CHECK(kc.size(1) == T + S * S - 1, "decode cache must hold the full sequence");
+  TORCH_CHECK(cosT.size(0) >= kc.size(1) && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes());
+  auto g = make_decode_geom(T, S, kc.size(1), H, K, pattern);
+  dalle::decode_attn_part(part.data_ptr<float>(), part.size(0), cosT.data_ptr<float>(), sinT.data_ptr<float>(), (float)qscale,
+                          kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, B, cur_stream());
 }
 
 void decode_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, Tensor pos, int64_t H, double qscale) {
@@ -981,10 +1049,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_out", &conv_out);
   m.def("softmax_rows", &softmax_rows);
   m.def("embed_bwd_", &embed_bwd_);
-  m.def("decode_ln_shift_", &decode_ln_shift_);
+  m.def("decode_ln_shift_", &decode_ln_shift_, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("hist"), py::arg("y"),
+        py::arg("pos"), py::arg("T"), py::arg("S"), py::arg("shift"), py::arg("part") = py::none(),
+        py::arg("pbias") = py::none(), py::arg("pscale") = py::none());
   m.def("decode_rope_", &decode_rope_);
   m.def("decode_attn_", &decode_attn_);
   m.def("skinny_linear", &skinny_linear);
+  m.def("skinny_partials", &skinny_partials);
+  m.def("skinny_partials_config", &dalle::skinny_partials_config);
+  m.def("residual_from_partials_", &residual_from_partials_, py::arg("x"), py::arg("part"), py::arg("pbias"), py::arg("pscale"));
+  m.def("decode_attn_part_", &decode_attn_part_);
   m.def("skinny_force_config", &dalle::skinny_force_config);
   m.def("skinny_shape_info", &dalle::skinny_shape_info);
   m.def("skinny_geglu", &skinny_geglu);

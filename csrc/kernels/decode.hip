@@ -8,25 +8,45 @@
 namespace dalle {
 
 // ---- LayerNorm of the new token, append to the per-branch LN history, emit the shifted row ----
+// Pending residual update of the stream a LayerNorm reads: x += scale * (sum_ks part[ks] + bias), the
+// split-K partial slabs of the projection that produced it (skinny EPI 4) -- summed here, so that
+// GEMM needs no cross-workgroup hand-off and its workgroups each read only a slice of K.
+struct PendingRes {
+  const float* part;  // (KS, B, D) fp32, or null
+  const __bf16* bias; // (D) bf16, may be null
+  const float* scale; // (D) LayerScale
+  int KS;
+};
+
 template <int D>
-__global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(64) void decode_ln_shift_kernel(float* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, __bf16* __restrict__ hist,
                                                              __bf16* __restrict__ y, const int* __restrict__ pos_ptr,
-                                                             DecodeGeom g, int shift) {
+                                                             DecodeGeom g, int shift, PendingRes pr) {
   constexpr int PER = D / 256;
   const int b = blockIdx.x, lane = threadIdx.x;
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
-  const float* xr = x + (size_t)b * D;
+  float* xr = x + (size_t)b * D;
   __bf16* hb = hist + (size_t)b * g.n * D;
   // every load is independent of the row statistics -- the row, the LN parameters and the shifted
   // history rows (earlier positions, written by earlier steps) -- so all of them are issued before
   // the first reduction: one memory round trip per step instead of three
-  f32x4 v[PER], wv[PER], bv[PER];
+  f32x4 v[PER], wv[PER], bv[PER], pacc[PER];
   s16x4 sh[PER];
+  const int B = gridDim.x;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = 4 * (lane + 64 * j);
+    pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (pr.part != nullptr) {  // all (<= 8) partial slabs in flight together with the row loads
+      f32x4 t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        t[k] = k < pr.KS ? *reinterpret_cast<const f32x4*>(pr.part + ((size_t)k * B + b) * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pacc[j] += t[k];
+    }
     v[j] = *reinterpret_cast<const f32x4*>(xr + c);
     wv[j] = *reinterpret_cast<const f32x4*>(w + c);
     bv[j] = *reinterpret_cast<const f32x4*>(bias + c);
@@ -41,6 +61,19 @@ __global__ __launch_bounds__(64) void decode_ln_shift_kernel(const float* __rest
         else src = (k % g.S) ? pos - 1 : -1;
       }
       if (src >= 0) sh[j] = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
+    }
+  }
+  if (pr.part != nullptr) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(pr.scale + c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float bb = pr.bias ? (float)pr.bias[c + i] : 0.f;
+        v[j][i] += sc[i] * (pacc[j][i] + bb);
+      }
+      *reinterpret_cast<f32x4*>(xr + c) = v[j];
     }
   }
   float s = 0.f;
@@ -100,6 +133,29 @@ __global__ void decode_rope_kernel(const __bf16* __restrict__ qkv, const float* 
   }
 }
 
+// the last pending update of a step (before the final LayerNorm): x += scale * (sum_ks part + bias)
+__global__ __launch_bounds__(256) void residual_from_partials_kernel(float* __restrict__ x, PendingRes pr, int B, int D) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= (long)B * D) return;
+  const int c = i % D;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(pr.part + i);
+  for (int k = 1; k < pr.KS; ++k) acc += *reinterpret_cast<const f32x4*>(pr.part + (size_t)k * B * D + i);
+  f32x4 xv = *reinterpret_cast<const f32x4*>(x + i);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) xv[t] += pr.scale[c + t] * (acc[t] + (pr.bias ? (float)pr.bias[c + t] : 0.f));
+  *reinterpret_cast<f32x4*>(x + i) = xv;
+}
+
+// q / k / v of the new token from the QKV projection's split-K partial slabs (KS, B, 3*H*64): summed,
+// rotated (3-axis rotary at *pos), q pre-scaled; k / v appended to the caches.
+struct QkvPartials {
+  const float* part;
+  const float* cosT;
+  const float* sinT;
+  int KS, B;
+  float qscale;
+};
+
 __device__ __forceinline__ int decode_num_keys(const DecodeGeom& g, int pos, int& nloc, int& r0, int& c0, int& nr, int& nc) {
   // text keys [0, min(T, pos+1)), then an image-local rectangle (rows r0.., cols c0..) clipped by causality
   if (pos < g.T) { nloc = 0; return pos + 1; }
@@ -147,18 +203,49 @@ __device__ __forceinline__ float slot_sum(float v) {  // over the 8 lanes of one
   return v;
 }
 
-__global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ kc,
-                                                          const __bf16* __restrict__ vc, __bf16* __restrict__ out,
-                                                          const int* __restrict__ pos_ptr, DecodeGeom g) {
+template <bool FROM_PART>
+__global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restrict__ q, __bf16* __restrict__ kc,
+                                                          __bf16* __restrict__ vc, __bf16* __restrict__ out,
+                                                          const int* __restrict__ pos_ptr, DecodeGeom g, QkvPartials qp) {
   __shared__ float sc[DA_MAXN];
   __shared__ float red[2][4];
   __shared__ float part[4][64];
+  __shared__ float qsh[64];
   const int bh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = lane & 7, slot = lane >> 3;
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   float qd[8];
-  unpack8(*reinterpret_cast<const s16x8*>(q + (size_t)bh * 64 + sub * 8), qd);
+  if (FROM_PART) {
+    // 96 threads: (q | k | v, dim pair); the new key / value land in the caches before any lane reads them
+    if (tid < 96) {
+      const int t = tid >> 5, d = (tid & 31) * 2;
+      const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
+      const size_t col = (size_t)t * HD + h * 64 + d;
+      float y0 = 0.f, y1 = 0.f;
+      for (int k = 0; k < qp.KS; ++k) {
+        const float2 pv = *reinterpret_cast<const float2*>(qp.part + ((size_t)k * qp.B + b) * 3 * HD + col);
+        y0 += pv.x;
+        y1 += pv.y;
+      }
+      const float c0 = qp.cosT[pos * 64 + d], c1 = qp.cosT[pos * 64 + d + 1];
+      const float s0 = qp.sinT[pos * 64 + d], s1 = qp.sinT[pos * 64 + d + 1];
+      float r0 = y0 * c0 + y1 * s0, r1 = y1 * c1 + y0 * s1;
+      if (t == 0) {  // rounded to bf16 as the cached-q path stores it
+        qsh[d] = bf2f(f2bf(r0 * qp.qscale));
+        qsh[d + 1] = bf2f(f2bf(r1 * qp.qscale));
+      } else {
+        __bf16* dst = (t == 1 ? kc : vc) + ((size_t)bh * g.n + pos) * 64 + d;
+        *reinterpret_cast<uint32_t*>(dst) = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qd[e] = qsh[sub * 8 + e];
+  } else {
+    unpack8(*reinterpret_cast<const s16x8*>(q + (size_t)bh * 64 + sub * 8), qd);
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
   int nloc, r0 = 0, c0 = 0, nr = 0, nc = 1;
@@ -289,14 +376,22 @@ __global__ void vq_embed_kernel(const int64_t* __restrict__ idx, const float* __
   z[gid] = codebook[code * C + c];
 }
 
-void decode_ln_shift(const float* x, const float* w, const float* b, void* hist, void* y, const int* pos, const DecodeGeom& g,
-                     int B, int D, int shift, hipStream_t st) {
+void decode_ln_shift(float* x, const float* w, const float* b, void* hist, void* y, const int* pos, const DecodeGeom& g,
+                     int B, int D, int shift, hipStream_t st, const float* part, const void* pbias, const float* pscale, int KS) {
+  const PendingRes pr{part, (const __bf16*)pbias, pscale, KS};
   switch (D) {
-    case 256: hipLaunchKernelGGL(decode_ln_shift_kernel<256>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
-    case 512: hipLaunchKernelGGL(decode_ln_shift_kernel<512>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
-    case 1024: hipLaunchKernelGGL(decode_ln_shift_kernel<1024>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
-    case 2048: hipLaunchKernelGGL(decode_ln_shift_kernel<2048>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift); break;
+    case 256: hipLaunchKernelGGL(decode_ln_shift_kernel<256>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 512: hipLaunchKernelGGL(decode_ln_shift_kernel<512>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 1024: hipLaunchKernelGGL(decode_ln_shift_kernel<1024>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 2048: hipLaunchKernelGGL(decode_ln_shift_kernel<2048>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
   }
+}
+
+void residual_from_partials(float* x, const float* part, const void* pbias, const float* pscale, int KS, int B, int D,
+                            hipStream_t st) {
+  const PendingRes pr{part, (const __bf16*)pbias, pscale, KS};
+  const long t = (long)B * D / 4;
+  hipLaunchKernelGGL(residual_from_partials_kernel, dim3((t + 255) / 256), dim3(256), 0, st, x, pr, B, D);
 }
 
 void decode_rope(const void* qkv, const float* cosT, const float* sinT, void* q, void* kc, void* vc, const int* pos,
@@ -306,10 +401,15 @@ void decode_rope(const void* qkv, const float* cosT, const float* sinT, void* q,
                      (__bf16*)q, (__bf16*)kc, (__bf16*)vc, pos, g, B, qscale);
 }
 
-void decode_attn(const void* q, const void* kc, const void* vc, void* out, const int* pos, const DecodeGeom& g, int B,
-                 hipStream_t st) {
-  hipLaunchKernelGGL(decode_attn_kernel, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vc,
-                     (__bf16*)out, pos, g);
+void decode_attn(const void* q, void* kc, void* vc, void* out, const int* pos, const DecodeGeom& g, int B, hipStream_t st) {
+  hipLaunchKernelGGL(decode_attn_kernel<false>, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)q, (__bf16*)kc, (__bf16*)vc,
+                     (__bf16*)out, pos, g, QkvPartials{});
+}
+
+void decode_attn_part(const float* part, int KS, const float* cosT, const float* sinT, float qscale, void* kc, void* vc, void* out,
+                      const int* pos, const DecodeGeom& g, int B, hipStream_t st) {
+  hipLaunchKernelGGL(decode_attn_kernel<true>, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)nullptr, (__bf16*)kc, (__bf16*)vc,
+                     (__bf16*)out, pos, g, QkvPartials{part, cosT, sinT, KS, B, qscale});
 }
 
 void vq_embed(const int64_t* idx, const float* codebook, float* z, int HW, int C, int B, hipStream_t st) {

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
   // Partials are written and read with agent-scope (device-coherent, L2-bypassing `sc1`) accesses and
   // ordered by vmcnt + barrier only: a __threadfence() here would write back and invalidate the L2
   // of the XCD on every workgroup (measured 5x slower).
-  if (a.KS > 1) {
+  if (a.KS > 1 && EPI != 4) {
 #pragma unroll
     for (int c = 0; c < PPT; ++c) {
       const int idx = tid + c * NT;
@@ -173,6 +173,10 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
     const int row = idx / PR, col = n0 + 2 * (idx % PR);
     if (row >= a.M) continue;
     float y0 = v[c][0][0], y1 = v[c][0][1];
+    if (EPI == 4) {  // raw split-K partial slab ks: the consuming kernel sums the KS slabs (+ bias)
+      *reinterpret_cast<float2*>(reinterpret_cast<float*>(a.out) + ((size_t)ks * a.M + row) * a.N + col) = make_float2(y0, y1);
+      continue;
+    }
     if (bias != nullptr) { y0 += (float)bias[col]; y1 += (float)bias[col + 1]; }
     if (EPI == 0) {
       if (a.out_f32) {
@@ -295,6 +299,29 @@ static void skinny_launch(const SkinnyArgs& a, dim3 grid, int NBV, int WK, hipSt
   if (a.M <= 16) skinny_launch_nb<1, EPI>(a, grid, NBV, WK, st);
   else if (a.M <= 32) skinny_launch_nb<2, EPI>(a, grid, NBV, WK, st);
   else skinny_launch_nb<4, EPI>(a, grid, NBV, WK, st);
+}
+
+// Split-K partials for a consumer that sums them (EPI 4): every workgroup covers 16 columns x a
+// 128 * WK slice of K and stores its fp32 slab; no hand-off between workgroups, so K is split as finely
+// as the X bytes per CU want (the kernel is bound by the X rows each CU reads, see skinny_shape).
+static int g_part_wk = 0;
+void skinny_partials_config(int wk) { g_part_wk = wk; }
+int skinny_partials_ks(int M, int N, int K) {
+  const int chunks = K / SK_KW;
+  int wk = g_part_wk > 0 ? g_part_wk : (K >= 4096 ? 4 : 2);
+  while (wk > 1 && (chunks % wk || !skinny_valid(M, N, K, 1, 1, wk))) wk >>= 1;
+  return chunks / wk;
+}
+bool skinny_partials(SkinnyArgs a, hipStream_t st) {
+  if (a.M < 1 || a.M > 64 || a.N % 16 || a.K % SK_KW) return false;
+  const int chunks = a.K / SK_KW;
+  const int KS = skinny_partials_ks(a.M, a.N, a.K);
+  const int WK = chunks / KS;
+  if (KS != a.KS || !skinny_valid(a.M, a.N, a.K, 1, 1, WK)) return false;
+  a.steps = 1;
+  a.dbg = g_dbg;
+  skinny_launch<4>(a, dim3(a.N / 16, KS), 1, WK, st);
+  return true;
 }
 
 // Host entry (the binding validates tensors); false for unsupported shapes.

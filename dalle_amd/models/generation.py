@@ -82,6 +82,13 @@ class DecodeEngine:
         self.skinny = (use_hip and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0
                        and os.environ.get("DALLE_AMD_SKINNY", "1") != "0")
         self.sk_cnt = torch.zeros(8192, dtype=torch.int32, device=dev) if self.skinny else None
+        # split-K partials (opt-in): QKV / out-proj / FF-out leave fp32 slabs that the next kernel sums
+        # (the attention prologue, the next LayerNorm), so those GEMMs split K without a hand-off.
+        # Measured slower at batch 64 (12.6 vs 14.7 images/s): the 64-workgroup LayerNorm and the
+        # attention prologue pay more for the slab reads than the GEMMs save
+        # (profiles/r2_decode_partials_ab.txt)
+        self.partials = self.skinny and os.environ.get("DALLE_AMD_DECODE_PARTIALS", "0") == "1"
+        self._pending = None  # (stream, partial slabs, bias, LayerScale) not yet added to the stream
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
     def _wt(self, p):
@@ -104,12 +111,25 @@ class DecodeEngine:
             k.zero_()
 
     # -- branch steps -------------------------------------------------------------------------------
+    def _flush_pending(self):
+        if self._pending is not None:
+            from ..ops.hip_ops import C
+            x, part, bias, scale = self._pending
+            self._pending = None
+            C().residual_from_partials_(x, part, bias, scale)
+
     def _ln_shift(self, ls, hist, x):
         pre = ls.fn
         if self.use_hip:
             from ..ops.hip_ops import C
-            C().decode_ln_shift_(x.contiguous(), pre.norm.weight.detach(), pre.norm.bias.detach(), hist, self.hbuf, self.pos,
-                                 self.T, self.S, bool(pre.fn.enabled))
+            pend = self._pending
+            if pend is not None and pend[0] is not x:
+                self._flush_pending()
+                pend = None
+            self._pending = None
+            part, pbias, pscale = (pend[1], pend[2], pend[3]) if pend is not None else (None, None, None)
+            C().decode_ln_shift_(x, pre.norm.weight.detach(), pre.norm.bias.detach(), hist, self.hbuf, self.pos,
+                                 self.T, self.S, bool(pre.fn.enabled), part, pbias, pscale)
             return self.hbuf
         y = F.layer_norm(x, (self.d,), pre.norm.weight, pre.norm.bias)
         p = int(self.pos)
@@ -134,6 +154,13 @@ class DecodeEngine:
         from ..ops.hip_ops import C
         attn = ls.fn.fn.fn
         h = self._ln_shift(ls, self.hist[li][0], x_in)
+        if self.partials:
+            part = C().skinny_partials(h, self._wt(attn.to_qkv.weight))
+            C().decode_attn_part_(part, self.cos, self.sin, self.Dh ** -0.5, self.kc[li], self.vc[li], self.obuf, self.pos,
+                                  self.T, self.S, self.H, self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+            po = C().skinny_partials(self.obuf, self._wt(attn.to_out[0].weight))
+            self._pending = (x_res, po, self._wt(attn.to_out[0].bias), self._scale(ls))
+            return x_res
         C().skinny_qkv_rope_(h, self._wt(attn.to_qkv.weight), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li],
                              self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
         C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
@@ -150,6 +177,9 @@ class DecodeEngine:
         ff = ls.fn.fn.fn
         h = self._ln_shift(ls, self.hist[li][1], x_in)
         a = C().skinny_geglu(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias), self.sk_cnt)
+        if self.partials:
+            self._pending = (x_res, C().skinny_partials(a, self._wt(ff.net[3].weight)), self._wt(ff.net[3].bias), self._scale(ls))
+            return x_res
         C().skinny_residual_(x_res, a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias), self._scale(ls), self.sk_cnt)
         return x_res
 
@@ -217,16 +247,19 @@ class DecodeEngine:
     def _forward_position(self) -> torch.Tensor:
         W = self.model.to_logits[1].weight
         x = F.embedding(self.tok, W.detach()).float()
+        self._pending = None
         if self.cfg.reversible:
             x1, x2 = x, x.clone()
             for li, (f, g) in enumerate(self.pairs):
                 x1 = self._attn_res(li, f, x2, x1)
                 x2 = self._ff_res(li, g, x1, x2)
+            self._flush_pending()
             out = (x1 + x2) * 0.5
         else:
             for li, (f, g) in enumerate(self.pairs):
                 x = self._attn_res(li, f, x, x)
                 x = self._ff_res(li, g, x, x)
+            self._flush_pending()
             out = x
         norm, head = self.model.to_logits[0], self.model.to_logits[1]
         h = F.layer_norm(out, (self.d,), norm.weight.detach(), norm.bias.detach())
