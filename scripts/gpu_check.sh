@@ -1,4 +1,4 @@
-# Round-2 check: GPU tests, smoke, bench (step + collab engines), 2-rank gloo rehearsal on one GPU
+# GPU check: GPU tests, smoke, bench (step + collab engines), 2-rank gloo rehearsal on one GPU
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,12 +1,16 @@
 set -o pipefail
-# BASELINE configs 3 and 4 + the reference 64-layer recipe on one MI355X
+# every BASELINE config on one MI355X (bench24 step + collab engine, PowerSGD, reference recipe, 1.3B, inference)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 run() {  # name, timeout, args...
   local name=$1 t=$2; shift 2
-  timeout -k 10 "$t" python3 bench.py "$@" --profile-steps 2 > gpurun_out/cfg_$name.log 2>&1 || { echo "$name failed"; tail -30 gpurun_out/cfg_$name.log; exit 1; }
-  grep -h "metric\|phase" gpurun_out/cfg_$name.log | cut -c1-400
+  timeout -k 10 "$t" python3 bench.py "$@" --profile-steps 2 > gpurun_out/cfg_r2_$name.log 2>&1 || { echo "$name failed"; tail -30 gpurun_out/cfg_r2_$name.log; exit 1; }
+  grep -h "metric\|phase" gpurun_out/cfg_r2_$name.log | cut -c1-300
 }
 run psgd8 240 --steps 5 --warmup 2 --compression powersgd --optim-bits 8
-run ref 300 --model reference --batch 16 --steps 3 --warmup 1
-run l13 300 --model dalle-1.3b --batch 16 --steps 3 --warmup 1
+run ref48 400 --model reference --batch 48 --steps 3 --warmup 1
+run l13_32 400 --model dalle-1.3b --batch 32 --steps 3 --warmup 1
+timeout -k 10 400 python3 benchmarks/bench_inference.py --batch 64 --model bench24 --iters 2 > gpurun_out/cfg_r2_inf24.log 2>&1 || { echo "inf24 failed"; tail -20 gpurun_out/cfg_r2_inf24.log; exit 1; }
+grep metric gpurun_out/cfg_r2_inf24.log | cut -c1-300
+timeout -k 10 400 python3 benchmarks/bench_inference.py --batch 64 --model reference --iters 2 > gpurun_out/cfg_r2_infref.log 2>&1 || { echo "infref failed"; tail -20 gpurun_out/cfg_r2_infref.log; exit 1; }
+grep metric gpurun_out/cfg_r2_infref.log | cut -c1-300
