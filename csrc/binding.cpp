@@ -63,7 +63,7 @@ void decode_attn_part(const float*, int, const float*, const float*, float, void
                       hipStream_t);
 bool skinny_partials(SkinnyArgs, hipStream_t);
 int skinny_partials_ks(int, int, int);
-void skinny_partials_config(int);
+void skinny_partials_config(int, int);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
                  hipStream_t);
 void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
@@ -827,6 +827,7 @@ void decode_ln_shift_(Tensor x, Tensor w, Tensor b, Tensor hist, Tensor y, Tenso
     pp = part->data_ptr<float>();
     ps = pscale->data_ptr<float>();
     KS = part->size(0);
+    TORCH_CHECK(KS >= 1 && KS <= 16, "decode_ln_shift: at most 16 pending slabs");
     if (pbias.has_value() && pbias->defined()) {
       CHECK_IN((*pbias), torch::kBFloat16); TORCH_CHECK(pbias->numel() == D);
       pb = pbias->data_ptr();

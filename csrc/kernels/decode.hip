@@ -18,84 +18,85 @@ struct PendingRes {
   int KS;
 };
 
+// One workgroup per batch row, one thread per 4 columns (D / 4 threads: 4 waves at D = 1024), so the
+// pending slab loads of a row are spread over 4x the lanes of a one-wave row.
 template <int D>
-__global__ __launch_bounds__(64) void decode_ln_shift_kernel(float* __restrict__ x, const float* __restrict__ w,
-                                                             const float* __restrict__ bias, __bf16* __restrict__ hist,
-                                                             __bf16* __restrict__ y, const int* __restrict__ pos_ptr,
-                                                             DecodeGeom g, int shift, PendingRes pr) {
-  constexpr int PER = D / 256;
-  const int b = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(D / 4) void decode_ln_shift_kernel(float* __restrict__ x, const float* __restrict__ w,
+                                                                const float* __restrict__ bias, __bf16* __restrict__ hist,
+                                                                __bf16* __restrict__ y, const int* __restrict__ pos_ptr,
+                                                                DecodeGeom g, int shift, PendingRes pr) {
+  constexpr int NW = D / 256;  // waves per row
+  __shared__ float red[2][NW];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
   float* xr = x + (size_t)b * D;
   __bf16* hb = hist + (size_t)b * g.n * D;
-  // every load is independent of the row statistics -- the row, the LN parameters and the shifted
-  // history rows (earlier positions, written by earlier steps) -- so all of them are issued before
-  // the first reduction: one memory round trip per step instead of three
-  f32x4 v[PER], wv[PER], bv[PER], pacc[PER];
-  s16x4 sh[PER];
+  const int c = 4 * tid;
+  // every load is independent of the row statistics -- the row, the LN parameters, the pending slabs
+  // and the shifted history row (an earlier position, written by an earlier step) -- so all of them
+  // are issued before the first reduction: one memory round trip per step
   const int B = gridDim.x;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = 4 * (lane + 64 * j);
-    pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (pr.part != nullptr) {  // all (<= 8) partial slabs in flight together with the row loads
-      f32x4 t[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        t[k] = k < pr.KS ? *reinterpret_cast<const f32x4*>(pr.part + ((size_t)k * B + b) * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) pacc[j] += t[k];
-    }
-    v[j] = *reinterpret_cast<const f32x4*>(xr + c);
-    wv[j] = *reinterpret_cast<const f32x4*>(w + c);
-    bv[j] = *reinterpret_cast<const f32x4*>(bias + c);
-    sh[j] = s16x4{};
-    if (shift && c < D / 2) {
-      int src = -1;
-      if (pos < g.T) {
-        src = pos - 1;
-      } else {
-        const int k = pos - g.T;
-        if (c < D / 4) src = (k >= g.S) ? pos - g.S : -1;
-        else src = (k % g.S) ? pos - 1 : -1;
-      }
-      if (src >= 0) sh[j] = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
-    }
-  }
+  f32x4 t[16];
   if (pr.part != nullptr) {
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int c = 4 * (lane + 64 * j);
-      const f32x4 sc = *reinterpret_cast<const f32x4*>(pr.scale + c);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float bb = pr.bias ? (float)pr.bias[c + i] : 0.f;
-        v[j][i] += sc[i] * (pacc[j][i] + bb);
-      }
-      *reinterpret_cast<f32x4*>(xr + c) = v[j];
-    }
+    for (int k = 0; k < 16; ++k)
+      t[k] = k < pr.KS ? *reinterpret_cast<const f32x4*>(pr.part + ((size_t)k * B + b) * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  float s = 0.f;
+  f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+  const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
+  s16x4 sh = s16x4{};
+  if (shift && c < D / 2) {
+    int src = -1;
+    if (pos < g.T) {
+      src = pos - 1;
+    } else {
+      const int k = pos - g.T;
+      if (c < D / 4) src = (k >= g.S) ? pos - g.S : -1;
+      else src = (k % g.S) ? pos - 1 : -1;
+    }
+    if (src >= 0) sh = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
+  }
+  if (pr.part != nullptr) {
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(pr.scale + c);
+    float pb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pr.bias != nullptr) {
+      float f[4];
+      unpack4(*reinterpret_cast<const s16x4*>(pr.bias + c), f);
 #pragma unroll
-  for (int j = 0; j < PER; ++j) s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
-  const float mean = wave_sum(s) * (1.0f / D);
+      for (int i = 0; i < 4; ++i) pb[i] = f[i];
+    }
+    f32x4 acc = t[0];  // fixed ks order: deterministic
+#pragma unroll
+    for (int k = 1; k < 16; ++k) acc += t[k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += sc[i] * (acc[i] + pb[i]);
+    *reinterpret_cast<f32x4*>(xr + c) = v;
+  }
+  float s = wave_sum(v[0] + v[1] + v[2] + v[3]);
+  if (lane == 0) red[0][wave] = s;
+  __syncthreads();
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[0][i];
+  const float mean = s * (1.0f / D);
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < PER; ++j)
+  for (int i = 0; i < 4; ++i) { const float d = v[i] - mean; q += d * d; }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  q = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
-  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+  for (int i = 0; i < NW; ++i) q += red[1][i];
+  const float rstd = rsqrtf(q * (1.0f / D) + 1e-5f);
+  float o[4];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = 4 * (lane + 64 * j);
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[j][i] + bv[j][i];
-    const s16x4 packed = pack4(o);
-    *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
-    *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = (shift && c < D / 2) ? sh[j] : packed;
-  }
+  for (int i = 0; i < 4; ++i) o[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
+  const s16x4 packed = pack4(o);
+  *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
+  *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = (shift && c < D / 2) ? sh : packed;
 }
 
 // ---- rotary on q/k/v of the new token; k, v appended to the cache at `pos` ----
@@ -168,12 +169,15 @@ __device__ __forceinline__ int decode_num_keys(const DecodeGeom& g, int pos, int
   return g.T + nloc;
 }
 
+// Cache row of key i of the key list (text keys, then the local rectangle row by row). Branch-free
+// (selects only), so a loop of loads indexed by it stays one basic block and the compiler can count
+// its vmcnt statically. l / nc by a float reciprocal: l < 2^20, nc <= S, the +0.5 keeps the quotient
+// off integer edges (exact; checked against integer division for every nc <= 64, l < 2^16).
 __device__ __forceinline__ int decode_key_at(const DecodeGeom& g, int i, int pos, int r0, int c0, int nc) {
-  if (pos < g.T || i < g.T) return i;  // text keys
   const int l = i - g.T;
-  if (g.pattern == 0) return g.T + l;
-  const int rr = r0 + l / nc, cc = c0 + l % nc;
-  return g.T + rr * g.S + cc;
+  const int qd = (int)(((float)l + 0.5f) * __builtin_amdgcn_rcpf((float)nc));
+  const int local = g.pattern == 0 ? g.T + l : g.T + (r0 + qd) * g.S + c0 + l - qd * nc;
+  return (pos < g.T || i < g.T) ? i : local;
 }
 
 // ---- one query per (b, h) against its allowed cached keys ----
@@ -211,65 +215,102 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
   __shared__ float red[2][4];
   __shared__ float part[4][64];
   __shared__ float qsh[64];
+  __shared__ __attribute__((aligned(16))) __bf16 kvsh[2][64];
   const int bh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = lane & 7, slot = lane >> 3;
   const int pos = *pos_ptr;
   if (pos < 0 || pos >= g.n) return;  // a replay past the cache end is a no-op, never an OOB write
-  float qd[8];
-  if (FROM_PART) {
-    // 96 threads: (q | k | v, dim pair); the new key / value land in the caches before any lane reads them
-    if (tid < 96) {
-      const int t = tid >> 5, d = (tid & 31) * 2;
-      const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
-      const size_t col = (size_t)t * HD + h * 64 + d;
-      float y0 = 0.f, y1 = 0.f;
-      for (int k = 0; k < qp.KS; ++k) {
-        const float2 pv = *reinterpret_cast<const float2*>(qp.part + ((size_t)k * qp.B + b) * 3 * HD + col);
-        y0 += pv.x;
-        y1 += pv.y;
-      }
-      const float c0 = qp.cosT[pos * 64 + d], c1 = qp.cosT[pos * 64 + d + 1];
-      const float s0 = qp.sinT[pos * 64 + d], s1 = qp.sinT[pos * 64 + d + 1];
-      float r0 = y0 * c0 + y1 * s0, r1 = y1 * c1 + y0 * s1;
-      if (t == 0) {  // rounded to bf16 as the cached-q path stores it
-        qsh[d] = bf2f(f2bf(r0 * qp.qscale));
-        qsh[d + 1] = bf2f(f2bf(r1 * qp.qscale));
-      } else {
-        __bf16* dst = (t == 1 ? kc : vc) + ((size_t)bh * g.n + pos) * 64 + d;
-        *reinterpret_cast<uint32_t*>(dst) = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
-      }
-    }
-    __threadfence_block();
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qd[e] = qsh[sub * 8 + e];
-  } else {
-    unpack8(*reinterpret_cast<const s16x8*>(q + (size_t)bh * 64 + sub * 8), qd);
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
   int nloc, r0 = 0, c0 = 0, nr = 0, nc = 1;
   const int nkeys = decode_num_keys(g, pos, nloc, r0, c0, nr, nc);
+  const bool one_chunk = nkeys <= DA_CHUNK;
   const __bf16* kb = kc + (size_t)bh * g.n * 64 + sub * 8;
   const __bf16* vb = vc + (size_t)bh * g.n * 64 + sub * 8;
+
+  // FROM_PART: q / k / v of the new token are split-K slabs of the QKV projection (threads 0..95: q | k
+  // | v x dim pair). Every load the query needs before its first score -- q, or its slabs and rotary
+  // row -- is issued ahead of the cache stream, and all loads are unconditional (threads >= 96 load
+  // thread 95's slabs; slots past the key list re-read the last key and get probability 0), so in the
+  // single-chunk path the compiler's vmcnt counts stay static: the slab round trip and the first
+  // scores overlap the stream. The new key's cache row, read stale, is patched from LDS.
+  const int pt = min(tid, 95) >> 5, pd = (min(tid, 95) & 31) * 2;
+  float2 pv[8], cs = make_float2(0.f, 0.f), sn = make_float2(0.f, 0.f);
+  s16x8 qraw = s16x8{};
+  // issued at the top of each path's basic block, so the compiler's vmcnt counting sees them with the
+  // stream that follows (an early, separate block makes it wait for everything)
+  auto issue_q = [&]() {
+    if (FROM_PART) {
+      const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
+      const size_t col = (size_t)pt * HD + h * 64 + pd;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)  // slabs past KS re-read the last one and are weighted 0
+        pv[k] = *reinterpret_cast<const float2*>(qp.part + ((size_t)min(k, qp.KS - 1) * qp.B + b) * 3 * HD + col);
+      cs = *reinterpret_cast<const float2*>(qp.cosT + pos * 64 + pd);
+      sn = *reinterpret_cast<const float2*>(qp.sinT + pos * 64 + pd);
+    } else {
+      qraw = *reinterpret_cast<const s16x8*>(q + (size_t)bh * 64 + sub * 8);
+    }
+    asm volatile("" ::: "memory");  // keeps these loads ahead of the cache stream (hipcc sinks them otherwise)
+  };
+  float qd[8];
+  // q / k / v of the new token: q to every lane (qd), k / v to LDS and the caches
+  auto prologue = [&]() {
+    if (FROM_PART) {
+      if (tid < 96) {
+        float y0 = 0.f, y1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // fixed ks order
+          const float wk = k < qp.KS ? 1.f : 0.f;
+          y0 += wk * pv[k].x;
+          y1 += wk * pv[k].y;
+        }
+        const float ra = y0 * cs.x + y1 * sn.x, rb = y1 * cs.y + y0 * sn.y;
+        if (pt == 0) {  // rounded to bf16 as the cached-q path stores it
+          qsh[pd] = bf2f(f2bf(ra * qp.qscale));
+          qsh[pd + 1] = bf2f(f2bf(rb * qp.qscale));
+        } else {
+          const uint32_t pk = (uint32_t)f2bf(ra) | ((uint32_t)f2bf(rb) << 16);
+          *reinterpret_cast<uint32_t*>(&kvsh[pt - 1][pd]) = pk;
+          __bf16* dst = (pt == 1 ? kc : vc) + ((size_t)bh * g.n + pos) * 64 + pd;
+          *reinterpret_cast<uint32_t*>(dst) = pk;
+        }
+      }
+      __threadfence_block();  // the chunked path reads the new row back from the cache
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qd[e] = qsh[sub * 8 + e] * LOG2E;
+    } else {
+      unpack8(qraw, qd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
+    }
+  };
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
   float m, inv;
 
-  if (nkeys <= DA_CHUNK) {
+  if (one_chunk) {
     // ---- single chunk: K and V of every key in flight at once ----
     s16x8 kf[DA_U], vf[DA_U];
+    int kidx[DA_U];
+    issue_q();
 #pragma unroll
-    for (int u = 0; u < DA_U; ++u) {
-      const int i = u * 32 + wave * 8 + slot;
-      if (i < nkeys) {
-        const size_t j = (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64;
-        kf[u] = *reinterpret_cast<const s16x8*>(kb + j);
-        vf[u] = *reinterpret_cast<const s16x8*>(vb + j);
-      } else {
-        kf[u] = s16x8{};
-        vf[u] = s16x8{};
+    for (int u = 0; u < DA_U; ++u) kidx[u] = decode_key_at(g, min(u * 32 + wave * 8 + slot, nkeys - 1), pos, r0, c0, nc) * 64;
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) kf[u] = *reinterpret_cast<const s16x8*>(kb + kidx[u]);
+    asm volatile("" ::: "memory");  // every K row ahead of every V row: the scores start while V streams
+#pragma unroll
+    for (int u = 0; u < DA_U; ++u) vf[u] = *reinterpret_cast<const s16x8*>(vb + kidx[u]);
+    prologue();
+    if (FROM_PART) {  // the new key is the last of the key list
+      const s16x8 kn = *reinterpret_cast<const s16x8*>(&kvsh[0][sub * 8]);
+      const s16x8 vn = *reinterpret_cast<const s16x8*>(&kvsh[1][sub * 8]);
+#pragma unroll
+      for (int u = 0; u < DA_U; ++u) {
+        if (u * 32 + wave * 8 + slot == nkeys - 1) {
+          kf[u] = kn;
+          vf[u] = vn;
+        }
       }
     }
     float sv[DA_U];
@@ -298,6 +339,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
     if (lane == 0) red[1][wave] = ssum;
   } else {
     // ---- chunked: scores of every key into LDS, then softmax, then P.V ----
+    issue_q();
+    prologue();
     float mloc = NEG_BIG;
     for (int c = 0; c < nkeys; c += DA_CHUNK) {
       s16x8 kf[DA_U];
@@ -381,9 +424,9 @@ void decode_ln_shift(float* x, const float* w, const float* b, void* hist, void*
   const PendingRes pr{part, (const __bf16*)pbias, pscale, KS};
   switch (D) {
     case 256: hipLaunchKernelGGL(decode_ln_shift_kernel<256>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
-    case 512: hipLaunchKernelGGL(decode_ln_shift_kernel<512>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
-    case 1024: hipLaunchKernelGGL(decode_ln_shift_kernel<1024>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
-    case 2048: hipLaunchKernelGGL(decode_ln_shift_kernel<2048>, dim3(B), dim3(64), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 512: hipLaunchKernelGGL(decode_ln_shift_kernel<512>, dim3(B), dim3(128), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 1024: hipLaunchKernelGGL(decode_ln_shift_kernel<1024>, dim3(B), dim3(256), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
+    case 2048: hipLaunchKernelGGL(decode_ln_shift_kernel<2048>, dim3(B), dim3(512), 0, st, x, w, b, (__bf16*)hist, (__bf16*)y, pos, g, shift, pr); break;
   }
 }
 

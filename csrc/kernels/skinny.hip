@@ -50,7 +50,10 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
     // lane's K elements for MFMA step j: kb + j * jstr (8 each). Standard MFMA order (fq * 8, j * 32):
     // one load instruction reads 64 contiguous bytes of each of 16 rows
     const bool perm = (a.dbg & 4) != 0;
-    const int kb = ((ks * WK + wave) * steps + st) * SK_KW + fq * (perm ? 8 * SK_U : 8);
+    // dbg & 8: rotate the wave -> K-chunk map by the column tile, so the workgroups that share an XCD
+    // do not all read the same X lines at the same moment
+    const int wv = (a.dbg & 8) ? ((wave + tile) & (WK - 1)) : wave;
+    const int kb = ((ks * WK + wv) * steps + st) * SK_KW + fq * (perm ? 8 * SK_U : 8);
     const int jstr = perm ? 8 : 32;
     bf16x8 w[NB][SK_U], x[MB][SK_U];
 #pragma unroll
@@ -304,11 +307,15 @@ static void skinny_launch(const SkinnyArgs& a, dim3 grid, int NBV, int WK, hipSt
 // Split-K partials for a consumer that sums them (EPI 4): every workgroup covers 16 columns x a
 // 128 * WK slice of K and stores its fp32 slab; no hand-off between workgroups, so K is split as finely
 // as the X bytes per CU want (the kernel is bound by the X rows each CU reads, see skinny_shape).
-static int g_part_wk = 0;
-void skinny_partials_config(int wk) { g_part_wk = wk; }
+static int g_part_wk[2] = {0, 0};  // override for K < 4096 / K >= 4096 (0: measured default)
+void skinny_partials_config(int wk_small, int wk_large) {
+  g_part_wk[0] = wk_small;
+  g_part_wk[1] = wk_large;
+}
 int skinny_partials_ks(int M, int N, int K) {
   const int chunks = K / SK_KW;
-  int wk = g_part_wk > 0 ? g_part_wk : (K >= 4096 ? 4 : 2);
+  const int big = K >= 4096;
+  int wk = g_part_wk[big] > 0 ? g_part_wk[big] : (big ? 4 : 2);
   while (wk > 1 && (chunks % wk || !skinny_valid(M, N, K, 1, 1, wk))) wk >>= 1;
   return chunks / wk;
 }

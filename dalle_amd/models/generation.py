@@ -82,12 +82,18 @@ class DecodeEngine:
         self.skinny = (use_hip and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0
                        and os.environ.get("DALLE_AMD_SKINNY", "1") != "0")
         self.sk_cnt = torch.zeros(8192, dtype=torch.int32, device=dev) if self.skinny else None
-        # split-K partials (opt-in): QKV / out-proj / FF-out leave fp32 slabs that the next kernel sums
-        # (the attention prologue, the next LayerNorm), so those GEMMs split K without a hand-off.
-        # Measured slower at batch 64 (12.6 vs 14.7 images/s): the 64-workgroup LayerNorm and the
-        # attention prologue pay more for the slab reads than the GEMMs save
-        # (profiles/r2_decode_partials_ab.txt)
-        self.partials = self.skinny and os.environ.get("DALLE_AMD_DECODE_PARTIALS", "0") == "1"
+        # split-K partials: the projections leave fp32 slabs summed by their consumer, so those GEMMs
+        # split K over 4-8x the workgroups with no cross-workgroup hand-off. 2 (default): out-proj /
+        # FF-out slabs summed by the next LayerNorm, QKV slabs by the attention prologue (under the KV
+        # stream); 1: residual projections only; 0: in-GEMM split-K hand-off
+        # (profiles/r2_decode_partials_ab.txt: 4.02 -> 3.70-3.73 ms per image-position step)
+        mode = os.environ.get("DALLE_AMD_DECODE_PARTIALS", "2") if self.skinny else "0"
+        self.partials = mode in ("1", "2")
+        self.qkv_partials = mode == "2"
+        wk = os.environ.get("DALLE_AMD_PARTIALS_WK")  # "a,b": waves per workgroup for K < 4096 / K >= 4096
+        if self.partials and wk:
+            from ..ops.hip_ops import C
+            C().skinny_partials_config(*(int(v) for v in wk.split(",")))
         self._pending = None  # (stream, partial slabs, bias, LayerScale) not yet added to the stream
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
@@ -154,17 +160,19 @@ class DecodeEngine:
         from ..ops.hip_ops import C
         attn = ls.fn.fn.fn
         h = self._ln_shift(ls, self.hist[li][0], x_in)
-        if self.partials:
+        if self.qkv_partials:
             part = C().skinny_partials(h, self._wt(attn.to_qkv.weight))
             C().decode_attn_part_(part, self.cos, self.sin, self.Dh ** -0.5, self.kc[li], self.vc[li], self.obuf, self.pos,
                                   self.T, self.S, self.H, self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+        else:
+            C().skinny_qkv_rope_(h, self._wt(attn.to_qkv.weight), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li],
+                                 self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
+            C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
+                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+        if self.partials:
             po = C().skinny_partials(self.obuf, self._wt(attn.to_out[0].weight))
             self._pending = (x_res, po, self._wt(attn.to_out[0].bias), self._scale(ls))
             return x_res
-        C().skinny_qkv_rope_(h, self._wt(attn.to_qkv.weight), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li],
-                             self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
-        C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
-                         self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
         C().skinny_residual_(x_res, self.obuf, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias),
                              self._scale(ls), self.sk_cnt)
         return x_res

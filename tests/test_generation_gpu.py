@@ -16,12 +16,13 @@ def _cfg(reversible):
                           "shared_attn_ids": [0, 1, 2, 3], "shared_ff_ids": [0, 1, 0, 1]})
 
 
-@pytest.mark.parametrize("skinny", ["1", "0", "partials"])
+@pytest.mark.parametrize("skinny", ["1", "0", "handoff", "residual_partials"])
 @pytest.mark.parametrize("reversible", [False, True])
 def test_hip_decode_matches_reference_decode(cuda, reversible, skinny, monkeypatch):
-    """``partials``: QKV / out-proj / FF-out leave split-K slabs summed by the next kernel (opt-in)."""
-    monkeypatch.setenv("DALLE_AMD_DECODE_PARTIALS", "1" if skinny == "partials" else "0")
-    skinny = "1" if skinny == "partials" else skinny
+    """``1``: every projection as split-K slabs summed by its consumer (default); ``handoff``: in-GEMM
+    split-K hand-off; ``residual_partials``: slabs for the residual projections only."""
+    monkeypatch.setenv("DALLE_AMD_DECODE_PARTIALS", {"handoff": "0", "residual_partials": "1"}.get(skinny, "2"))
+    skinny = "1" if skinny in ("handoff", "residual_partials") else skinny
     monkeypatch.setenv("DALLE_AMD_SKINNY", skinny)
     torch.manual_seed(0)
     cfg = _cfg(reversible)
