@@ -97,6 +97,19 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
     return wt
 
 
+NT_INPUT_GRAD = os.environ.get("DALLE_AMD_NT_DGRAD", "1") != "0"
+
+
+def input_grad(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = g W for a Linear weight W (out, in), computed as g . (W^T)^T from the cached transposed bf16
+    copy: with W^T contiguous hipBLASLt runs the NT form of the product, 12-20 % faster than the NN form
+    at every training input-gradient shape (M = 61440: 1041 vs 895, 1230 vs 1100, 1432 vs 1192 TF/s;
+    ``benchmarks/bench_gemm_layouts.py``, profiles/r2_gemm_layouts.jsonl). DALLE_AMD_NT_DGRAD=0: NN form."""
+    if NT_INPUT_GRAD:
+        return torch.mm(g, bf16_weight_t(w).t())
+    return torch.mm(g, bf16_weight(w))
+
+
 _tables: Dict[tuple, tuple] = {}
 
 
@@ -272,7 +285,7 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, gy):
         x2, wb = ctx.saved_tensors
         g2 = _bf16c(gy.reshape(-1, gy.shape[-1]))
-        dx = torch.mm(g2, wb).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = input_grad(g2, ctx.w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = weight_grad(ctx.w, g2, x2) if ctx.needs_input_grad[1] else None
         db = torch.sum(g2, 0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db
@@ -297,7 +310,7 @@ class _FF1GEGLU(torch.autograd.Function):
         h2, a, wb = ctx.saved_tensors
         g = _bf16c(gout.reshape(a.shape[0], -1))
         da, db = C().geglu_bwd_bias(a, g)
-        dh = torch.mm(da, wb).view(ctx.hshape)
+        dh = input_grad(da, ctx.w).view(ctx.hshape)
         dw = weight_grad(ctx.w, da, h2)
         return dh, dw, db
 
@@ -324,7 +337,7 @@ class _ProjResidual(torch.autograd.Function):
         o2, y, wb, s = ctx.saved_tensors
         dy, dscale, gsum = C().scale_residual_bwd(g.contiguous(), y, s)
         dy = dy.view(-1, dy.shape[-1])
-        do = torch.mm(dy, wb).view(ctx.oshape)
+        do = input_grad(dy, ctx.w).view(ctx.oshape)
         dw = weight_grad(ctx.w, dy, o2)
         db = gsum * s
         return g, do, dw, db, dscale.view(ctx.sshape)
@@ -512,7 +525,7 @@ def _attn_core_bwd(saved, params, dy):
     B, n, T, S, K, H, pattern, shift, col = geo
     dy = dy.view(-1, dy.shape[-1])
     o2 = out.view(-1, out.shape[-1])
-    do = torch.mm(dy, wo).view(out.shape)
+    do = input_grad(dy, w_out).view(out.shape)
     dwo = _wgrad(w_out, dy, o2)
     if FUSED_ROPE_BWD:  # rotary backward inside the attention-backward epilogues
         dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
@@ -522,7 +535,7 @@ def _attn_core_bwd(saved, params, dy):
         del do
         dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
         del dq, dk, dv
-    dh = torch.mm(dqkv, wq).view(x.shape)
+    dh = input_grad(dqkv, w_qkv).view(x.shape)
     dwq = _wgrad(w_qkv, dqkv, h2)
     return dh, dwq, dwo
 
@@ -555,11 +568,11 @@ def _ff_core_bwd(saved, params, dy, sk):
         _count("ff_dgrad_geglu")
         dw2 = _wgrad(w2, dy, u)
     else:
-        du = torch.mm(dy, w2b)
+        du = input_grad(dy, w2)
         dw2 = _wgrad(w2, dy, u)
         da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
         del du
-    dh = torch.mm(da, w1b).view(x.shape)
+    dh = input_grad(da, w1).view(x.shape)
     dw1 = _wgrad(w1, da, h2)
     return dh, dw1, db1, dw2
 
