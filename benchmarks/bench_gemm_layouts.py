@@ -29,8 +29,29 @@ def timeit(fn, reps=20, warmup=3):
     return ts[len(ts) // 2]
 
 
+def wgrad(M, dev):
+    """dW (N_out, K_in) fp32 = dY^T X over M tokens, each operand stored either way (the contraction runs
+    over the tokens): which storage makes the weight-gradient GEMMs fastest."""
+    for N, K in [(3072, 1024), (1024, 1024), (8192, 1024), (1024, 4096)]:
+        g = torch.randn(M, N, device=dev).bfloat16()
+        x = torch.randn(M, K, device=dev).bfloat16()
+        gt, xt = g.t().contiguous(), x.t().contiguous()
+        out = torch.empty(N, K, device=dev, dtype=torch.float32)
+        fl = 2.0 * M * N * K
+        res = {"shape": f"wgrad_N{N}_K{K}_M{M}"}
+        # A = dY^T (N x M): a transposed view of g (cm) or gt (rm); B = X (M x K): x (rm) or xt.t() (cm)
+        for an, a in (("A_rm", gt), ("A_cm", g.t())):
+            for bn, b in (("B_rm", x), ("B_cm", xt.t())):
+                res[f"{an}_{bn}_TF"] = round(fl / timeit(lambda: torch.mm(a, b, out_dtype=torch.float32, out=out)) / 1e9)
+        print(json.dumps(res), flush=True)
+        del g, x, gt, xt, out
+        torch.cuda.empty_cache()
+
+
 def main():
     M = int(os.environ.get("M", 61440))
+    if "--wgrad" in sys.argv:
+        return wgrad(M, torch.device("cuda"))
     dev = torch.device("cuda")
     torch.manual_seed(0)
     # forward (x . W^T): (N, K) = (3072, 1024) QKV, (1024, 1024) out-proj, (8192, 1024) FF-in, (1024, 4096) FF-out;
