@@ -23,6 +23,8 @@
 // spilled, reloaded once per tile), and the exposed prologue was not the bottleneck.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dalle {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
@@ -192,7 +194,24 @@ struct RopeEpi {
   // EPI 3 / 4 (weight gradients, MN-major operands): fp32 tile stored into slab blockIdx.y of fout
   // (3) or accumulated into fout (4)
   float* fout;
+  // non-temporal epilogue output stores (DALLE_AMD_GEMM_NT_STORE=1): -5 % on the plain-store kernel at
+  // the large shapes, no gain on the fused epilogues or the full step (profiles/r2_gemm_epilogue_cost.jsonl)
+  int nt = 0;
 };
+
+// 16-byte epilogue store, non-temporal when the launch asks for it (wave-uniform branch)
+__device__ __forceinline__ void epi_store16(s16x8* dst, const s16x8& v, int nt) {
+  if (nt) __builtin_nontemporal_store(v, dst);
+  else *dst = v;
+}
+
+static int gemm_nt_store_default() {
+  static const int v = [] {
+    const char* e = getenv("DALLE_AMD_GEMM_NT_STORE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 __device__ __forceinline__ int rope_epi_seq2st(const RopeEpi& e, int p) {
   if (p < e.T) return p;
@@ -285,6 +304,17 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
                                                     int lane, const RopeEpi& rope) {
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (EPI == 5) {  // measurement only: main loop without the epilogue (results kept live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t += acc[i][j][r];
+    if (N < 0) C[lane] = (__bf16)t;
+    return;
+  }
   __bf16* ep = smem + wave * (128 * 64);
   // EPI 2: all 32 [value | gate] pre-activation loads of a lane (16 rows x 2 halves) are issued before
   // any math instead of the 8 a partially unrolled loop keeps in flight (the epilogue does not overlap
@@ -314,15 +344,23 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_s_waitcnt(0xC07F);
-  if (EPI == 0) {
+  if (EPI == 0 || EPI == 6 || EPI == 7) {  // 6: measurement only, LDS staging without the global stores
     __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
+    int t = 0;
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int idx = it * 64 + lane;
       const int row = idx >> 3, ch = idx & 7;
       const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
-      *reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8) = v;
+      if (EPI == 0) {
+        epi_store16(reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8), v, rope.nt);
+      } else if (EPI == 7) {  // non-temporal stores
+        __builtin_nontemporal_store(v, reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8));
+      } else {
+        t += v[0];
+      }
     }
+    if (EPI == 6 && N < 0) C[lane] = (__bf16)(float)t;
   } else if (EPI == 2) {
     // GEGLU backward: the staged tile is du = dy . W2 (bf16, as the unfused path rounds it) for F-columns
     // [c0, c0 + 64); each lane owns one 8-column chunk of 16 rows: da_value = du * gelu(gate),
@@ -350,8 +388,8 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
         dg[i] = d[i] * a[i] * gr;
       }
       const s16x8 pa = pack8(da), pg = pack8(dg);
-      *reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + c) = pa;
-      *reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + F + c) = pg;
+      epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + c), pa, rope.nt);
+      epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + F + c), pg, rope.nt);
       unpack8(pa, da);
       unpack8(pg, dg);
 #pragma unroll
@@ -398,7 +436,7 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
         x[i + 1] = (a1 * cs[i + 1] + a0 * sn[i + 1]) * sc;
       }
       const int srow = rope_epi_seq2st(rope, p);
-      *reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8) = pack8(x);
+      epi_store16(reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8), pack8(x), rope.nt);
     }
   }
 }
@@ -740,6 +778,18 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
                            (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, group);
         return true;
       }
+      if (epi == 350 || epi == 360 || epi == 370) {  // measurement: no epilogue / staging only / nt stores
+        if (epi == 370)
+          hipLaunchKernelGGL((gemm_nt_8ph_kernel<7, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                             (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, 4);
+        else if (epi == 350)
+          hipLaunchKernelGGL((gemm_nt_8ph_kernel<5, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                             (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, 4);
+        else
+          hipLaunchKernelGGL((gemm_nt_8ph_kernel<6, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                             (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, 4);
+        return true;
+      }
       if (epi > 400 && epi < 433) {
         hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
                            (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, -(epi - 400));
@@ -756,6 +806,7 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
                     hipStream_t st) {
   if (M % GBM || F % GBN || K % GBK) return false;
   RopeEpi e{};
+  e.nt = gemm_nt_store_default();
   e.gh = (const __bf16*)h;
   e.gdh = (__bf16*)dh;
   e.gpart = part;
@@ -805,6 +856,7 @@ bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, cons
   while ((1 << logS) < S) ++logS;
   const int Tp = (T + 31) / 32 * 32;
   RopeEpi e{(__bf16*)q, (__bf16*)k, (__bf16*)v, cosT, sinT, T, Tp, S, logS, n, Tp + S * S, H, col_major, qscale};
+  e.nt = gemm_nt_store_default();
   const int nwg = (M / GBM) * (N / GBN);
   // 8-phase staggered template: 1073 vs 1042 TF for the phased kernel at M=61440, N=3072, K=1024
   // (profiles/r1_gemm_8phase.jsonl)
