@@ -59,6 +59,7 @@ void embed_bwd(const float*, const int*, const int*, const int*, float*, float*,
 void decode_ln_shift(float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int, hipStream_t,
                      const float*, const void*, const float*, int);
 void residual_from_partials(float*, const float*, const void*, const float*, int, int, int, hipStream_t);
+void prefill_rope(const void*, const float*, const float*, void*, void*, void*, int, int, int, int, float, hipStream_t);
 void decode_attn_part(const float*, int, const float*, const float*, float, void*, void*, void*, const int*, const DecodeGeom&, int,
                       hipStream_t);
 bool skinny_partials(SkinnyArgs, hipStream_t);
@@ -866,6 +867,19 @@ void decode_attn_part_(Tensor part, Tensor cosT, Tensor sinT, double qscale, Ten
                           kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, B, cur_stream());
 }
 
+// caption prefill: qkv (B, P, 3*H*64) bf16 -> q (B*H, P, 64) rotated + pre-scaled, k / v rotated into cache rows 0..P-1
+void prefill_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, int64_t H, double qscale) {
+  CHECK_IN(qkv, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
+  CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * H * 64, "prefill_rope: qkv (B, P, 3*H*64)");
+  const int B = qkv.size(0), P = qkv.size(1);
+  TORCH_CHECK(q.numel() == (long)B * H * P * 64 && kc.dim() == 3 && kc.size(0) == B * H && kc.size(2) == 64 &&
+              kc.size(1) >= P && vc.sizes() == kc.sizes() && cosT.size(0) >= P && cosT.size(1) == 64 &&
+              sinT.sizes() == cosT.sizes(), "prefill_rope: shapes");
+  dalle::prefill_rope(qkv.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                      B, P, H, kc.size(1), (float)qscale, cur_stream());
+}
+
 void decode_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, Tensor pos, int64_t H, double qscale) {
   CHECK_IN(qkv, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
   CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
@@ -1054,6 +1068,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pos"), py::arg("T"), py::arg("S"), py::arg("shift"), py::arg("part") = py::none(),
         py::arg("pbias") = py::none(), py::arg("pscale") = py::none());
   m.def("decode_rope_", &decode_rope_);
+  m.def("prefill_rope_", &prefill_rope_);
   m.def("decode_attn_", &decode_attn_);
   m.def("skinny_linear", &skinny_linear);
   m.def("skinny_partials", &skinny_partials);

@@ -134,6 +134,52 @@ __global__ void decode_rope_kernel(const __bf16* __restrict__ qkv, const float* 
   }
 }
 
+// ---- batched caption prefill: rotary on q/k/v of positions 0..P-1; q (pre-scaled) to (B*H, P, 64),
+// k / v straight into the KV caches (one pass instead of the PyTorch rotate / convert / scatter chain) ----
+__global__ __launch_bounds__(256) void prefill_rope_kernel(const __bf16* __restrict__ qkv, const float* __restrict__ cosT,
+                                                           const float* __restrict__ sinT, __bf16* __restrict__ q_out,
+                                                           __bf16* __restrict__ kc, __bf16* __restrict__ vc, int B, int P,
+                                                           int H, int n, float qscale) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (b, p, h, chunk)
+  if (gid >= (long)B * P * H * 8) return;
+  const int chunk = gid & 7;
+  const long bph = gid >> 3;
+  const int h = bph % H;
+  const long bp = bph / H;
+  const int p = bp % P, b = bp / P;
+  const int HD = H * 64;
+  const __bf16* src = qkv + bp * 3 * HD + h * 64 + chunk * 8;
+  float c[8], sn[8];
+  *reinterpret_cast<f32x4*>(c) = *reinterpret_cast<const f32x4*>(cosT + p * 64 + chunk * 8);
+  *reinterpret_cast<f32x4*>(c + 4) = *reinterpret_cast<const f32x4*>(cosT + p * 64 + chunk * 8 + 4);
+  *reinterpret_cast<f32x4*>(sn) = *reinterpret_cast<const f32x4*>(sinT + p * 64 + chunk * 8);
+  *reinterpret_cast<f32x4*>(sn + 4) = *reinterpret_cast<const f32x4*>(sinT + p * 64 + chunk * 8 + 4);
+  const size_t bh = (size_t)b * H + h;
+  __bf16* dst[3] = {q_out + (bh * P + p) * 64 + chunk * 8, kc + (bh * n + p) * 64 + chunk * 8, vc + (bh * n + p) * 64 + chunk * 8};
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    float x[8], r[8];
+    unpack8(*reinterpret_cast<const s16x8*>(src + t * HD), x);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      r[i] = x[i] * c[i] + x[i + 1] * sn[i];
+      r[i + 1] = x[i + 1] * c[i + 1] + x[i] * sn[i + 1];
+    }
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] *= qscale;
+    }
+    *reinterpret_cast<s16x8*>(dst[t]) = pack8(r);
+  }
+}
+
+void prefill_rope(const void* qkv, const float* cosT, const float* sinT, void* q, void* kc, void* vc, int B, int P, int H, int n,
+                  float qscale, hipStream_t st) {
+  const long threads = (long)B * P * H * 8;
+  hipLaunchKernelGGL(prefill_rope_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, (const __bf16*)qkv, cosT, sinT,
+                     (__bf16*)q, (__bf16*)kc, (__bf16*)vc, B, P, H, n, qscale);
+}
+
 // the last pending update of a step (before the final LayerNorm): x += scale * (sum_ks part + bias)
 __global__ __launch_bounds__(256) void residual_from_partials_kernel(float* __restrict__ x, PendingRes pr, int B, int D) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;

@@ -339,6 +339,21 @@ class DecodeEngine:
         attn = ls.fn.fn.fn
         B, P, H, Dh = x.shape[0], x.shape[1], self.H, self.Dh
         h = self._pf_ln_shift(ls, self.hist[li][0], x)
+        if self.use_hip:
+            # one kernel rotates q / k / v and writes k / v into the caches (q pre-scaled, bf16 as in the
+            # decode steps); scores in fp32, causal over the caption
+            from ..ops.hip_ops import C
+            qkv = F.linear(h, self._wt(attn.to_qkv.weight)).contiguous()
+            q = torch.empty(B * H, P, Dh, dtype=self.cdt, device=x.device)
+            C().prefill_rope_(qkv, self.cos, self.sin, q, self.kc[li], self.vc[li], H, Dh ** -0.5)
+            k, v = self.kc[li][:, :P], self.vc[li][:, :P]
+            sc = torch.bmm(q, k.transpose(1, 2), out_dtype=torch.float32)
+            mask = static_mask(self.geom, attn.attn_type, self.n, device=x.device)[:P, :P]
+            sc.masked_fill_(~mask, float("-inf"))
+            o = torch.bmm(torch.softmax(sc, -1).to(self.cdt), v)
+            o = o.view(B, H, P, Dh).transpose(1, 2).reshape(B, P, H * Dh)
+            y = F.linear(o, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias)).float()
+            return y * self._scale(ls)
         qkv = F.linear(h, self._wt(attn.to_qkv.weight)).view(B, P, 3, H, Dh).permute(2, 0, 3, 1, 4).float()
         c, sn = self.cos[:P], self.sin[:P]
         q, k, v = (apply_rotary(t, c, sn) for t in qkv)
@@ -357,8 +372,12 @@ class DecodeEngine:
         ff = ls.fn.fn.fn
         h = self._pf_ln_shift(ls, self.hist[li][1], x)
         a = F.linear(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias))
-        val, gate = a.float().chunk(2, -1)
-        u = (val * F.gelu(gate)).to(self.cdt)
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            u = C().geglu_fwd(a.reshape(-1, a.shape[-1]).contiguous()).view(*a.shape[:-1], -1)
+        else:
+            val, gate = a.float().chunk(2, -1)
+            u = (val * F.gelu(gate)).to(self.cdt)
         return F.linear(u, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias)).float() * self._scale(ls)
 
     @torch.no_grad()
