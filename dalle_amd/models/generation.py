@@ -508,6 +508,12 @@ class SplitDecodeEngine:
         for i, p in enumerate(self.parts):
             p.prefill(text_bos[i * b:(i + 1) * b])
 
+    @torch.no_grad()
+    def prefill_parallel(self, text_bos: torch.Tensor):
+        b = self.B // self.nparts
+        for i, p in enumerate(self.parts):
+            p.prefill_parallel(text_bos[i * b:(i + 1) * b])
+
     def _capture(self):
         if self.graph is not None and self._graph_cfg == (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p):
             return
@@ -548,9 +554,7 @@ class SplitDecodeEngine:
         self._start_all(text_bos)
         if use_graph:
             self._capture()
-        b = self.B // self.nparts
-        for i, p in enumerate(self.parts):
-            p.prefill_parallel(text_bos[i * b:(i + 1) * b])
+        self.prefill_parallel(text_bos)
         for _ in range(n - (self.parts[0].T - 1)):
             if use_graph:
                 self.graph.replay()
@@ -561,12 +565,14 @@ class SplitDecodeEngine:
 
 
 def decode_parts(batch_size: int, device) -> int:
-    """How many concurrent batch-slice chains a decode engine uses: ``DALLE_AMD_DECODE_PARTS`` (default
-    1). Measured on the reference model at batch 64 (profiles/r2_decode_split_parts.txt): 2 parts
-    3.96 ms per position vs 4.01 for one chain, 4 parts 6.43 -- the half-batch chains do overlap (a
-    batch-32 chain alone takes 3.16 ms), but each skinny-GEMM workgroup occupies a whole CU, so two
-    concurrent kernels mostly run one after the other at CU granularity."""
-    n = max(1, int(os.environ.get("DALLE_AMD_DECODE_PARTS", "1")))
+    """How many concurrent batch-slice chains a decode engine uses: ``DALLE_AMD_DECODE_PARTS``, default 2
+    for batches of 32 and more (1 below). Reference model, batch 64, same box
+    (profiles/r2_decode_split_parts.txt): 2 parts 3.53 ms per image-position step and 17.0 images/s vs
+    3.74 ms / 16.0 for one chain; 4 parts 4.0-6.1 ms. With the decode kernels at a few us each, two
+    half-batch chains overlap one chain's latency-bound kernels with the other's (it measured +1 % when
+    the skinny GEMMs still carried their split-K hand-off)."""
+    default = "2" if batch_size >= 32 else "1"
+    n = max(1, int(os.environ.get("DALLE_AMD_DECODE_PARTS", default)))
     return n if batch_size % n == 0 else 1
 
 

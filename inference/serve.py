@@ -7,7 +7,8 @@ counterpart for deployment. Requests are queued and a single GPU worker thread f
 * requests with the same sampling parameters (temperature, top-k, top-p) share a batch; the worker
   waits at most ``--batch-window-ms`` for more work after the first request, up to ``--max-batch``
   images (the decode engine's skinny-GEMM path covers batches <= 64);
-* the batch is padded to the next power of two and run through a :class:`DecodeEngine` cached per
+* the batch is padded to the next power of two and run through a decode engine (two concurrent
+  :class:`DecodeEngine` chains from batch 32 on) cached per
   padded size, so every shape's hipGraph is captured once and replayed for every later batch;
 * codes are decoded by the VQGAN and returned as base64 PNGs together with per-request timings.
 
@@ -34,7 +35,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from dalle_amd.models.generation import DecodeEngine  # noqa: E402
+from dalle_amd.models.generation import DecodeEngine, make_decode_engine  # noqa: E402
 from dalle_amd.utils.logging import get_logger  # noqa: E402
 
 logger = get_logger(__name__)
@@ -152,7 +153,7 @@ class BatchingGenerator:
         ids = self._ids(prompts + [prompts[-1]] * (padded - n)).to(self.device)
         eng = self.engines.get(padded)
         if eng is None:
-            eng = self.engines[padded] = DecodeEngine(self.model, padded, device=self.device)
+            eng = self.engines[padded] = make_decode_engine(self.model, padded, device=self.device)
         temperature, top_k, top_p = batch[0].key
         t0 = time.perf_counter()
         codes = eng.generate(self.model.prepare_text(ids), temperature=temperature, top_k=top_k, top_p=top_p)[:n]
