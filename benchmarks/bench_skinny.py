@@ -46,7 +46,6 @@ def main():
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--sweep", action="store_true", help="time every (column blocks per wave, waves) shape")
     ap.add_argument("--ablate", action="store_true", help="also time with the X / W / both loads skipped")
-    ap.add_argument("--rotate", action="store_true", help="also time with the wave -> K-chunk map rotated per column tile")
     args = ap.parse_args()
     from dalle_amd.ops.hip_ops import C
     dev = torch.device("cuda")
@@ -99,8 +98,6 @@ def main():
             configs += [(nbv, wk, ks, 0) for nbv in (1, 2) for wk in (2, 4, 8) for ks in (1, 2, 4)]
         if args.ablate:
             configs += [(0, 0, 0, 1), (0, 0, 0, 2), (0, 0, 0, 3), (0, 0, 0, 4), (0, 0, 0, 5)]
-        if args.rotate:
-            configs += [(0, 0, 0, 8), (0, 0, 0, 12)]
         seen = set()
         for nbv, wk, ks, dbg in configs:
             C().skinny_force_config(nbv, wk, ks, dbg)

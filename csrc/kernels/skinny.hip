@@ -50,10 +50,7 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
     // lane's K elements for MFMA step j: kb + j * jstr (8 each). Standard MFMA order (fq * 8, j * 32):
     // one load instruction reads 64 contiguous bytes of each of 16 rows
     const bool perm = (a.dbg & 4) != 0;
-    // dbg & 8: rotate the wave -> K-chunk map by the column tile, so the workgroups that share an XCD
-    // do not all read the same X lines at the same moment
-    const int wv = (a.dbg & 8) ? ((wave + tile) & (WK - 1)) : wave;
-    const int kb = ((ks * WK + wv) * steps + st) * SK_KW + fq * (perm ? 8 * SK_U : 8);
+    const int kb = ((ks * WK + wave) * steps + st) * SK_KW + fq * (perm ? 8 * SK_U : 8);
     const int jstr = perm ? 8 : 32;
     bf16x8 w[NB][SK_U], x[MB][SK_U];
 #pragma unroll
