@@ -97,3 +97,28 @@ def test_vq_embed_kernel(cuda):
     assert torch.allclose(z, ref.view(2, 8, 8, 32).permute(0, 3, 1, 2))
     img = vae.decode(codes)
     assert img.shape == (2, 3, 16, 16)
+
+
+@pytest.mark.parametrize("mode", ["2", "0"])
+def test_decode_long_full_attention_chunked(cuda, mode, monkeypatch):
+    """Full attention past 384 keys takes the chunked two-pass decode-attention path -- in mode 2 with
+    the new token's q / k / v summed from the QKV slabs in its prologue: compare with the PyTorch
+    decode over a 64 + 32x32 sequence."""
+    monkeypatch.setenv("DALLE_AMD_DECODE_PARTIALS", mode)
+    torch.manual_seed(0)
+    c = tiny(False)
+    cfg = DALLEConfig(**{**c.to_dict(), "image_size": 256, "depth": 2, "attn_types": ["full", "axial_row"],
+                          "shared_attn_ids": [0, 1], "shared_ff_ids": [0, 1]})
+    assert cfg.text_seq_len + cfg.image_seq_len > 384
+    m = DALLE(cfg).eval()
+    B = 2
+    text = torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len))
+    img = torch.randint(0, cfg.num_image_tokens, (B, cfg.image_seq_len))
+    ref = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False).teacher_forced_logits(m.prepare_text(text), img)
+    mg = m.to(cuda)
+    eng = DecodeEngine(mg, B, device=cuda, use_hip=True)
+    assert eng.skinny and eng.qkv_partials == (mode == "2")
+    out = eng.teacher_forced_logits(mg.prepare_text(text.to(cuda)), img.to(cuda)).cpu()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    assert (out.argmax(-1) == ref.argmax(-1)).float().mean().item() > 0.9
