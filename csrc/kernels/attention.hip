@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   store_pair(0);
   __syncthreads();
   for (int pi = 0; pi < npairs; ++pi) {
-    const bool more = pi + 1 < npairs;
+    const bool more = pi + 1 < npairs && !(g.diag & 1);
     if (more) load_pair(pi + 1);
     const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
     const int ta = 2 * pi, tb = 2 * pi + 1;
@@ -414,11 +414,11 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
       fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
     if (more) store_pair((pi + 1) & 1);
-    __syncthreads();
+    if (!(g.diag & 2)) __syncthreads();
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
-  if (active && qb >= ntext) {
+  if (active && qb >= ntext && !(g.diag & 4)) {
     __bf16* P = smem + wave * (2 * TILE);
     const int lo = local_lo_tile(g, qb);
     s16x8 kr[4], vr[4];
