@@ -32,6 +32,22 @@ __device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >
 __device__ __forceinline__ int lds_idx(int r, int col) { return r * 64 + ((((col >> 3) ^ swz(r)) << 3) | (col & 7)); }
 constexpr int TILE = 32 * 64;  // elements of one 32-row tile image
 
+// LDS-DMA staging of one 32-row tile image (no VGPRs, no ds_write): wave w moves rows 8w .. 8w+7 as one
+// 1 KiB global_load_lds_dwordx4 piece. The DMA writes lane-linearly (lane l -> row 8w + l/8, physical
+// chunk l%8), so the swizzle goes on the SOURCE: that lane fetches logical chunk (l%8) ^ swz(row).
+__device__ __forceinline__ void dma_tile(const __bf16* src_rows, __bf16* tile, int wave, int lane) {
+  const int row = 8 * wave + (lane >> 3);
+  const __bf16* gp = src_rows + (size_t)row * 64 + (((lane & 7) ^ swz(row)) << 3);
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gp,
+                                   (void __attribute__((address_space(3)))*)(tile + 512 * wave), 16, 0, 0);
+}
+// a whole tile moved by ONE wave (4 pieces)
+__device__ __forceinline__ void dma_tile_wave(const __bf16* src_rows, __bf16* tile, int lane) {
+#pragma unroll
+  for (int piece = 0; piece < 4; ++piece) dma_tile(src_rows, tile, piece, lane);
+}
+constexpr int WAIT_VM0 = 0x0F70;  // s_waitcnt vmcnt(0) (expcnt / lgkmcnt untouched)
+
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ int st2seq(const AttnGeom& g, int s) {
@@ -368,41 +384,36 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   const int my_text_end = active ? min(qb + 1, ntext) : 0;
   const int qs = qb * 32 + c32;
   bf16x8 qf[4];
-  {
-    const __bf16* qp = Q + base + (size_t)(active ? qs : 0) * 64 + 8 * hl;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = ld16(qp + 16 * s);
-  }
+  // this wave's Q tile (32 contiguous rows) by LDS-DMA into buffer 1, which the loop first refills at
+  // step 0: 4 coalesced 1 KiB pieces instead of per-lane row reads that touch 32 lines per instruction
+  dma_tile_wave(Q + base + (size_t)(active ? qb : 0) * 32 * 64, smem + 4 * TILE + wave * TILE, lane);
   SoftmaxState st;
 
   // ---- phase A: shared text tiles, two per step ----
-  const int st_row = tid >> 3, st_col = (tid & 7) * 8;
-  const int st_off = lds_idx(st_row, st_col);
   const int npairs = (n_text + 1) >> 1;
-  s16x8 sreg[4];  // Ka, Kb, Va, Vb chunks of this thread
-  auto load_pair = [&](int pi) {
+  // {Ka, Kb, Va, Vb} of a pair step by LDS-DMA straight into buffer `buf` (dma_tile)
+  auto dma_pair = [&](int pi, int buf) {
     const int ta = 2 * pi, tb = min(2 * pi + 1, n_text - 1);
-    const size_t oa = base + (size_t)(ta * 32 + st_row) * 64 + st_col;
-    const size_t ob = base + (size_t)(tb * 32 + st_row) * 64 + st_col;
-    sreg[0] = *reinterpret_cast<const s16x8*>(Kt + oa);
-    sreg[1] = *reinterpret_cast<const s16x8*>(Kt + ob);
-    sreg[2] = *reinterpret_cast<const s16x8*>(V + oa);
-    sreg[3] = *reinterpret_cast<const s16x8*>(V + ob);
-  };
-  auto store_pair = [&](int buf) {
     __bf16* S0 = smem + buf * (4 * TILE);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<s16x8*>(S0 + i * TILE + st_off) = sreg[i];
+    dma_tile(Kt + base + (size_t)ta * 32 * 64, S0, wave, lane);
+    dma_tile(Kt + base + (size_t)tb * 32 * 64, S0 + TILE, wave, lane);
+    dma_tile(V + base + (size_t)ta * 32 * 64, S0 + 2 * TILE, wave, lane);
+    dma_tile(V + base + (size_t)tb * 32 * 64, S0 + 3 * TILE, wave, lane);
   };
-  load_pair(0);
-  store_pair(0);
+  dma_pair(0, 0);
+  __builtin_amdgcn_s_waitcnt(WAIT_VM0);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = row_operand(smem + 4 * TILE + wave * TILE, s, c32, hl);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Q is in registers before step 0 refills buffer 1
   __syncthreads();
   for (int pi = 0; pi < npairs; ++pi) {
     const bool more = pi + 1 < npairs && !(g.diag & 1);
-    if (more) load_pair(pi + 1);
+    if (more) dma_pair(pi + 1, (pi + 1) & 1);  // that buffer was released by the previous step's barrier
     const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
     const int ta = 2 * pi, tb = 2 * pi + 1;
-    if (tb < my_text_end) {
+    if (g.diag & 32) {
+    } else if (tb < my_text_end) {
       const __bf16* const Ks[2] = {S0, S0 + TILE};
       const __bf16* const Vs[2] = {S0 + 2 * TILE, S0 + 3 * TILE};
       const int kt[2] = {ta, tb};
@@ -413,7 +424,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
       const int kt[1] = {ta};
       fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
-    if (more) store_pair((pi + 1) & 1);
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next pair landed (this wave's pieces) before the barrier
     if (!(g.diag & 2)) __syncthreads();
   }
 
@@ -455,9 +466,9 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   const float ltot = half_sum(st.lsum);
   const float inv = 1.0f / ltot;
   lse[(size_t)bh * g.Np + qs] = st.m * LOG2E + log2f(ltot);
-  const int p = st2seq(g, qs);
-  if (p < 0) return;
-  __bf16* op = out + ((size_t)b * g.n + p) * (g.H * 64) + h * 64;
+  // O through the wave's private slot (free: its last reads fed the MFMAs above), then stored as whole
+  // 128-byte token rows (8 lanes x 16 B per row) instead of 8-byte pieces scattered over 32 rows
+  __bf16* Os = smem + wave * (2 * TILE);
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
     const f32x16& o = dt ? st.o1 : st.o0;
@@ -466,8 +477,17 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
       float f[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) f[i] = o[4 * gq + i] * inv;
-      *reinterpret_cast<s16x4*>(op + 32 * dt + 8 * gq + 4 * hl) = pack4(f);
+      *reinterpret_cast<s16x4*>(Os + lds_idx(c32, 32 * dt + 8 * gq + 4 * hl)) = pack4(f);
     }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * i + (lane >> 3), col = (lane & 7) * 8;
+    const s16x8 v = *reinterpret_cast<const s16x8*>(Os + lds_idx(row, col));
+    const int p = st2seq(g, qb * 32 + row);
+    if (p >= 0) *reinterpret_cast<s16x8*>(out + ((size_t)b * g.n + p) * (g.H * 64) + h * 64 + col) = v;
   }
 }
 
@@ -612,18 +632,18 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   store_pair(0);
   __syncthreads();
   for (int pi = 0; pi < npairs; ++pi) {
-    const bool more = pi + 1 < npairs;
+    const bool more = pi + 1 < npairs && !(g.diag & 1);
     if (more) load_pair(pi + 1);
     const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
     const int ta = 2 * pi, tb = 2 * pi + 1;
-    if (ta < my_text_end) dq_tile(dq0, dq1, S0, S0 + 2 * TILE, ta, qf, dof, lq, dl, g, qb, qs, lane);
-    if (tb < my_text_end) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
+    if (ta < my_text_end && !(g.diag & 32)) dq_tile(dq0, dq1, S0, S0 + 2 * TILE, ta, qf, dof, lq, dl, g, qb, qs, lane);
+    if (tb < my_text_end && !(g.diag & 32)) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
     if (more) store_pair((pi + 1) & 1);
-    __syncthreads();
+    if (!(g.diag & 2)) __syncthreads();
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
-  if (active && qb >= ntext) {
+  if (active && qb >= ntext && !(g.diag & 4)) {
     __bf16* P = smem + wave * (2 * TILE);
     const int lo = local_lo_tile(g, qb);
     s16x8 kr[4], vr[4];
@@ -935,7 +955,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
   }
   __syncthreads();
   for (int i = 0; i < nsteps; ++i) {
-    const bool more = i + 1 < nsteps;
+    const bool more = i + 1 < nsteps && !(g.diag & 8);
     if (more) load_step(i + 1);
     const int buf = i & 1;
     const int qt = kb0 + 2 * i + par;
@@ -977,7 +997,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
       dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
     }
     if (more) store_step((i + 1) & 1);
-    __syncthreads();
+    if (!(g.diag & 16)) __syncthreads();
   }
   // parity 1 waves hand their partials to the parity 0 wave of the same key block through LDS
   // (value-major layout: consecutive lanes on consecutive banks), which sums and stores

@@ -13,7 +13,7 @@ struct AttnGeom {
   int K;        // conv window
   int H;        // heads
   int pattern;  // 0 full, 1 axial_row, 2 axial_col, 3 conv_like
-  int diag = 0; // measurement only (DALLE_AMD_ATTN_DIAG): forward skips 1 = the text-tile staging, 2 = its barriers, 4 = the local tiles
+  int diag = 0;  // measurement only (DALLE_AMD_ATTN_DIAG): skip parts of a kernel -- forward / dQ: 1 = the text-tile staging, 2 = its barriers, 4 = the local tiles, 32 = the text tiles' compute; text dK/dV: 8 = the staging, 16 = its barriers
 };
 struct RopeGeom {
   int T, Tp, S, logS, n, Np, H, col_major;
