@@ -4,6 +4,7 @@
 
 * ``dalle_amd._C``       -- hand-written HIP/CDNA4 kernels (csrc/kernels, csrc/optim) + torch bindings
 * ``dalle_amd._kvstore`` -- C++ TCP key-value store with subkeys / expiration (the DHT replacement)
+* ``dalle_amd._tokenizer`` -- C++ SentencePiece-unigram caption tokenizer (the Rust ``tokenizers`` replacement)
 """
 import os
 
@@ -56,6 +57,20 @@ if os.path.exists(os.path.join(ROOT, "csrc/store/kvstore.cpp")):
             extra_compile_args=["-O2", "-std=c++17"],
         )
     )
+
+# plain pybind11 module: no torch / HIP libraries, so the data-loader can import it on its own
+import pybind11  # noqa: E402
+
+ext_modules.append(
+    Extension(
+        "dalle_amd._tokenizer",
+        ["csrc/tokenizer/tokenizer.cpp"],
+        include_dirs=[os.path.join(ROOT, "csrc/tokenizer"), pybind11.get_include()],
+        language="c++",
+        extra_compile_args={"cxx": ["-O2", "-std=c++17", "-fvisibility=hidden"]},
+        extra_link_args=["-pthread"],
+    )
+)
 
 setup(
     name="dalle_amd",
