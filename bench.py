@@ -228,6 +228,8 @@ def run_rank(args) -> None:
                 allreduce_weighted(arena.grad, 1.0, compression=comp, segments=arena.segments())  # no-op on one GPU
         else:
             reduce_grads = sync_grads.all_reduce
+            if os.environ.get("DALLE_AMD_DP_OVERLAP", "1") != "0":
+                sync_grads.attach()  # all-reduce grads that are final while the rest of backward runs
 
         def opt_step():
             reduce_grads()
@@ -333,6 +335,8 @@ def run_rank(args) -> None:
         }
         if ema is not None:
             out["collab_performance_ema_samples_per_s"] = round(ema, 3)
+        if args.engine == "step" and world > 1 and args.compression == "none":
+            out["grad_allreduce_overlapped_frac"] = round(sync_grads.last_early_elems / max(1, arena.numel), 3)
         if os.environ.get("BENCH_DUMP_PARAMS"):
             out["param_checksum"] = float(arena.data.double().sum())
         print(json.dumps(out), flush=True)

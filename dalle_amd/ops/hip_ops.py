@@ -695,6 +695,37 @@ def rev_store_budget(device) -> float:
     return max(0.0, free + idle - max(6 * 2 ** 30, 0.08 * total))
 
 
+# ---------------------------------------------------------------------------------------------
+# Data-parallel hand-off: the fused stacks' backward reports parameters whose arena grads just became
+# final (their last use in backward order), so the gradient all-reduce of those ranges can start while
+# the remaining layers' backward runs (parallel/dp.py GradSync.attach).
+# ---------------------------------------------------------------------------------------------
+_grad_ready_hook = None
+
+
+def set_grad_ready_hook(fn):
+    global _grad_ready_hook
+    prev, _grad_ready_hook = _grad_ready_hook, fn
+    return prev
+
+
+def _final_at(groups):
+    """``groups[i]`` = params used by step i (forward order); returns, per step, the params whose LAST
+    use in backward order (descending i) is step i -- i.e. whose first forward use is i."""
+    first = {}
+    for i, prm in enumerate(groups):
+        for p in prm:
+            first.setdefault(id(p), i)
+    out = [[] for _ in groups]
+    seen = set()
+    for i, prm in enumerate(groups):
+        for p in prm:
+            if first[id(p)] == i and id(p) not in seen:
+                seen.add(id(p))
+                out[i].append(p)
+    return out
+
+
 class _ReversibleFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blocks, recompute, *params):
@@ -746,6 +777,8 @@ class _ReversibleFused(torch.autograd.Function):
                 pending[k] = gr if k not in pending else pending[k] + gr
 
         stored, ctx.stored = ctx.stored, None
+        hook = _grad_ready_hook
+        final = _final_at([fa[1] + ga[1] for fa, ga in blocks]) if hook is not None else None
         with torch.no_grad():
             for bi in reversed(range(len(blocks))):
                 fa, ga = blocks[bi]
@@ -767,6 +800,8 @@ class _ReversibleFused(torch.autograd.Function):
                 del saved_f
                 dy2 = res[0]
                 collect(f_params, res[1:])
+                if final is not None and final[bi]:
+                    hook([p for p in final[bi] if id(p) not in pending])
         dx = dy1 + dy2
         return (dx, None, None, *[pending.get(id(p)) for p in ctx.params])
 
@@ -856,6 +891,9 @@ class _SequentialFused(torch.autograd.Function):
 
     @staticmethod
     def _backward(subs, saved_all, sinks, g):
+        # weight grads on the side stream (_wgrad) are not ordered before the hand-off: no early hand-off then
+        hook = _grad_ready_hook if _wgrad.stream is None else None
+        final = _final_at([prm for _, _, prm in subs]) if hook is not None else None
         with torch.no_grad():
             kind, args, prm = subs[-1]
             i_s, i_b = _SCALE_BIAS[kind]
@@ -883,6 +921,10 @@ class _SequentialFused(torch.autograd.Function):
                 else:
                     g, _, _ = C().ln_shift_bwd(x, prm[0].contiguous(), dh, mean, rstd, T, S, shift, g, sk[0], sk[1])
                 del sv
+                # sublayer i's LayerScale / bias grads were written one iteration earlier (its successor's
+                # LN backward), its weights and LN grads just now
+                if final is not None and final[i]:
+                    hook(final[i])
         return g
 
 

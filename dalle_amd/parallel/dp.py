@@ -4,10 +4,18 @@ The gradient arena is one contiguous buffer (``FlatArena``), so a bucket is just
 unpack copies. Buckets are sized for the xGMI mesh: each of the 8 GPUs has 7
 point-to-point links; RCCL splits an all-reduce into per-peer slices, and a 64 MB bucket keeps each
 per-link slice at >= 4 MB, past the latency-bound regime, while still pipelining several
-collectives. With weight sharing (5 blocks reused by every layer, tied embedding) no gradient is
-final before the end of backward, so all buckets are issued after ``backward()``: RCCL runs them on
-its own stream back to back, and the compute stream only waits for them (``Work.wait`` is a stream
-dependency, not a host block) before the optimizer kernels -- nothing overlaps the all-reduce itself.
+collectives.
+
+Overlap with backward (``attach()``): the fused stacks' backward (``hip_ops._SequentialFused`` /
+``_ReversibleFused``) reports the parameters whose arena grads have just become final -- a layer's
+own weights right after its backward in an unshared model (the 1.3B preset), a shared block's after
+the LAST layer that reuses it (the first in forward order) -- and ``notify`` launches their
+all-reduce right there, asynchronously: RCCL's stream waits for the kernels that produced those grads
+and then runs beside the remaining backward layers. ``all_reduce()`` after ``backward()`` only sends
+what is left (tied embedding / head, final LayerNorm) and waits. In the bench24 / reference presets
+(5 blocks reused by every layer) two thirds of the bytes become final during the last five layers'
+backward; in an unshared model almost everything overlaps. Requires one ``all_reduce()`` per
+``backward()`` (no local accumulation across micro-batches while attached).
 
 ``grad_dtype='bf16'`` halves the bytes on the wire (the averaged gradient is accumulated in fp32
 by RCCL's reduction of bf16 inputs is bf16 -- use for large worlds only).
@@ -30,9 +38,66 @@ class GradSync:
         self.group = group
         self.grad_dtype = grad_dtype
         self.average = average
-        elems = max(1, bucket_bytes // 4)
+        self.bucket_elems = max(1, bucket_bytes // 4)
+        elems = self.bucket_elems
         self.buckets = [(s, min(s + elems, arena.numel)) for s in range(0, arena.numel, elems)]
         self._lowp = None
+        self._range = {id(p): (o, (p.numel() + arena.align - 1) // arena.align * arena.align)
+                       for p, o in zip(arena.params, arena.offsets)}
+        self._sent = []   # (start, end) arena ranges already launched this step
+        self._works = []
+        self._attached = False
+        self.early_elems = 0  # elements launched from inside backward in the current step
+        self.last_early_elems = 0  # ... and in the last completed step (diagnostics)
+
+    # -------------------------------------------------------------------- overlap with backward
+    def attach(self):
+        """Let the fused backward hand over final grads as soon as they exist (see module doc)."""
+        if self.world_size > 1 and self.grad_dtype == "fp32":
+            from ..ops import hip_ops
+
+            hip_ops.set_grad_ready_hook(self.notify)
+            self._attached = True
+        return self
+
+    def detach(self):
+        if self._attached:
+            from ..ops import hip_ops
+
+            hip_ops.set_grad_ready_hook(None)
+            self._attached = False
+
+    def _launch(self, s: int, e: int):
+        g = self.arena.grad
+        for b in range(s, e, self.bucket_elems):
+            self._works.append(dist.all_reduce(g[b:min(e, b + self.bucket_elems)], group=self.group, async_op=True))
+        self._sent.append((s, e))
+
+    @torch.no_grad()
+    def notify(self, params):
+        """All-reduce the arena ranges of ``params`` now (their grads are final for this step)."""
+        if self.world_size <= 1:
+            return
+        rs = sorted(self._range[id(p)] for p in params if id(p) in self._range)
+        merged = []
+        for o, n in rs:
+            if merged and o <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], o + n)
+            else:
+                merged.append([o, o + n])
+        for s, e in merged:
+            self._launch(s, e)
+            self.early_elems += e - s
+
+    def _remaining(self):
+        out, cur = [], 0
+        for s, e in sorted(self._sent):
+            if s > cur:
+                out.append((cur, s))
+            cur = max(cur, e)
+        if cur < self.arena.numel:
+            out.append((cur, self.arena.numel))
+        return out
 
     @torch.no_grad()
     def all_reduce(self):
@@ -49,8 +114,11 @@ class GradSync:
                 w.wait()
             g.copy_(lp)
         else:
-            works = [dist.all_reduce(g[s:e], group=self.group, async_op=True) for s, e in self.buckets]
-            for w in works:
+            for s, e in self._remaining():
+                self._launch(s, e)
+            for w in self._works:
                 w.wait()
+            self._works, self._sent = [], []
+            self.last_early_elems, self.early_elems = self.early_elems, 0
         if self.average:
             g.mul_(1.0 / self.world_size)

@@ -67,8 +67,8 @@ ext_modules.append(
         ["csrc/tokenizer/tokenizer.cpp"],
         include_dirs=[os.path.join(ROOT, "csrc/tokenizer"), pybind11.get_include()],
         language="c++",
-        extra_compile_args={"cxx": ["-O2", "-std=c++17", "-fvisibility=hidden"]},
-        extra_link_args=["-pthread"],
+        extra_compile_args={"cxx": ["-O2", "-std=c++17", "-fvisibility=hidden", "-g0"]},
+        extra_link_args=["-pthread", "-s"],
     )
 )
 

@@ -301,3 +301,38 @@ def test_reference_geometry_end_to_end(cuda, reversible):
         worst = max(worst, rel)
         assert rel < 0.05, (name, rel)
     print(f"reference geometry: loss {loss.item():.5f} vs {loss_ref.item():.5f}, worst grad rel err {worst:.4f}")
+
+
+@pytest.mark.parametrize("reversible", [False, True])
+def test_grad_ready_handoff_reports_final_grads(cuda, reversible):
+    """The fused stacks' backward hands every stack parameter to the data-parallel hook exactly once, and
+    only when its arena grad is final (GradSync.attach all-reduces it right there, beside the rest of
+    backward): the value seen at hand-off equals the value after backward, shared blocks included."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = _cfg(reversible)
+    m = DALLE(cfg).to(cuda)
+    arena = FlatArena(m.parameters(), device=cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+    seen = {}
+
+    def record(params):
+        for p in params:
+            assert id(p) not in seen, "parameter handed over twice"
+            seen[id(p)] = (p, p.grad.detach().clone())  # stream-ordered copy of the value at hand-off
+
+    prev = hip_ops.set_grad_ready_hook(record)
+    try:
+        arena.zero_grad()
+        m(text, img, return_loss=True).backward()
+        torch.cuda.synchronize()
+    finally:
+        hip_ops.set_grad_ready_hook(prev)
+    stack = {id(p) for n, p in m.named_parameters() if ".layers." in n or "transformer" in n}
+    assert len(seen) > 0 and len(seen) >= len(stack) // 2, (len(seen), len(stack))
+    for p, g_at in seen.values():
+        assert torch.equal(g_at, p.grad), "grad changed after it was handed over"
+    # the tied embedding / head and the final norm are not stack parameters: never handed over early
+    assert id(m.to_logits[1].weight) not in seen
