@@ -508,9 +508,16 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
 
     def _collective_part(self, grad_scaler):
         self.tracker.report_local_progress(self.local_epoch, self.grad_averager.local_samples_accumulated)
-        if self.tracker.mode in ("collective", "dht") and self.tracker.max_epoch_seen > self.local_epoch + 1:
-            # the lockstep tracker saw the epochs of all peers: the decision is identical on every rank
-            logger.info(f"local epoch {self.local_epoch} lags the collaboration ({self.tracker.max_epoch_seen}); loading state")
+        tr = self.tracker
+        if tr.mode == "collective":
+            # load_state_from_peers is a collective: decide on (min, max) epoch, which the lockstep
+            # tracker's reduction gives every rank identically -- up-to-date ranks join as donors
+            lagging = tr.min_epoch_seen is not None and tr.min_epoch_seen < tr.max_epoch_seen - 1
+        else:
+            lagging = tr.mode == "dht" and tr.max_epoch_seen > self.local_epoch + 1
+        if lagging:
+            logger.info(f"epochs {tr.min_epoch_seen if tr.mode == 'collective' else self.local_epoch}..{tr.max_epoch_seen} "
+                        f"diverged (local {self.local_epoch}); loading state from the newest peer")
             self.load_state_from_peers()
             self.grad_averager.reset_accumulated_grads_()
             return

@@ -122,6 +122,7 @@ class ProgressTracker:
         self.local_progress = LocalTrainingProgress(peer_id, 0, 0, 0.0, get_dht_time(), client_mode)
         self.global_progress = GlobalTrainingProgress(0, 0, target_batch_size, 1, int(client_mode), float("inf"), 0.0)
         self.max_epoch_seen = 0
+        self.min_epoch_seen = None  # "collective" mode: the lowest epoch of any peer at the last update
         self._last_report = 0.0
         self._epoch_start = time.perf_counter()
         self._publish_lock = threading.Lock()
@@ -182,12 +183,14 @@ class ProgressTracker:
         lp = self.local_progress
         dt = torch.float64 if self.device.type == "cpu" else torch.float32
         s = torch.tensor([lp.samples_accumulated, lp.samples_per_second, 1.0, float(lp.client_mode)], dtype=dt, device=self.device)
-        e = torch.tensor([float(lp.epoch)], dtype=dt, device=self.device)
+        e = torch.tensor([float(lp.epoch), -float(lp.epoch)], dtype=dt, device=self.device)
         dist.all_reduce(s, group=self.group)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)  # (max epoch, -min epoch)
         s = s.tolist()
-        max_epoch = int(e.item())
+        e = e.tolist()
+        max_epoch = int(e[0])
         self.max_epoch_seen = max_epoch
+        self.min_epoch_seen = int(-e[1])
         total, sps, peers, clients = int(round(s[0])), s[1], int(round(s[2])), int(round(s[3]))
         remaining = max(0, self.target_batch_size - total)
         eta = get_dht_time() + (remaining / sps if sps > 0 else float("inf"))

@@ -309,3 +309,35 @@ def test_dead_peer_mid_averaging_survivors_fall_back_and_continue():
         assert abs(upd[0] - 2.0) < 1e-5, upd
         assert abs(upd[1] - (rank + 1) * 2.0) < 1e-5, upd
         assert abs(upd[3] - (rank + 1) * 4.0) < 1e-5, upd
+
+
+# ------------------------------------------------------------------------------------------------
+def _lagging_collective_worker(rank, world, port, q):
+    """Lockstep ("collective") tracker with one peer two epochs behind (e.g. it restored an old local
+    backup): the resync is a collective, so EVERY rank must take it -- the laggard as receiver, the
+    others as donors -- or the group deadlocks on mismatched collectives."""
+    try:
+        _init(rank, world, port)
+        from dalle_amd.parallel.optimizer import CollaborativeOptimizer
+
+        torch.manual_seed(rank)
+        p = torch.nn.Parameter(torch.randn(50, 40))
+        opt = CollaborativeOptimizer(run_id="lag", params=[p], optimizer=lambda ps: torch.optim.SGD(ps, lr=0.1),
+                                     target_batch_size=4, batch_size_per_step=2, reuse_grad_buffers=True,
+                                     average_state_every=0, tracker_mode="collective")
+        opt.local_epoch = 5 if rank == 0 else 2
+        opt.tracker.update_epoch(opt.local_epoch)
+        p.grad = torch.ones_like(p)
+        opt.step()
+        q.put(pickle.dumps((rank, opt.local_epoch, p.detach().clone())))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put(pickle.dumps(("error", rank, traceback.format_exc())))
+
+
+def test_collective_tracker_resyncs_lagging_peer_on_every_rank():
+    (r0, e0, p0), (r1, e1, p1) = _run(_lagging_collective_worker, 2)
+    assert e0 == e1 == 5
+    assert torch.equal(p0, p1)
