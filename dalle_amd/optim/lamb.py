@@ -64,11 +64,11 @@ class LAMB8bit(torch.optim.Optimizer):
             raise ValueError("Invalid clamp value: {}".format(clamp_value))
         if optim_bits not in (8, 32):
             raise NotImplementedError(f"Amount of optimizer bits not supported: {optim_bits}")
-        self.clamp_value = clamp_value
-        self.bias_correction = bias_correction
-        self.reuse_grad_buffers = reuse_grad_buffers
-        self.update_chunk_size = update_chunk_size
-        self.max_grad_norm = max_grad_norm
+        # non-group options (CPULAMB8Bit keeps them as attributes; state_dict compatibility needs the names)
+        for name, val in (("clamp_value", clamp_value), ("bias_correction", bias_correction),
+                          ("reuse_grad_buffers", reuse_grad_buffers), ("update_chunk_size", update_chunk_size),
+                          ("max_grad_norm", max_grad_norm)):
+            setattr(self, name, val)
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, optim_bits=optim_bits,
                         min_8bit_size=min_8bit_size, percentile_clipping=100, block_wise=block_wise, max_unorm=0.0)
         super().__init__(params, defaults)

@@ -77,6 +77,12 @@ def generate(query, *, tokenizer, model, batch_size, n_iters, temperature, top_k
     return result
 
 
+def load_queries(path: str):
+    """One caption per line; trailing whitespace dropped, empty lines skipped (the reference's format)."""
+    with open(path, encoding="utf-8") as fh:
+        return [q for q in (raw.rstrip() for raw in fh) if q]
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser()
     parser.add_argument('--queries', type=str, help='List of queries (*.txt, newline-separated)')
@@ -95,9 +101,7 @@ def main(argv=None):
     args = parser.parse_args(argv)
     torch.set_grad_enabled(False)  # inference only (the reference disabled grads at import time)
 
-    with open(args.queries) as f:
-        queries = [line.rstrip() for line in f]
-        queries = [item for item in queries if len(item) > 0]
+    queries = load_queries(args.queries)
     print(f'[*] Loaded {len(queries)} queries')
 
     device = "cuda" if torch.cuda.is_available() else "cpu"
