@@ -6,7 +6,10 @@ locally (nmt_nfkc normalisation -> the same precompiled-charsmap pipeline t5-sma
 them with transformers' own slow->fast converter; parity on the real t5-small vocabulary is unpinned.
 """
 import json
+import os
 import random
+import shutil
+import subprocess
 
 import pytest
 
@@ -127,3 +130,39 @@ def test_unsupported_pipeline_falls_back_to_library(tmp_path):
     fallback = load_tokenizer(str(tmp_path))
     assert not isinstance(fallback, NativeUnigramTokenizer)
     assert fallback("a red apple", add_special_tokens=False)["input_ids"] == tok.encode("a red apple").ids
+
+
+SANITIZERS = {
+    "tsan": ["-fsanitize=thread"],
+    "asan_ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+}
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+@pytest.mark.parametrize("kind", sorted(SANITIZERS))
+def test_tokenizer_core_under_sanitizers(kind, t5_dir, tmp_path):
+    """Random / invalid UTF-8 through the pybind-free core on 4 threads sharing one pipeline, under
+    TSan and ASan+UBSan, with the trained model's vocabulary and precompiled charsmap."""
+    import base64
+
+    spec = json.load(open(t5_dir / "tokenizer.json"))
+    with open(tmp_path / "vocab.tsv", "wb") as f:
+        for piece, score in spec["model"]["vocab"]:
+            f.write(piece.encode() + b"\t" + repr(float(score)).encode() + b"\n")
+    norm = spec["normalizer"]
+    steps = norm["normalizers"] if norm.get("type") == "Sequence" else [norm]
+    blob = next(st["precompiled_charsmap"] for st in steps if st.get("type") == "Precompiled")
+    (tmp_path / "charsmap.bin").write_bytes(base64.b64decode(blob))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "csrc", "tokenizer", "tokenizer_fuzz.cpp")
+    exe = str(tmp_path / f"tokenizer_fuzz_{kind}")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", *SANITIZERS[kind], "-I", os.path.dirname(src), src, "-o", exe,
+                    "-pthread"], check=True, capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="halt_on_error=1 detect_leaks=1",
+               UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1")
+    r = subprocess.run([exe, str(tmp_path), "4", "3000"], capture_output=True, text=True, timeout=240, env=env)
+    report = r.stdout + r.stderr
+    assert r.returncode == 0, report[-4000:]
+    assert "WARNING: ThreadSanitizer" not in report and "ERROR: AddressSanitizer" not in report, report[-4000:]
+    assert "runtime error:" not in report, report[-4000:]
+    assert "tokenizer fuzz ok" in r.stdout
