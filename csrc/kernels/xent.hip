@@ -98,15 +98,19 @@ void xent_fwd_bwd(void* logits, const int64_t* labels, float* loss, long R, int 
 // separate column-reduction pass over the logits disappears, deterministically.
 constexpr int XENT_RB = 16;
 constexpr int XENT_T = 1024;  // 16 waves: one workgroup per CU when the vocabulary fills the LDS
-constexpr int XENT_MAXV = 40000;  // (V + 32) floats of dynamic LDS must fit the 160 KiB per workgroup
+constexpr int XENT_MAXV = 35000;  // the padded accumulator (9/8 V floats + 32) must fit the 160 KiB per workgroup
+// column c of the LDS accumulator lives at c + c/8: a lane adds 8 consecutive columns, so unpadded the
+// 64 lanes of a wave would hit banks 8 apart (8-way conflicts, 23M per dispatch measured); with one pad
+// float per 8 columns consecutive lanes are 9 floats apart -- conflict-free
+__host__ __device__ __forceinline__ int xpad(int c) { return c + (c >> 3); }
 
 __global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict__ logits, const int64_t* __restrict__ labels,
                                                           float* __restrict__ loss, float* __restrict__ part, long R, int V,
                                                           float gscale) {
-  extern __shared__ float colacc[];  // V floats (+16 for the reductions)
-  float* red = colacc + ((V + 3) & ~3);
+  extern __shared__ float colacc[];  // xpad(V) floats (+32 for the reductions)
+  float* red = colacc + ((xpad(V) + 3) & ~3);
   const int tid = threadIdx.x;
-  for (int c = tid; c < V; c += XENT_T) colacc[c] = 0.f;
+  for (int c = tid; c < V; c += XENT_T) colacc[xpad(c)] = 0.f;
   const long r0 = (long)blockIdx.x * XENT_RB;
   for (long row = r0; row < r0 + XENT_RB && row < R; ++row) {
     __bf16* lrow = logits + row * (long)V;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict_
       if (tid == lab) g -= 1.0f;
       const bf16_raw q = f2bf(g * gscale);
       *p = q;
-      colacc[tid] += bf2f(q);
+      colacc[xpad(tid)] += bf2f(q);
     }
     const int64_t labb = lab - head;
     for (int i = tid; i < nvec; i += XENT_T) {
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict_
       *p = q;
       unpack8(q, f);  // the bias gradient sums the bf16 values the GEMMs consume
 #pragma unroll
-      for (int j = 0; j < 8; ++j) colacc[head + 8 * i + j] += f[j];
+      for (int j = 0; j < 8; ++j) colacc[xpad(head + 8 * i + j)] += f[j];
     }
     for (int i = nvec * 8 + tid; i < Vb; i += XENT_T) {
       bf16_raw* p = reinterpret_cast<bf16_raw*>(lr) + i;
@@ -187,18 +191,18 @@ __global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict_
       if (i == labb) g -= 1.0f;
       const bf16_raw q = f2bf(g * gscale);
       *p = q;
-      colacc[head + i] += bf2f(q);
+      colacc[xpad(head + i)] += bf2f(q);
     }
     __syncthreads();  // the next row may map a column to another thread
   }
   float* prow = part + (size_t)blockIdx.x * V;
-  for (int c = tid; c < V; c += XENT_T) prow[c] = colacc[c];
+  for (int c = tid; c < V; c += XENT_T) prow[c] = colacc[xpad(c)];
 }
 
 bool xent_colsum(void* logits, const int64_t* labels, float* loss, float* part, long R, int V, float gscale, hipStream_t st) {
   if (V > XENT_MAXV) return false;
   const long nblk = (R + XENT_RB - 1) / XENT_RB;
-  const size_t lds = (size_t)(((V + 3) & ~3) + 2 * (XENT_T / 64)) * sizeof(float);
+  const size_t lds = (size_t)(((xpad(V) + 3) & ~3) + 2 * (XENT_T / 64)) * sizeof(float);
   static bool attr = false;
   if (!attr) {  // dynamic LDS beyond the default cap needs an explicit per-kernel limit
     (void)hipFuncSetAttribute((const void*)xent_colsum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
