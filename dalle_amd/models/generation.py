@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 from typing import List, Optional
 
 import torch
@@ -20,6 +21,11 @@ import torch.nn.functional as F
 
 from .patterns import PATTERN_IDS, static_mask
 from .rotary import apply_rotary, rotary_tables
+
+# hipGraph captures of different engines (e.g. one serving generator per GPU, each in its own thread)
+# run one at a time, in thread-local capture mode: another thread's replays and allocations on its own
+# device neither break a capture nor are refused while it runs
+_CAPTURE_LOCK = threading.Lock()
 
 
 def filter_logits(logits: torch.Tensor, top_k: int = 0, top_p: float = 1.0) -> torch.Tensor:
@@ -446,7 +452,7 @@ class DecodeEngine:
                 self._step()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _CAPTURE_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._static_logits = self._step()
         self.graph = g
         self._graph_cfg = (self.temperature, self.top_k, self.top_p)
@@ -527,7 +533,7 @@ class SplitDecodeEngine:
                     p._step()
         main.wait_stream(warm)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _CAPTURE_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
             cap = torch.cuda.current_stream()
             for s in streams:
                 s.wait_stream(cap)

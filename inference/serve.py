@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Text -> image serving on one MI355X: an HTTP front-end over the hipGraph decode engine.
+"""Text -> image serving on MI355X: an HTTP front-end over the hipGraph decode engine, on one GPU or on
+every GPU of a node (``--devices all``: one model copy, decode-engine cache and worker thread per GPU;
+each request goes to the device with the fewest images queued).
 
 The reference only has the offline batch script (``inference/run_inference.py``); this is its online
 counterpart for deployment. Requests are queued and a single GPU worker thread forms batches:
@@ -21,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import base64
+import copy
 import io
 import os
 import queue
@@ -177,6 +180,77 @@ class BatchingGenerator:
             job.future.set_result(res)
 
 
+class MultiDeviceGenerator:
+    """One :class:`BatchingGenerator` per device (its own model copy, decode-engine cache and worker
+    thread); ``submit`` routes each request to the device with the fewest images in flight, so a node's
+    GPUs batch and decode independently. Same interface as a single generator."""
+
+    def __init__(self, model, tokenizer, devices: List[str], max_batch: int = 64, batch_window_ms: float = 20.0):
+        if not devices:
+            raise ValueError("need at least one device")
+        self.gens: List[BatchingGenerator] = []
+        for i, d in enumerate(devices):
+            m = model if i == len(devices) - 1 else copy.deepcopy(model)  # the last device takes the original
+            self.gens.append(BatchingGenerator(m.to(d).eval(), tokenizer, d, max_batch, batch_window_ms))
+        self.max_batch = self.gens[0].max_batch
+        self._inflight = [0] * len(self.gens)
+        self._lock = threading.Lock()
+
+    @property
+    def device(self) -> str:
+        return ",".join(str(g.device) for g in self.gens)
+
+    @property
+    def engines(self) -> Dict[int, DecodeEngine]:
+        out: Dict[int, DecodeEngine] = {}
+        for g in self.gens:
+            out.update(g.engines)
+        return out
+
+    @property
+    def stats(self) -> Dict[str, float]:
+        tot = {"requests": 0, "images": 0, "batches": 0, "gpu_seconds": 0.0}
+        for g in self.gens:
+            for k in tot:
+                tot[k] += g.stats[k]
+        tot["per_device_images"] = [g.stats["images"] for g in self.gens]
+        return tot
+
+    def submit(self, prompts: List[str], images_per_prompt: int = 1, temperature: float = 1.0, top_k: int = 0,
+               top_p: float = 1.0) -> Future:
+        n = len(prompts) * int(images_per_prompt)
+        with self._lock:
+            i = min(range(len(self.gens)), key=lambda k: (self._inflight[k], k))
+            self._inflight[i] += n
+        try:
+            fut = self.gens[i].submit(prompts, images_per_prompt, temperature, top_k, top_p)
+        except Exception:
+            with self._lock:
+                self._inflight[i] -= n
+            raise
+
+        def done(_f, i=i, n=n):
+            with self._lock:
+                self._inflight[i] -= n
+
+        fut.add_done_callback(done)
+        return fut
+
+    def close(self):
+        for g in self.gens:
+            g.close()
+
+
+def parse_devices(spec: str) -> List[str]:
+    """``all`` -> every visible GPU; ``0,2`` -> those GPUs; ``cpu`` -> CPU (tests); default: one device."""
+    if spec in (None, "", "auto"):
+        return ["cuda:0" if torch.cuda.is_available() else "cpu"]
+    if spec == "all":
+        n = torch.cuda.device_count()
+        return [f"cuda:{i}" for i in range(n)] if n else ["cpu"]
+    return [d if (d.startswith("cuda") or d == "cpu") else f"cuda:{int(d)}" for d in spec.split(",")]
+
+
 try:  # the HTTP layer is optional: BatchingGenerator works without fastapi / pydantic
     from pydantic import BaseModel, Field
 
@@ -190,7 +264,8 @@ except ImportError:  # pragma: no cover
     GenerateRequest = None
 
 
-def create_app(gen: BatchingGenerator):
+def create_app(gen):
+    """HTTP app around a :class:`BatchingGenerator` or :class:`MultiDeviceGenerator`."""
     from fastapi import FastAPI, HTTPException
 
     app = FastAPI(title="dalle-mi355x")
@@ -225,6 +300,7 @@ def main(argv=None):
     ap.add_argument("--vqgan-config", default=None)
     ap.add_argument("--tokenizer", default="t5-small")
     ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--devices", default="auto", help='"all" GPUs of the node, a list like "0,1,2,3", or "auto" (one)')
     ap.add_argument("--batch-window-ms", type=float, default=20.0)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
@@ -233,14 +309,18 @@ def main(argv=None):
     from dalle_amd.models.vqgan import VQGanVAE
 
     torch.set_grad_enabled(False)
-    device = "cuda" if torch.cuda.is_available() else "cpu"
+    devices = parse_devices(args.devices)
     tokenizer, wrapper = make_model(args.model_preset, args.tokenizer)
     if args.model:
         wrapper.load_state_dict(normalize_state_dict_keys(torch.load(args.model, map_location="cpu", weights_only=True)),
                                 strict=False)
     wrapper.model.vae = VQGanVAE(args.vqgan, args.vqgan_config).eval()
-    model = wrapper.model.to(device).eval()
-    gen = BatchingGenerator(model, tokenizer, device, args.max_batch, args.batch_window_ms)
+    if len(devices) == 1:
+        gen = BatchingGenerator(wrapper.model.to(devices[0]).eval(), tokenizer, devices[0], args.max_batch,
+                                args.batch_window_ms)
+    else:
+        gen = MultiDeviceGenerator(wrapper.model.eval(), tokenizer, devices, args.max_batch, args.batch_window_ms)
+    logger.info(f"serving on {gen.device}")
     import uvicorn
 
     uvicorn.run(create_app(gen), host=args.host, port=args.port)

@@ -63,3 +63,33 @@ def test_http_endpoints(gen):
     assert client.post("/generate", json={"prompts": ["x"], "images_per_prompt": 99}).status_code == 400
     s = client.get("/stats").json()
     assert s["requests"] >= 1 and s["images"] >= 2 and s["batches"] >= 1
+
+
+def test_multi_device_generator_spreads_requests():
+    """--devices: one generator (model copy, engine cache, worker thread) per device, requests routed to
+    the device with the fewest images in flight; two CPU "devices" stand in for a node's GPUs."""
+    from fastapi.testclient import TestClient
+    from serve import MultiDeviceGenerator, create_app, parse_devices
+
+    assert parse_devices("cpu,cpu") == ["cpu", "cpu"] and parse_devices("0,3") == ["cuda:0", "cuda:3"]
+    torch.manual_seed(0)
+    c = tiny(False)
+    cfg = DALLEConfig(**{**c.to_dict(), "text_seq_len": 16, "image_size": 64})
+    model = DALLE(cfg).eval()
+    g = MultiDeviceGenerator(model, HashingTokenizer(vocab_size=cfg.num_text_tokens), ["cpu", "cpu"], max_batch=4,
+                             batch_window_ms=50)
+    try:
+        futs = [g.submit([f"prompt {i}"], images_per_prompt=2, temperature=0.0) for i in range(4)]
+        res = [f.result(timeout=300) for f in futs]
+        assert all(len(r["codes"]) == 2 for r in res)
+        per = g.stats["per_device_images"]
+        assert sum(per) == 8 and min(per) > 0, per   # both devices got work
+        # greedy: the same prompt gives the same codes on either device (identical weight copies)
+        a = g.gens[0].submit(["same"], 1, temperature=0.0).result(timeout=300)["codes"]
+        b = g.gens[1].submit(["same"], 1, temperature=0.0).result(timeout=300)["codes"]
+        assert a == b
+        client = TestClient(create_app(g))
+        assert client.get("/health").json()["device"] == "cpu,cpu"
+        assert client.get("/stats").json()["images"] == 10
+    finally:
+        g.close()

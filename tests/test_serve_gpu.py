@@ -49,3 +49,27 @@ def test_serving_on_gpu(cuda):
         assert all(np.abs(a - px[0]).max() <= 1 for a in px)
     finally:
         gen.close()
+
+
+def test_multi_device_serving_concurrent_captures(cuda):
+    """Two generators (model copies, engine caches, worker threads) share the GPU here, standing in for a
+    node's devices: their first batches capture hipGraphs while the other thread replays -- captures run
+    one at a time in thread-local mode -- and greedy results match across the copies."""
+    from serve import MultiDeviceGenerator
+
+    torch.manual_seed(0)
+    cfg = tiny(False)
+    model = DALLE(cfg).eval()
+    dev = str(cuda)
+    g = MultiDeviceGenerator(model, HashingTokenizer(vocab_size=cfg.num_text_tokens), [dev, dev], max_batch=8,
+                             batch_window_ms=20)
+    try:
+        futs = [g.submit([f"p{i}"], images_per_prompt=[1, 2, 4, 8][i % 4], temperature=1.0, top_k=32) for i in range(12)]
+        res = [f.result(timeout=100) for f in futs]
+        assert sum(len(r["codes"]) for r in res) == 3 * (1 + 2 + 4 + 8)
+        assert min(g.stats["per_device_images"]) > 0
+        a = g.gens[0].submit(["same"], 4, temperature=0.0).result(timeout=100)["codes"]
+        b = g.gens[1].submit(["same"], 4, temperature=0.0).result(timeout=100)["codes"]
+        assert a == b
+    finally:
+        g.close()
