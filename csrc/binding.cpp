@@ -47,6 +47,7 @@ void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
 void embed_fwd(const int64_t*, const int64_t*, const float*, float*, int*, int*, int, int, int, int, int, int, int, int,
                hipStream_t);
 bool xent_colsum(void*, const int64_t*, float*, float*, long, int, float, hipStream_t);
+void transpose_cast_bf16(const float* w, void* wt, int R, int C, hipStream_t st);
 bool conv3x3(const ConvArgs&, hipStream_t);
 bool gn_stats(const void*, float*, float*, float*, int, int, int, float, hipStream_t);
 size_t gn_part_floats(int);
@@ -395,6 +396,15 @@ void scale_residual_(Tensor x, Tensor y, Tensor scale) {
   TORCH_CHECK(D % 8 == 0 && y.numel() == x.numel() && scale.numel() == D);
   dalle::scale_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), x.data_ptr<float>(), x.numel() / D, D,
                         cur_stream());
+}
+
+Tensor transpose_bf16(Tensor w) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kFloat32 && w.dim() == 2 && w.is_contiguous(),
+              "transpose_bf16: contiguous fp32 matrix expected");
+  TORCH_CHECK(w.size(0) < (1L << 31) && w.size(1) < (1L << 31), "transpose_bf16: matrix too large");
+  auto wt = torch::empty({w.size(1), w.size(0)}, w.options().dtype(torch::kBFloat16));
+  if (w.numel()) dalle::transpose_cast_bf16(w.data_ptr<float>(), wt.data_ptr(), (int)w.size(0), (int)w.size(1), cur_stream());
+  return wt;
 }
 
 void scale_residual_out(Tensor x, Tensor y, Tensor scale, Tensor out) {
@@ -1039,6 +1049,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ff_dgrad_geglu", &ff_dgrad_geglu, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
   m.def("scale_residual_", &scale_residual_);
   m.def("scale_residual_out", &scale_residual_out);
+  m.def("transpose_bf16", &transpose_bf16, "fp32 (R, C) -> bf16 (C, R) in one pass");
   m.def("scale_residual_bwd", &scale_residual_bwd, py::arg("g"), py::arg("y"), py::arg("scale"),
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);

@@ -311,4 +311,30 @@ void zero_if_flag(float* x, long n, const int* flag, hipStream_t st) {
   hipLaunchKernelGGL(zero_if_flag_kernel, dim3(blocks), dim3(256), 0, st, x, n, flag);
 }
 
+// fp32 W (R x C) -> bf16 W^T (C x R) in one pass: the transposed operand copy of the input-gradient GEMMs
+// (hip_ops.bf16_weight_t). 32 x 32 tiles through LDS (row stride 33: conflict-free column reads); reads
+// and writes are both row-contiguous across the 32 lanes of a tile row. Replaces a cast kernel plus
+// a strided elementwise copy (~25 us per 8 MB weight, measured) with one ~2 us pass.
+__global__ __launch_bounds__(256) void transpose_cast_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ wt,
+                                                                  int R, int C) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    tile[ty + k][tx] = (r < R && c < C) ? w[(size_t)r * C + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (c < C && r < R) wt[(size_t)c * R + r] = (__bf16)tile[tx][ty + k];
+  }
+}
+
+void transpose_cast_bf16(const float* w, void* wt, int R, int C, hipStream_t st) {
+  hipLaunchKernelGGL(transpose_cast_bf16_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, st, w, (__bf16*)wt, R, C);
+}
+
 }  // namespace dalle

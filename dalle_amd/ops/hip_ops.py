@@ -92,7 +92,10 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
     hit = _wcache.get(key)
     if hit is not None and hit[0] == stamp:
         return hit[1]
-    wt = bf16_weight(w).t().contiguous()
+    if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous():
+        wt = C().transpose_bf16(w)  # one tiled pass instead of a cast + a strided copy
+    else:
+        wt = bf16_weight(w).t().contiguous()
     _wcache[key] = (stamp, wt)
     return wt
 

@@ -358,3 +358,13 @@ def test_embedding_kernel(cuda, B, T, I, d):
     assert torch.equal(grads[0], grads[1])
     ref = torch.zeros(table.shape, dtype=torch.float64, device=cuda).index_add_(0, ids.reshape(-1), g.reshape(-1, d).double())
     assert torch.allclose(table.grad.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(3072, 1024), (1024, 4096), (8192, 1024), (37, 70), (1, 33)])
+def test_transpose_cast_bf16_bitwise(cuda, shape):
+    """fp32 W -> bf16 W^T in one tiled pass (the input-gradient operand copy) == cast then transpose."""
+    from dalle_amd.ops.hip_ops import C
+
+    w = torch.randn(*shape, device=cuda) * 3.0
+    got = C().transpose_bf16(w)
+    assert torch.equal(got, w.bfloat16().t().contiguous())
