@@ -1052,8 +1052,12 @@ class _SplitXent(torch.autograd.Function):
                 r1 = min(N, r0 + HEAD_CHUNK_ROWS)
                 hc = hs2[r0:r1]
                 logit = torch.addmm(bb[v0:v1], hc, wb[v0:v1].t())
-                if eager:  # logit -> dL/dlogits in place, their column sums -> db (the bias gradient)
+                if eager and v1 - v0 <= XENT_COLSUM_MAXV:
+                    # logit -> dL/dlogits in place, their column sums -> db (the bias gradient)
                     lc = C().xent_colsum_(logit, ls2[r0:r1], gscale, db[v0:v1])
+                elif eager:  # vocabulary split wider than the kernel's LDS accumulator
+                    lc = C().xent_fwd_bwd_(logit, ls2[r0:r1], gscale)
+                    db[v0:v1] += logit.float().sum(0)
                 else:
                     lc = C().xent_fwd_bwd_(logit, ls2[r0:r1], gscale)
                 loss = loss + lc.sum() * gscale
@@ -1088,6 +1092,8 @@ class _SplitXent(torch.autograd.Function):
 
 # rows of one head chunk (logits of 4096 text rows: 265 MB bf16, image rows: 67 MB)
 HEAD_CHUNK_ROWS = int(os.environ.get("DALLE_AMD_HEAD_CHUNK_ROWS", "4096"))
+# widest vocabulary split xent_colsum_ holds in LDS (csrc/kernels/xent.hip XENT_MAXV); wider splits sum in PyTorch
+XENT_COLSUM_MAXV = 35000
 
 
 def logits_loss(out, norm_w, norm_b, weight, bias, labels, text_seq_len: int, num_text_tokens: int, loss_img_weight: float):

@@ -336,3 +336,25 @@ def test_grad_ready_handoff_reports_final_grads(cuda, reversible):
         assert torch.equal(g_at, p.grad), "grad changed after it was handed over"
     # the tied embedding / head and the final norm are not stack parameters: never handed over early
     assert id(m.to_logits[1].weight) not in seen
+
+
+def test_head_fallback_for_wide_vocabulary_splits(cuda, monkeypatch):
+    """Vocabulary splits wider than the CE kernel's LDS accumulator take the xent_fwd_bwd_ + PyTorch column
+    sum path: same loss and gradients as the fused CE + bias-grad kernel."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    cfg = _cfg(False)
+    m = DALLE(cfg).to(cuda)
+    arena = FlatArena(m.parameters(), device=cuda)
+    text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
+    img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
+    out = []
+    for maxv in (hip_ops.XENT_COLSUM_MAXV, 0):
+        monkeypatch.setattr(hip_ops, "XENT_COLSUM_MAXV", maxv)
+        arena.zero_grad()
+        loss = m(text, img, return_loss=True)
+        loss.backward()
+        out.append((loss.item(), arena.grad.clone()))
+    assert abs(out[0][0] - out[1][0]) <= 1e-6 * abs(out[0][0])
+    assert torch.allclose(out[0][1], out[1][1], rtol=1e-4, atol=1e-7)
