@@ -1,12 +1,16 @@
 """Dataclass -> CLI parser compatible with ``transformers.HfArgumentParser`` as the reference uses it
 (``run_trainer.py:27``, ``run_aux_peer.py:86``): every field becomes ``--field value``; ``bool``
 fields take ``--flag True/False`` (or bare ``--flag``); ``List[str]`` fields take space-separated
-values; ``Optional[T]`` accepts the string ``None``.
+values; ``Optional[T]`` accepts the string ``None``. As with the HF parser, a run can also be configured
+from a dict or a JSON / YAML file (``parse_dict`` / ``parse_json_file`` / ``parse_yaml_file``; the
+entrypoints accept a single ``*.json`` / ``*.yaml`` argument), with the same type conversions and
+defaults as the command line.
 """
 from __future__ import annotations
 
 import argparse
 import dataclasses
+import json
 import sys
 import typing
 from typing import Any, List, Sequence, Tuple
@@ -87,6 +91,46 @@ class DataclassArgumentParser(argparse.ArgumentParser):
         if return_remaining_strings:
             outputs.append(remaining)
         return tuple(outputs)
+
+
+    def parse_dict(self, args: dict, allow_extra_keys: bool = False) -> Tuple:
+        """Dataclasses from a ``{field: value}`` mapping; values may be native (JSON / YAML) or strings,
+        and go through the same conversions as their command-line form."""
+        known = {a.dest: a for a in self._actions}
+        unknown = [k for k in args if k not in known]
+        if unknown and not allow_extra_keys:
+            raise ValueError(f"unknown keys: {sorted(unknown)}")
+        argv: List[str] = []
+        for k, v in args.items():
+            if k not in known:
+                continue
+            flag = "--" + k
+            if isinstance(v, (list, tuple)):
+                argv += [flag, *[str(x) for x in v]]
+            elif v is None:
+                argv += [flag, "None"]
+            else:
+                argv += [flag, str(v)]
+        return self.parse_args_into_dataclasses(argv)
+
+    def parse_json_file(self, path: str, allow_extra_keys: bool = False) -> Tuple:
+        with open(path, encoding="utf-8") as fh:
+            return self.parse_dict(json.load(fh), allow_extra_keys=allow_extra_keys)
+
+    def parse_yaml_file(self, path: str, allow_extra_keys: bool = False) -> Tuple:
+        import yaml
+
+        with open(path, encoding="utf-8") as fh:
+            return self.parse_dict(yaml.safe_load(fh) or {}, allow_extra_keys=allow_extra_keys)
+
+    def parse_cli_or_file(self, argv: Sequence[str] = None) -> Tuple:
+        """``script.py config.json`` / ``config.yaml`` (one argument) or the usual ``--flag value`` list."""
+        argv = list(argv if argv is not None else sys.argv[1:])
+        if len(argv) == 1 and argv[0].endswith(".json"):
+            return self.parse_json_file(argv[0])
+        if len(argv) == 1 and argv[0].endswith((".yaml", ".yml")):
+            return self.parse_yaml_file(argv[0])
+        return self.parse_args_into_dataclasses(argv)
 
 
 HfArgumentParser = DataclassArgumentParser

@@ -44,7 +44,7 @@ def _sinks(peer_args):
 
 def main(argv=None):
     parser = HfArgumentParser((AuxiliaryPeerArguments, HFTrainerArguments, CollaborativeArguments))
-    peer_args, trainer_args, collab_args = parser.parse_args_into_dataclasses(argv)
+    peer_args, trainer_args, collab_args = parser.parse_cli_or_file(argv)
     if peer_args.assist_in_averaging:
         raise NotImplementedError("aux peers are not members of the RCCL averaging group (as in the reference)")
 

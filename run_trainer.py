@@ -33,7 +33,7 @@ def _newest_checkpoint(output_dir: str):
 
 def main(argv=None):
     peer_args, trainer_args, collab_args = HfArgumentParser(
-        (TrainingPeerArguments, HFTrainerArguments, CollaborativeArguments)).parse_args_into_dataclasses(argv)
+        (TrainingPeerArguments, HFTrainerArguments, CollaborativeArguments)).parse_cli_or_file(argv)
     if trainer_args.local_rank < 0 and "LOCAL_RANK" in os.environ:  # torchrun
         trainer_args.local_rank = int(os.environ["LOCAL_RANK"])
     if not trainer_args.do_train or trainer_args.do_eval:
