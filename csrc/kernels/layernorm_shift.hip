@@ -227,7 +227,12 @@ __global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restri
 // multiplied per column by mul1), written or ACCUMULATED into the destination -- the destinations
 // are the parameters' fp32 .grad views in the flat arena, so no autograd add kernel follows.
 constexpr int CS_COLS = 16, CS_RG = 16;
-__global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part, int nrows, int width, GradSink sink) {
+// blockIdx.y selects one of up to two independent (part, sink) tasks of the same shape: the LN+shift
+// backward's two reductions (this sublayer's [dw | db], the previous one's [dscale | dbias]) in one launch
+__global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ part0, const float* __restrict__ part1,
+                                                         int nrows, int width, GradSink sink0, GradSink sink1) {
+  const float* __restrict__ part = blockIdx.y ? part1 : part0;
+  const GradSink& sink = blockIdx.y ? sink1 : sink0;
   __shared__ float red[CS_RG][CS_COLS];
   const int cl = threadIdx.x % CS_COLS, rg = threadIdx.x / CS_COLS;
   const int c = blockIdx.x * CS_COLS + cl;
@@ -262,7 +267,13 @@ __global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict
 }
 
 void column_sum(const float* part, int nrows, int width, const GradSink& sink, hipStream_t st) {
-  hipLaunchKernelGGL(column_sum_kernel, dim3((width + CS_COLS - 1) / CS_COLS), dim3(256), 0, st, part, nrows, width, sink);
+  hipLaunchKernelGGL(column_sum_kernel, dim3((width + CS_COLS - 1) / CS_COLS, 1), dim3(256), 0, st, part, part, nrows, width, sink,
+                     sink);
+}
+static void column_sum2(const float* part0, const GradSink& sink0, const float* part1, const GradSink& sink1, int nrows, int width,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(column_sum_kernel, dim3((width + CS_COLS - 1) / CS_COLS, 2), dim3(256), 0, st, part0, part1, nrows, width,
+                     sink0, sink1);
 }
 void column_sum(const float* part, int nrows, int width, float* out, hipStream_t st) {
   column_sum(part, nrows, width, GradSink{out, nullptr, nullptr, width, 0}, st);
@@ -291,7 +302,8 @@ static void launch_bwd(const float* x, const float* w, const void* dy, const flo
   if (yprev) {
     hipLaunchKernelGGL((ln_shift_bwd_kernel<D, true>), dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid,
                        dx, part, g, rows, (const __bf16*)yprev, sprev, (__bf16*)dyprev, part2);
-    column_sum(part2, blocks, 2 * D, *sink2, st);
+    column_sum2(part, sink, part2, *sink2, blocks, 2 * D, st);  // both reductions, one launch
+    return;
   } else {
     hipLaunchKernelGGL((ln_shift_bwd_kernel<D, false>), dim3(blocks), dim3(256), 0, st, x, w, (const __bf16*)dy, mean, rstd, resid,
                        dx, part, g, rows, (const __bf16*)nullptr, (const float*)nullptr, (__bf16*)nullptr, (float*)nullptr);
