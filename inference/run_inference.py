@@ -12,6 +12,7 @@ Checkpoints in the training layout are accepted (the reference's CachedAs rename
 ``net.fn.fn -> net.fn.fn.fn`` / ``to_qkv -> fn.to_qkv`` / ``to_out -> fn.to_out`` is undone when present).
 """
 import argparse
+import copy
 import os
 import pickle
 import sys
@@ -77,6 +78,50 @@ def generate(query, *, tokenizer, model, batch_size, n_iters, temperature, top_k
     return result
 
 
+def parse_devices(spec):
+    """``all`` -> every visible GPU, ``0,2`` -> those GPUs, ``cpu`` (tests); default: one device."""
+    if spec in (None, "", "auto"):
+        return ["cuda" if torch.cuda.is_available() else "cpu"]
+    if spec == "all":
+        n = torch.cuda.device_count()
+        return [f"cuda:{i}" for i in range(n)] if n else ["cpu"]
+    return [d if (d.startswith("cuda") or d == "cpu") else f"cuda:{int(d)}" for d in spec.split(",")]
+
+
+def run_queries(queries, per_device, work):
+    """Spread ``queries`` over the devices: one worker thread per entry of ``per_device`` (its device's
+    model copy and state), each taking the next unclaimed query -- GPUs finish at their own pace."""
+    import queue
+    import threading
+
+    q = queue.Queue()
+    for item in queries:
+        q.put(item)
+    errors = []
+
+    def worker(ctx):
+        while not errors:
+            try:
+                item = q.get_nowait()
+            except queue.Empty:
+                return
+            try:
+                work(item, ctx)
+            except BaseException as e:  # noqa: BLE001 - surfaced after the join
+                errors.append(e)
+
+    if len(per_device) == 1:
+        worker(per_device[0])
+    else:
+        threads = [threading.Thread(target=worker, args=(ctx,), daemon=True) for ctx in per_device]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    if errors:
+        raise errors[0]
+
+
 def load_queries(path: str):
     """One caption per line; trailing whitespace dropped, empty lines skipped (the reference's format)."""
     with open(path, encoding="utf-8") as fh:
@@ -98,13 +143,15 @@ def main(argv=None):
     parser.add_argument('--n-iters', type=int, default=8, help='[new] generate calls per query (reference: 8)')
     parser.add_argument('--clip', type=str, default=None, help='[new] CLIP ViT-B/32 weights (safetensors/state dict) or "random"')
     parser.add_argument('--clip-tokenizer', type=str, default=None, help='[new] CLIP BPE tokenizer.json (tokenizers format)')
+    parser.add_argument('--devices', type=str, default='auto',
+                        help='[new] "all" GPUs of the node or a list like "0,1": queries are spread over per-GPU workers')
     args = parser.parse_args(argv)
     torch.set_grad_enabled(False)  # inference only (the reference disabled grads at import time)
 
     queries = load_queries(args.queries)
     print(f'[*] Loaded {len(queries)} queries')
 
-    device = "cuda" if torch.cuda.is_available() else "cpu"
+    devices = parse_devices(args.devices)
     tokenizer, model = make_model(args.model_preset)
     if args.model is not None:
         print(f'[*] Model modification time: {datetime.fromtimestamp(os.stat(args.model).st_mtime)}')
@@ -116,13 +163,14 @@ def main(argv=None):
 
     gan = VQGanVAE(args.vqgan, args.vqgan_config)
     model.model.vae = gan.eval()
-    model = model.to(device).eval()
+    # one model copy per device (the last device takes the original)
+    models = [(model if i == len(devices) - 1 else copy.deepcopy(model)).to(d).eval() for i, d in enumerate(devices)]
 
-    clip_model = clip_tok = None
+    clip_models, clip_tok = [None] * len(devices), None
     if args.clip:
         from dalle_amd.models.clip import ClipTokenizer, load_clip
 
-        clip_model = load_clip(None if args.clip == "random" else args.clip, device=device)
+        clip_models = [load_clip(None if args.clip == "random" else args.clip, device=d) for d in devices]
         clip_tok = ClipTokenizer(args.clip_tokenizer)
         print(f"[*] CLIP ViT-B/32 {'random-init (scores are not meaningful)' if args.clip == 'random' else 'from ' + args.clip}")
     else:
@@ -130,7 +178,11 @@ def main(argv=None):
 
     os.makedirs(args.output_dir, exist_ok=True)
     print(f'[*] Saving results to `{args.output_dir}`')
-    for query in queries:
+    if len(devices) > 1:
+        print(f'[*] {len(devices)} devices: {", ".join(devices)}')
+
+    def work(query, ctx):
+        model, clip_model, device = ctx
         images = generate(query, tokenizer=tokenizer, model=model, batch_size=args.batch_size, n_iters=args.n_iters,
                           temperature=args.temperature, top_k=args.top_k, top_p=args.top_p,
                           text_seq_len=model.model.text_seq_len, device=device)
@@ -143,6 +195,8 @@ def main(argv=None):
         with open(os.path.join(args.output_dir, f'{query}.pickle'), 'wb') as f:
             outputs = {'query': query, 'temperature': args.temperature, 'images': images, 'clip_scores': clip_scores}
             pickle.dump(outputs, f)
+
+    run_queries(queries, list(zip(models, clip_models, devices)), work)
 
 
 if __name__ == '__main__':

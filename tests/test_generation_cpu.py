@@ -1,4 +1,6 @@
 """KV-cache decoding == full forward (static masks, cached token shift, rotary at position)."""
+import os
+
 import pytest
 import torch
 
@@ -134,3 +136,24 @@ def test_parallel_prefill_matches_sequential_steps(reversible):
                 assert torch.allclose(seq.hist[li][j][:, :P], par.hist[li][j][:, :P], atol=1e-4, rtol=1e-4)
         l_seq, l_par = seq._forward_position(), par._forward_position()
     assert torch.allclose(l_seq, l_par, atol=2e-4, rtol=1e-4), (l_seq - l_par).abs().max()
+
+
+def test_run_inference_spreads_queries_over_devices(tmp_path):
+    """inference/run_inference.py --devices: one model copy per device, queries taken by per-device workers;
+    every query gets its pickle (reference output format: query, temperature, images, clip_scores)."""
+    import pickle
+    import subprocess
+    import sys as _sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    (tmp_path / "q.txt").write_text("a red apple\nthe northern lights\n\na cat\n")
+    r = subprocess.run([_sys.executable, os.path.join(root, "inference", "run_inference.py"), "--queries", str(tmp_path / "q.txt"),
+                        "--model-preset", "tiny", "--output-dir", str(tmp_path / "out"), "--batch-size", "1", "--n-iters", "2",
+                        "--devices", "cpu,cpu", "--top-k", "16"], capture_output=True, text=True, timeout=600,
+                       env={k: v for k, v in os.environ.items() if k != "HIP_VISIBLE_DEVICES"} | {"HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "2 devices" in r.stdout
+    for q in ("a red apple", "the northern lights", "a cat"):
+        with open(tmp_path / "out" / f"{q}.pickle", "rb") as f:  # written by this test's own subprocess
+            out = pickle.load(f)
+        assert out["query"] == q and len(out["images"]) == 2 and out["clip_scores"].shape == (2,)
