@@ -38,6 +38,11 @@ def main(argv=None):
         trainer_args.local_rank = int(os.environ["LOCAL_RANK"])
     if not trainer_args.do_train or trainer_args.do_eval:
         raise ValueError("a training peer runs with --do_train True --do_eval False")
+    if torch.cuda.is_available() and trainer_args.per_device_train_batch_size < 16:
+        # the reference's default (2) is sized for 16 GB T4s: on MI355X it gives GEMMs of M = 2,560 tokens,
+        # launch-bound; 48 was the measured optimum of the bench sweep (README "Running")
+        logger.warning(f"per_device_train_batch_size={trainer_args.per_device_train_batch_size} leaves an MI355X mostly "
+                       f"idle; --per_device_train_batch_size 48 is the measured optimum (72 GB of HBM)")
     logger.info(f"initial peers ({len(peer_args.initial_peers)}): {peer_args.initial_peers}")
     utils.log_process_rank(trainer_args)
 
