@@ -74,23 +74,30 @@ __global__ __launch_bounds__(D / 4) void decode_ln_shift_kernel(float* __restric
     for (int i = 0; i < 4; ++i) v[i] += sc[i] * (acc[i] + pb[i]);
     *reinterpret_cast<f32x4*>(xr + c) = v;
   }
-  float s = wave_sum(v[0] + v[1] + v[2] + v[3]);
-  if (lane == 0) red[0][wave] = s;
-  __syncthreads();
-  s = 0.f;
+  // one reduction round for both moments (a decode step is latency-bound: one barrier fewer per row);
+  // the shifted second moment about this thread's first element keeps E[x^2] - mean^2 cancellation-free
+  const float piv = __shfl(v[0], 0, 64);
+  float s = 0.f, q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) s += red[0][i];
-  const float mean = s * (1.0f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { const float d = v[i] - mean; q += d * d; }
+  for (int i = 0; i < 4; ++i) { const float d = v[i] - piv; s += d; q += d * d; }
+  s = wave_sum(s);
   q = wave_sum(q);
-  if (lane == 0) red[1][wave] = q;
+  __shared__ float pivs[NW];
+  if (lane == 0) { red[0][wave] = s; red[1][wave] = q; pivs[wave] = piv; }
   __syncthreads();
-  q = 0.f;
+  // combine the waves' (pivot, shifted sum, shifted sum of squares) about wave 0's pivot
+  const float p0 = pivs[0];
+  float S = 0.f, Q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) q += red[1][i];
-  const float rstd = rsqrtf(q * (1.0f / D) + 1e-5f);
+  for (int i = 0; i < NW; ++i) {
+    const float dp = pivs[i] - p0, si = red[0][i], n = (float)(D / NW);
+    S += si + n * dp;
+    Q += red[1][i] + 2.f * dp * si + n * dp * dp;
+  }
+  const float dm = S * (1.0f / D);           // mean - p0
+  const float mean = p0 + dm;
+  const float var = fmaxf(Q * (1.0f / D) - dm * dm, 0.f);
+  const float rstd = rsqrtf(var + 1e-5f);
   float o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
