@@ -8,6 +8,7 @@ blocks (summed over every layer that reuses them) never round through bf16.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Dict, Tuple
 
 import torch
@@ -58,7 +59,7 @@ def C():
 # ---------------------------------------------------------------------------------------------
 # bf16 weight cast cache (one cast per unique weight per forward; invalidated by begin_forward)
 # ---------------------------------------------------------------------------------------------
-_wcache: Dict[int, Tuple[int, torch.Tensor]] = {}
+_wcache: Dict[object, Tuple[object, tuple, torch.Tensor]] = {}
 _epoch = 0
 
 
@@ -68,36 +69,35 @@ def begin_forward():
     _wcache.clear()
 
 
+def _cached(key, w: torch.Tensor, make):
+    """Per-weight cache entry. A hit needs the SAME live tensor (weak reference: a recycled id() and a
+    recycled storage address of a new tensor never match a dead one's entry) at the same address, shape
+    and version counter; begin_forward() clears everything per forward, which covers the optimizer's
+    raw-pointer updates."""
+    stamp = (w.data_ptr(), tuple(w.shape), w._version)
+    hit = _wcache.get(key)
+    if hit is not None and hit[0]() is w and hit[1] == stamp:
+        return hit[2]
+    val = make()
+    _wcache[key] = (weakref.ref(w), stamp, val)
+    return val
+
+
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     if w.dtype == torch.bfloat16:
         return w
-    key = id(w)
-    # id() and the storage address can both be recycled by a new tensor between forwards: the entry
-    # must also match shape and version counter (begin_forward() clears everything per forward, which
-    # covers the optimizer's raw-pointer updates)
-    stamp = (w.data_ptr(), tuple(w.shape), w._version)
-    hit = _wcache.get(key)
-    if hit is not None and hit[0] == stamp:
-        return hit[1]
-    wb = w.detach().to(torch.bfloat16)
-    _wcache[key] = (stamp, wb)
-    return wb
+    return _cached(id(w), w, lambda: w.detach().to(torch.bfloat16))
 
 
 def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
     """Transposed (in, out) bf16 copy of a Linear weight, cached per forward like ``bf16_weight``: the
     B operand of an NT GEMM that multiplies by W instead of W^T (the fused FF dgrad)."""
-    key = ("t", id(w))
-    stamp = (w.data_ptr(), tuple(w.shape), w._version)
-    hit = _wcache.get(key)
-    if hit is not None and hit[0] == stamp:
-        return hit[1]
-    if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous():
-        wt = C().transpose_bf16(w)  # one tiled pass instead of a cast + a strided copy
-    else:
-        wt = bf16_weight(w).t().contiguous()
-    _wcache[key] = (stamp, wt)
-    return wt
+    def make():
+        if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous():
+            return C().transpose_bf16(w)  # one tiled pass instead of a cast + a strided copy
+        return bf16_weight(w).t().contiguous()
+
+    return _cached(("t", id(w)), w, make)
 
 
 NT_INPUT_GRAD = os.environ.get("DALLE_AMD_NT_DGRAD", "1") != "0"
@@ -1091,7 +1091,10 @@ class _SplitXent(torch.autograd.Function):
 
 
 # rows of one head chunk (logits of 4096 text rows: 265 MB bf16, image rows: 67 MB)
-HEAD_CHUNK_ROWS = int(os.environ.get("DALLE_AMD_HEAD_CHUNK_ROWS", "4096"))
+# rows per head chunk: 16384 measured 0.9 % faster per bench24 step than 4096 (6 of 6 same-box pairs,
+# profiles/r2_s4_head_chunk_ab.txt) for ~0.55 GB more peak memory (B48: the 12288 text rows form one 0.8 GB
+# logits chunk, the image rows three of 0.27 GB; the full 1.6 GB never exists)
+HEAD_CHUNK_ROWS = int(os.environ.get("DALLE_AMD_HEAD_CHUNK_ROWS", "16384"))
 # widest vocabulary split xent_colsum_ holds in LDS (csrc/kernels/xent.hip XENT_MAXV); wider splits sum in PyTorch
 XENT_COLSUM_MAXV = 35000
 
