@@ -177,7 +177,7 @@ class CollaborativeCallback(TrainerCallback):
             logger.info(f"Backup (epoch {snapshot['local_epoch']}) is older than the current state "
                         f"(epoch {opt.local_epoch}); keeping the current state")
             return
-        self.task.model.load_state_dict(snapshot["model"], strict=False)
+        self.task.model.load_state_dict(snapshot["model"], strict=True)  # our own backup: every key must match
         opt.load_state_dict(snapshot["training"])
         opt.state_averager.scheduler.load_state_dict(snapshot["scheduler"])
         opt.state_averager.local_epoch = snapshot["local_epoch"]

@@ -3,6 +3,7 @@
 // (a mis-sized launch of a hand-written kernel can fault the GPU).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 #include "kernels/geom.h"
@@ -73,6 +74,13 @@ void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 bool sample_step(const SampleArgs&, hipStream_t);
 bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
+bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
+bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
+                      hipStream_t);
+bool gemm_pt_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
+bool gemm_pt_geglu_fwd(const void*, const void*, const void*, void*, void*, int, int, int, hipStream_t);
+void permlane16_probe(unsigned*, hipStream_t);
+void rope_pad_zero(void*, void*, void*, int, int, int, int, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
 void lamb_step(float*, const float*, uint8_t*, uint8_t*, float*, float*, float*, float*, const float*, const float*,
                const int*, const int*, const long*, const long*, const int*, const float*, const float*, const float*, float*,
@@ -83,7 +91,14 @@ using torch::Tensor;
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
-#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define DALLE_CAT2(a, b) a##b
+#define DALLE_CAT(a, b) DALLE_CAT2(a, b)
+// every op's first device check also makes that tensor's GPU the current device for the rest of the op,
+// so cur_stream() and the kernel launches bind to the operand's device (a serving thread whose current
+// device is still GPU 0 must not launch on GPU 0's stream against GPU N's memory)
+#define CHECK_CUDA(x)                                                  \
+  TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor");              \
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA DALLE_CAT(_dev_guard_, __COUNTER__)((x).device())
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " has wrong dtype")
 #define CHECK_IN(x, dt) CHECK_CUDA(x); CHECK_CONTIG(x); CHECK_DT(x, dt)
@@ -472,6 +487,94 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
   auto C = torch::empty({M, N}, A.options());
   TORCH_CHECK(dalle::gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, (int)variant, cur_stream()));
   return C;
+}
+
+// ---- persistent GEMM family (csrc/kernels/gemm_pt.hip): transposed accumulators, register-direct epilogues ----
+// C (M, N) = A (M, K) . B (N, K)^T (+ bias); variant 5 = main loop only (measurement)
+Tensor gemm_pt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant, int64_t group) {
+  CHECK_IN(A, torch::kBFloat16); CHECK_IN(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_pt: A (M, K) and B (N, K)");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 128, "gemm_pt: M, N multiples of 256, K of 64 (>= 128)");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN((*bias), torch::kBFloat16);
+    TORCH_CHECK(bias->numel() == N, "gemm_pt: bias (N,)");
+    bp = bias->data_ptr();
+  }
+  auto C = torch::empty({M, N}, A.options());
+  TORCH_CHECK(dalle::gemm_pt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, N, (int)variant, (int)group, cur_stream()),
+              "gemm_pt: unsupported shape");
+  return C;
+}
+
+// QKV projection + rotary (persistent kernel): cs = (n + 1, 32, 2) fp32 (cos, sin) per rotary pair
+std::vector<Tensor> qkv_rope_pt(Tensor h, Tensor w, Tensor cs, int64_t T, int64_t S, int64_t H, int64_t n, bool col_major,
+                                double qscale) {
+  CHECK_IN(h, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16); CHECK_IN(cs, torch::kFloat32);
+  TORCH_CHECK(h.dim() == 2 && w.dim() == 2 && w.size(0) == 3 * H * 64 && w.size(1) == h.size(1), "qkv_rope_pt: shapes");
+  const int M = h.size(0), K = h.size(1);
+  TORCH_CHECK(M % n == 0 && M % 256 == 0 && (3 * H * 64) % 256 == 0 && K % 64 == 0 && K >= 128, "qkv_rope_pt: tile multiples");
+  TORCH_CHECK(cs.dim() == 3 && cs.size(0) >= n && cs.size(1) == 32 && cs.size(2) == 2, "qkv_rope_pt: cs (n + 1, 32, 2)");
+  auto g = make_attn_geom(T, S, n, 1, H, 0);
+  const int B = M / n;
+  auto opts = h.options();
+  auto q = torch::empty({B * H, g.Np, 64}, opts);
+  auto k = torch::empty({B * H, g.Np, 64}, opts);
+  auto v = torch::empty({B * H, g.Np, 64}, opts);
+  TORCH_CHECK(dalle::gemm_pt_qkv_rope(h.data_ptr(), w.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cs.data_ptr<float>(), M,
+                                      K, H, T, S, n, col_major ? 1 : 0, (float)qscale, cur_stream()),
+              "qkv_rope_pt: unsupported shape");
+  dalle::rope_pad_zero(q.data_ptr(), k.data_ptr(), v.data_ptr(), g.Tp, T, g.Np, B * H, cur_stream());
+  return {q, k, v};
+}
+
+// FF-out dgrad + GEGLU backward (persistent kernel): dy (M, K), w2t = W2^T (F, K), h (M, 2F) -> (dh, dbias)
+std::vector<Tensor> ff_dgrad_geglu_pt(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
+  CHECK_IN(dy, torch::kBFloat16); CHECK_IN(w2t, torch::kBFloat16); CHECK_IN(h, torch::kBFloat16);
+  TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2, "ff_dgrad_geglu_pt: 2-D operands");
+  const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
+  TORCH_CHECK(w2t.size(1) == K && h.size(0) == M && h.size(1) == 2 * F, "ff_dgrad_geglu_pt: shape mismatch");
+  TORCH_CHECK(M % 256 == 0 && F % 256 == 0 && K % 64 == 0 && K >= 128, "ff_dgrad_geglu_pt: M, F multiples of 256, K of 64");
+  auto dh = torch::empty_like(h);
+  auto part = torch::empty({M / 64, 2 * F}, h.options().dtype(torch::kFloat32));
+  float* pb = sink_ptr(gb, 2 * F, "ff_dgrad_geglu_pt dbias");
+  Tensor db;
+  if (!pb) {
+    db = torch::empty({2 * F}, h.options().dtype(torch::kFloat32));
+    pb = db.data_ptr<float>();
+  }
+  TORCH_CHECK(dalle::gemm_pt_geglu_bwd(dy.data_ptr(), w2t.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), M, F, K,
+                                       cur_stream()), "ff_dgrad_geglu_pt: unsupported shape");
+  dalle::column_sum(part.data_ptr<float>(), M / 64, 2 * F, dalle::GradSink{pb, nullptr, nullptr, (int)(2 * F), db.defined() ? 0 : 1},
+                    cur_stream());
+  return {dh, db};
+}
+
+// FF-in GEMM + GEGLU forward (persistent kernel): x (M, K), w1i / b1i = W1 / b1 rows interleaved per 64-row
+// group ([32 value | 32 gate]) -> a (M, 2F) pre-activation in the original [value | gate] order, u (M, F)
+std::vector<Tensor> ff_in_geglu_pt(Tensor x, Tensor w1i, c10::optional<Tensor> b1i) {
+  CHECK_IN(x, torch::kBFloat16); CHECK_IN(w1i, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && w1i.dim() == 2 && x.size(1) == w1i.size(1), "ff_in_geglu_pt: x (M, K), w1i (2F, K)");
+  const int M = x.size(0), K = x.size(1), F2 = w1i.size(0);
+  TORCH_CHECK(M % 256 == 0 && F2 % 256 == 0 && K % 64 == 0 && K >= 128, "ff_in_geglu_pt: M, 2F multiples of 256, K of 64");
+  const void* bp = nullptr;
+  if (b1i.has_value() && b1i->defined()) {
+    CHECK_IN((*b1i), torch::kBFloat16);
+    TORCH_CHECK(b1i->numel() == F2, "ff_in_geglu_pt: bias (2F,)");
+    bp = b1i->data_ptr();
+  }
+  auto a = torch::empty({M, F2}, x.options());
+  auto u = torch::empty({M, F2 / 2}, x.options());
+  TORCH_CHECK(dalle::gemm_pt_geglu_fwd(x.data_ptr(), w1i.data_ptr(), bp, a.data_ptr(), u.data_ptr(), M, F2 / 2, K, cur_stream()),
+              "ff_in_geglu_pt: unsupported shape");
+  return {a, u};
+}
+
+Tensor permlane16_probe() {
+  auto out = torch::empty({128}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA));
+  dalle::permlane16_probe((unsigned*)out.data_ptr<int>(), cur_stream());
+  return out;
 }
 
 // dW (N, K) fp32 (+)= G^T X: G (M, N), X (M, K) bf16 row-major (tokens on the rows of both), the
@@ -1064,6 +1167,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zero_if_nonfinite_", &zero_if_nonfinite_);
   m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
+  m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
+  m.def("qkv_rope_pt", &qkv_rope_pt);
+  m.def("ff_dgrad_geglu_pt", &ff_dgrad_geglu_pt, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
+  m.def("ff_in_geglu_pt", &ff_in_geglu_pt, py::arg("x"), py::arg("w1i"), py::arg("b1i") = py::none());
+  m.def("permlane16_probe", &permlane16_probe);
   m.def("gemm_wgrad_", &gemm_wgrad_, py::arg("G"), py::arg("X"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("embed_fwd", &embed_fwd);

@@ -750,6 +750,10 @@ __global__ void rope_pad_zero_kernel(__bf16* q, __bf16* k, __bf16* v, int Tp, in
   *reinterpret_cast<s16x8*>(v + off) = z;
 }
 
+void rope_pad_zero(void* q, void* k, void* v, int Tp, int T, int Np, int BH, hipStream_t st) {
+  hipLaunchKernelGGL(rope_pad_zero_kernel, dim3(BH), dim3(256), 0, st, (__bf16*)q, (__bf16*)k, (__bf16*)v, Tp, T, Np, BH);
+}
+
 bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int epi, hipStream_t st) {
   if (M % GBM || N % GBN || K % GBK) return false;
   const int nwg = (M / GBM) * (N / GBN);

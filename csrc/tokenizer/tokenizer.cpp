@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <exception>
 #include <thread>
 
 #include "unigram_core.h"
@@ -24,12 +25,22 @@ std::vector<std::vector<int>> encode_batch(const Pipeline& p, const std::vector<
     for (size_t i = 0; i < texts.size(); ++i) out[i] = p.encode(texts[i], add_special, max_length, truncation);
     return out;
   }
+  // an exception inside a worker (bad_alloc, a malformed model) must not std::terminate the data-loader:
+  // each worker parks it, the first one is rethrown on the calling thread after the join (pybind11 then
+  // raises it as a Python exception)
+  std::vector<std::exception_ptr> errs(nt);
   std::vector<std::thread> pool;
   for (int t = 0; t < nt; ++t)
     pool.emplace_back([&, t] {
-      for (size_t i = t; i < texts.size(); i += nt) out[i] = p.encode(texts[i], add_special, max_length, truncation);
+      try {
+        for (size_t i = t; i < texts.size(); i += nt) out[i] = p.encode(texts[i], add_special, max_length, truncation);
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
     });
   for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
   return out;
 }
 

@@ -257,6 +257,7 @@ class Unigram {
   void encode(const std::string& s, std::vector<int>* out) const {
     const size_t n = s.size();
     if (!n) return;
+    if (nodes_.empty()) throw std::runtime_error("unigram: no model loaded (call set_model first)");
     struct Best { double score = 0.0; long start = -1; int id = -1; };
     std::vector<Best> best(n + 1);
     best[0].start = 0;

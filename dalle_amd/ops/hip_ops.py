@@ -125,6 +125,38 @@ def _rope_tables(geom: AttnGeometry, dim_head: int, device):
     return t
 
 
+_cs_tables: Dict[tuple, torch.Tensor] = {}
+
+
+def rope_cs_table(geom: AttnGeometry, dim_head: int, device) -> torch.Tensor:
+    """(n + 1, dim_head / 2, 2) fp32 (cos, sin) per rotary pair -- the packed form of the rotary tables
+    read by the persistent QKV GEMM's epilogue (pairs share their cos; the rotate_half sign is applied
+    in the kernel)."""
+    key = (geom.text_len, geom.image_size, dim_head, str(device))
+    t = _cs_tables.get(key)
+    if t is None:
+        cos, sin = _rope_tables(geom, dim_head, device)
+        t = torch.stack([cos[:, 0::2], sin[:, 1::2]], dim=-1).contiguous()
+        _cs_tables[key] = t
+    return t
+
+
+_perm_cache: Dict[tuple, torch.Tensor] = {}
+
+
+def geglu_interleave_index(F: int, device) -> torch.Tensor:
+    """Row order of W1 / b1 for the fused FF-in GEGLU GEMM: per 64-row group g, the 32 value rows
+    32g .. 32g+31 followed by the matching gate rows F + 32g .. F + 32g + 31, so each wave's 64 output
+    columns hold a feature's value and gate side by side (csrc/kernels/gemm_pt.hip EPI 3)."""
+    key = (F, str(device))
+    idx = _perm_cache.get(key)
+    if idx is None:
+        g = torch.arange(F // 32).view(-1, 1) * 32 + torch.arange(32).view(1, -1)  # (F/32, 32) feature ids
+        idx = torch.cat([g, g + F], dim=1).reshape(-1).to(device)
+        _perm_cache[key] = idx
+    return idx
+
+
 # ---------------------------------------------------------------------------------------------
 # Linear: bf16 GEMM forward, fp32 weight grads accumulated straight into the fp32 grad buffer
 # ---------------------------------------------------------------------------------------------

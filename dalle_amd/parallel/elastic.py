@@ -22,6 +22,7 @@ any process that is not itself a trainer):
 from __future__ import annotations
 
 import datetime
+import os
 import threading
 import time
 from typing import List, Optional
@@ -39,6 +40,31 @@ def coordinator_store(host: str, port: int, is_master: bool, timeout: float = 30
     """The long-lived store the generations rendezvous on (``is_master`` on the coordinator process)."""
     return dist.TCPStore(host, port, world_size=None, is_master=is_master, timeout=datetime.timedelta(seconds=timeout),
                          wait_for_workers=False)
+
+
+def recovery_store(run_id: str, timeout: float = 300.0) -> Optional[dist.Store]:
+    """A key/value store that OUTLIVES every trainer process, for re-forming the group after a failure on
+    the default launch path, or None:
+
+    * ``DALLE_AMD_COORDINATOR=host:port`` -- an external coordinator (aux peer, launcher, test harness);
+    * a torchrun worker (``TORCHELASTIC_USE_AGENT_STORE=True``): the elastic AGENT hosts the job's
+      TCPStore at ``MASTER_ADDR:MASTER_PORT`` -- not the rank-0 worker -- so it survives any worker.
+
+    Keys live under ``dalle_recovery/{run_id}``."""
+    spec = os.environ.get("DALLE_AMD_COORDINATOR")
+    try:
+        if spec:
+            host, port = spec.rsplit(":", 1)
+            base = coordinator_store(host, int(port), is_master=False, timeout=timeout)
+        elif os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true" and "MASTER_PORT" in os.environ:
+            base = coordinator_store(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), is_master=False,
+                                     timeout=timeout)
+        else:
+            return None
+    except Exception as e:  # noqa: BLE001 - no recovery store: the caller falls back to detaching
+        logger.warning(f"[elastic] recovery store unavailable ({e!r})")
+        return None
+    return dist.PrefixStore(f"dalle_recovery/{run_id}", base)
 
 
 class ElasticGroup:
@@ -77,6 +103,16 @@ class ElasticGroup:
         except Exception:  # noqa: BLE001
             return False
 
+    @classmethod
+    def adopt(cls, store: dist.Store, rank: int, world_size: int, backend: str, **kw) -> "ElasticGroup":
+        """Take over an EXISTING process group (the torchrun world) as generation -1: no rendezvous now,
+        but heartbeats start, so that after a failure the survivors re-form a group among themselves
+        (generation 0, 1, ...) instead of each training alone."""
+        eg = cls(store, peer_id=f"r{rank}", backend=backend, **kw)
+        eg.generation, eg.rank, eg.world_size = -1, int(rank), int(world_size)
+        eg.members = [f"r{i}" for i in range(int(world_size))]
+        return eg
+
     # -- membership -----------------------------------------------------------------------------------
     def _current_generation(self) -> int:
         return int(self.store.add("elastic/gen", 0))
@@ -109,7 +145,7 @@ class ElasticGroup:
         while True:
             n = int(self.store.add(f"elastic/g{g}/count", 0))
             if time.time() >= deadline:
-                if g == 0:
+                if not previous:  # the first formation: wait for min_peers
                     done = n >= self.min_peers
                 else:  # wait for every previous member that is still alive (fresh heartbeat), but not for a
                     # straggler past allreduce_timeout: it is dropped from this generation and rejoins later
@@ -143,7 +179,8 @@ class ElasticGroup:
             # then drop the registry entry so the next generation can initialise the default group again
             abort_group()
             try:
-                dist.destroy_process_group()
+                if dist.is_initialized():  # an abort may already have dropped the group from the registry
+                    dist.destroy_process_group()
             except Exception as e:  # noqa: BLE001 - a broken group may fail to tear down cleanly
                 logger.warning(f"[elastic] destroy_process_group: {e!r}")
         # first survivor to get here opens generation old+1 (compare-and-set: bumped exactly once)

@@ -145,11 +145,21 @@ class GradientAverager:
                             tt = torch.tensor([s], device=flat.device, dtype=torch.float32)
                             dist.all_reduce(tt, group=self.group)
                             total = float(tt.item())
+                        saved_grads = None
                         if views is not None:  # PowerSGD reads and writes the params' .grad
                             self._unflat(flat, views)
+                            # temporary .grad bindings: without reuse_grad_buffers `views` are the
+                            # accumulators, and leaving them bound as .grad would alias p.grad with its
+                            # own accumulator (the next accumulate_grads_ would add it into itself)
+                            saved_grads = [p.grad for p in self.params]
                             for p, g in zip(self.params, views):
                                 p.grad = g
-                        self.powersgd.allreduce_(scale=s * world / max(total, 1e-30))
+                        try:
+                            self.powersgd.allreduce_(scale=s * world / max(total, 1e-30))
+                        finally:
+                            if saved_grads is not None:
+                                for p, g0 in zip(self.params, saved_grads):
+                                    p.grad = g0
                         if views is not None:
                             flat, views = self._flat_nodiv(grads), grads
                     else:
@@ -244,7 +254,7 @@ class TrainingStateAverager:
     def __init__(self, optimizer: torch.optim.Optimizer, scheduler=None, params=None, arena: Optional[FlatArena] = None,
                  group=None, compression: Optional[CompressionBase] = None, average_state_every: int = 1,
                  master: Optional[MasterParams] = None, delay: bool = False, averaging_timeout: Optional[float] = None,
-                 skip_if_exact: bool = True):
+                 skip_if_exact: bool = True, check_every: int = 16):
         self.optimizer = optimizer
         self.scheduler = scheduler
         self.params = params
@@ -257,6 +267,8 @@ class TrainingStateAverager:
         self.runner = AsyncStep(master.masters[0].device) if (delay and master is not None and master.masters) else None
         self.averaging_timeout = averaging_timeout
         self.skip_if_exact = skip_if_exact
+        self.check_every = int(check_every)  # verify the "replicas are identical" assumption this often
+        self.drift_detected = 0
         self.detached = False
         self.comm_failed = False
         self.rounds_skipped = 0
@@ -320,13 +332,35 @@ class TrainingStateAverager:
         self._unapplied = False
 
     @torch.no_grad()
+    def _replicas_differ(self) -> bool:
+        if self.arena is not None:
+            data = self.arena.data
+        else:
+            data = torch.cat([p.detach().reshape(-1).float() for p in self.params])
+        h = data.view(torch.int32).sum(dtype=torch.int64)
+        v = torch.stack([h, -h])  # int64: exact
+        try:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)  # (max, -min) of the checksum
+        except Exception as e:  # noqa: BLE001
+            logger.warning(f"replica check failed ({e!r})")
+            self.comm_failed = True
+            return False
+        return bool(v[0].item() != -v[1].item())
+
+    @torch.no_grad()
     def average_parameters(self):
         world, _ = (1, 0) if self.detached else _group_world(self.group)
         if world == 1:
             return
         if self.skip_if_exact and self._exact:
-            self.rounds_skipped += 1
-            return
+            # the skip assumes every peer ran the same deterministic update on identical parameters; every
+            # `check_every` epochs that is VERIFIED with one 2-element all-reduce of an exact parameter
+            # checksum (integer sum of the fp32 bit patterns), and a real round runs if replicas drifted
+            if not (self.check_every > 0 and self.local_epoch % self.check_every == 0 and self._replicas_differ()):
+                self.rounds_skipped += 1
+                return
+            self.drift_detected += 1
+            logger.warning(f"replica parameters differ after an exact round (epoch {self.local_epoch}); averaging them")
         buf = self.arena.data if self.arena is not None else torch.cat([p.detach().reshape(-1).float() for p in self.params])
         segs = self.arena.segments() if self.arena is not None else _segments_of(self.params)
         backup = buf.clone()
@@ -358,7 +392,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                  state_averaging_compression: Optional[CompressionBase] = None, average_state_every: int = 1,
                  client_mode: bool = False, auxiliary: bool = False, verbose: bool = False, process_group=None,
                  arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "auto",
-                 device=None, elastic=None, skip_exact_state_averaging: bool = True, offload_device=None, **kwargs):
+                 device=None, elastic=None, skip_exact_state_averaging: bool = True, offload_device=None,
+                 recovery: str = "auto", state_check_every: int = 16, **kwargs):
         self.dht, self.run_id = dht, run_id
         self.target_batch_size = target_batch_size
         self.batch_size_per_step = batch_size_per_step
@@ -393,11 +428,30 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         device = device or (flat_params[0].device if flat_params else torch.device("cpu"))
         self.device = device
         peer_id = dht.peer_id if dht is not None else f"rank{_group_world(process_group)[1]}"
+        # failure recovery on the default (static torchrun) world: with a store that outlives the trainers
+        # (the torchrun agent's, or DALLE_AMD_COORDINATOR) the world is adopted as elastic generation -1,
+        # so after a dead / timed-out peer the survivors re-form a group and keep averaging; without one
+        # (or recovery="detach") a failed peer's survivors detach and train alone
+        self.adopted = False
+        tracker_store = None
+        world0, rank0 = _group_world(process_group)
+        if elastic is None and recovery == "auto" and world0 > 1 and (process_group is None or process_group == dist.group.WORLD):
+            from .elastic import ElasticGroup, recovery_store
+            rstore = recovery_store(run_id, timeout=max(30.0, float(averaging_timeout or 0)))
+            if rstore is not None:
+                elastic = ElasticGroup.adopt(rstore, rank0, world0, backend=dist.get_backend(),
+                                             matchmaking_time=min(float(matchmaking_time), 15.0),
+                                             allreduce_timeout=float(allreduce_timeout), device=device)
+                self.elastic = elastic
+                self.adopted = True
+                tracker_store = dist.PrefixStore("progress", rstore)
         if tracker_mode == "auto":
-            # asynchronous store records on a static group; the elastic generations keep the lockstep tracker
-            tracker_mode = "collective" if elastic is not None else "store"
+            # asynchronous store records on a static (or adopted) group; pure elastic generations keep
+            # the lockstep tracker
+            tracker_mode = "collective" if (elastic is not None and not self.adopted) else "store"
         self.tracker = ProgressTracker(dht=dht, prefix=run_id, target_batch_size=target_batch_size, group=process_group,
-                                       device=device, client_mode=client_mode, peer_id=peer_id, mode=tracker_mode)
+                                       device=device, client_mode=client_mode, peer_id=peer_id, mode=tracker_mode,
+                                       store=tracker_store)
         psgd = PowerSGD(flat_params, rank=powersgd_rank, group=process_group) if powersgd_rank else None
         self.grad_averager = GradientAverager(flat_params, arena=arena, group=process_group,
                                               reuse_grad_buffers=reuse_grad_buffers, compression=grad_compression,
@@ -408,7 +462,10 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                                                     average_state_every=average_state_every,
                                                     master=self._master, delay=delay_optimizer_step and self._master is not None,
                                                     averaging_timeout=averaging_timeout,
-                                                    skip_if_exact=skip_exact_state_averaging)
+                                                    # the CPU-offloaded LAMB reduces with threads: not
+                                                    # bitwise reproducible across peers, so never skip then
+                                                    skip_if_exact=skip_exact_state_averaging and offload_device is None,
+                                                    check_every=state_check_every)
         self.detached = False
         self.last_round_samples = 0  # this peer's samples in the last averaging round
         self.last_epoch_time = None
@@ -523,9 +580,6 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             return
         if self.tracker.ready_to_update_epoch:
             self._update_global_epoch(grad_scaler)
-            if self.elastic is not None and self.elastic.poll_join():
-                logger.info(f"{self.run_id}: a peer asked to join; regrouping at epoch {self.local_epoch}")
-                self._regroup()
 
     def _regroup(self):
         """New communicator over the live members, then one donor brings everyone (joiners, or
@@ -600,6 +654,13 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if self.verbose:
             logger.info(f"{self.run_id}: epoch {self.local_epoch} (averaged {int(total)} samples across "
                         f"{peers} peers in {self.last_epoch_time * 1e3:.1f} ms)")
+        # joiners are admitted at a round boundary that EVERY member passes through (training peers from
+        # step(), finished peers from leave()), so the poll's all-reduce always matches; a failed round
+        # regroups anyway -- never poll over a broken communicator
+        if self.elastic is not None and not self._comm_failed() and self.grad_averager.last_averaging_ok \
+                and self.elastic.poll_join():
+            logger.info(f"{self.run_id}: a peer asked to join; regrouping at epoch {self.local_epoch}")
+            self._regroup()
 
     # -- delayed parameter update ---------------------------------------------------------------------
     def finish_pending(self) -> bool:
@@ -696,7 +757,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                     logger.warning(f"{self.run_id}: collective failure while leaving ({e!r})")
                     self.detach()
                 continue
-            if int(store.add(done_key, 0)) >= world:
+            if int(store.add(done_key, 0)) >= _group_world(self.group)[0]:  # (a regroup may have changed it)
                 break
             time.sleep(poll)
         self.finish_pending()

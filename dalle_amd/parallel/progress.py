@@ -61,31 +61,90 @@ class GlobalTrainingProgress:
 
 
 class PerformanceEMA:
-    """Exponential moving average of samples/s (``tracker.performance_ema``)."""
+    """Exponential moving average of samples/s (``tracker.performance_ema``; the reference's throughput
+    metric, ``callback.py:63``, summed over peers by the aux peer, ``run_aux_peer.py:129,141``).
 
-    def __init__(self, alpha: float = 0.1, eps: float = 1e-20):
+    On a GPU peer the intervals are DEVICE time: every ``update`` records an event on the current stream
+    and an interval is the time between two consecutive events' completions on the device, read once the
+    later event has completed (non-blocking; the value lags the host by the queue depth). Host
+    ``perf_counter`` deltas between calls would measure how fast the host ENQUEUES work -- with no
+    per-step device sync they run ahead of the GPU (the warm-up queue fill biased the round-2 value up
+    to +11 % over wall clock). The first ``warmup`` intervals are dropped. On CPU peers the host clock is
+    the device clock."""
+
+    def __init__(self, alpha: float = 0.1, eps: float = 1e-20, device=None, warmup: int = 2):
         self.alpha, self.eps = alpha, eps
         self.ema_seconds_per_sample = 0.0
-        self.samples_per_second = 0.0
+        self._sps = 0.0
         self.num_updates = 0
         self.timestamp = time.perf_counter()
         self.paused = False
+        self.warmup = int(warmup)
+        self._seen = 0  # intervals observed (including the dropped warm-up ones)
+        dev = torch.device(device) if device is not None else None
+        self._events = dev is not None and dev.type == "cuda" and torch.cuda.is_available()
+        self._device = dev
+        self._pending = []   # (event, task_size, counted) in record order
+        self._last_event = None
+
+    def _record(self):
+        """An event on the current device stream (query / elapsed_time / synchronize)."""
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self._device))
+        return ev
+
+    def _ema(self, task_size: float, interval: float):
+        self._seen += 1
+        if self._seen <= self.warmup:
+            return
+        self.num_updates += 1
+        adjusted = self.alpha / (1 - (1 - self.alpha) ** self.num_updates)
+        self.ema_seconds_per_sample = adjusted * interval / task_size + (1 - adjusted) * self.ema_seconds_per_sample
+        self._sps = 1.0 / max(self.ema_seconds_per_sample, self.eps)
+
+    def _drain(self):
+        while self._pending and self._pending[0][0].query():
+            ev, task_size, counted = self._pending.pop(0)
+            if self._last_event is not None and counted and task_size > 0:
+                self._ema(task_size, self._last_event.elapsed_time(ev) / 1e3)
+            self._last_event = ev
+
+    @property
+    def samples_per_second(self) -> float:
+        if self._events:
+            self._drain()
+        return self._sps
+
+    @samples_per_second.setter
+    def samples_per_second(self, v: float):
+        self._sps = float(v)
 
     def update(self, task_size: float, interval: Optional[float] = None) -> float:
+        if self._events and interval is None:
+            self._pending.append((self._record(), float(task_size), not self.paused))
+            self._drain()
+            return self._sps
         now = time.perf_counter()
         if interval is None:
             interval = now - self.timestamp
         self.timestamp = now
         if task_size <= 0 or self.paused:
-            return self.samples_per_second
-        self.num_updates += 1
-        adjusted = self.alpha / (1 - (1 - self.alpha) ** self.num_updates)
-        self.ema_seconds_per_sample = adjusted * interval / task_size + (1 - adjusted) * self.ema_seconds_per_sample
-        self.samples_per_second = 1.0 / max(self.ema_seconds_per_sample, self.eps)
-        return self.samples_per_second
+            return self._sps
+        self._ema(task_size, interval)
+        return self._sps
+
+    def flush(self) -> float:
+        """Wait for every recorded event and fold in its interval (end of a measurement)."""
+        if self._events:
+            for ev, _, _ in self._pending:
+                ev.synchronize()
+            self._drain()
+        return self._sps
 
     def reset_timer(self):
         self.timestamp = time.perf_counter()
+        self._last_event = None
+        self._pending = [(ev, t, False) for ev, t, _ in self._pending]
 
     def pause(self):
         self.paused = True
@@ -99,7 +158,7 @@ class ProgressTracker:
     def __init__(self, dht=None, prefix: str = "run", target_batch_size: int = 4096, group=None, device=None,
                  client_mode: bool = False, peer_id: str = "local", mode: str = "collective",
                  metadata_expiration: float = 60.0, report_period: float = 1.0, performance_ema_alpha: float = 0.1,
-                 max_wait_time: Optional[float] = None):
+                 max_wait_time: Optional[float] = None, store=None):
         self.dht, self.prefix = dht, prefix
         self.target_batch_size = target_batch_size
         self.group = group
@@ -112,13 +171,14 @@ class ProgressTracker:
         self.mode = mode
         self.store = None
         if mode == "store":
-            self.store = dist.distributed_c10d._get_default_store()
+            # the job's store (torchrun: hosted by the elastic agent), or an explicit long-lived one
+            self.store = store if store is not None else dist.distributed_c10d._get_default_store()
             self._ns = f"collab/{prefix}"
             self._reported = 0  # samples of the current epoch already added to the shared counter
         self.metadata_expiration = metadata_expiration
         self.report_period = report_period
         self.max_wait_time = max_wait_time
-        self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha)
+        self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha, device=self.device)
         self.local_progress = LocalTrainingProgress(peer_id, 0, 0, 0.0, get_dht_time(), client_mode)
         self.global_progress = GlobalTrainingProgress(0, 0, target_batch_size, 1, int(client_mode), float("inf"), 0.0)
         self.max_epoch_seen = 0

@@ -88,9 +88,11 @@ def parse_devices(spec):
     return [d if (d.startswith("cuda") or d == "cpu") else f"cuda:{int(d)}" for d in spec.split(",")]
 
 
-def run_queries(queries, per_device, work):
+def run_queries(queries, per_device, work, device_of=None):
     """Spread ``queries`` over the devices: one worker thread per entry of ``per_device`` (its device's
-    model copy and state), each taking the next unclaimed query -- GPUs finish at their own pace."""
+    model copy and state), each taking the next unclaimed query -- GPUs finish at their own pace.
+    ``device_of(ctx)`` names the entry's device: its thread makes it the CURRENT device, so streams,
+    graph captures and the native ops' stream lookups bind to that GPU and not to GPU 0."""
     import queue
     import threading
 
@@ -100,6 +102,9 @@ def run_queries(queries, per_device, work):
     errors = []
 
     def worker(ctx):
+        dev = torch.device(device_of(ctx)) if device_of is not None else None
+        if dev is not None and dev.type == "cuda":
+            torch.cuda.set_device(dev)
         while not errors:
             try:
                 item = q.get_nowait()
@@ -156,8 +161,10 @@ def main(argv=None):
     if args.model is not None:
         print(f'[*] Model modification time: {datetime.fromtimestamp(os.stat(args.model).st_mtime)}')
         state_dict = normalize_state_dict_keys(torch.load(args.model, map_location="cpu", weights_only=True))
-        ok = model.load_state_dict(state_dict, strict=False)
-        print(f'[*] Loaded model: {ok}')
+        from dalle_amd.utils.checkpoint import load_state_dict_checked
+
+        tolerated = load_state_dict_checked(model, state_dict)  # strict, as the reference (run_inference.py:119)
+        print(f'[*] Loaded model' + (f' (recomputed buffers: {tolerated})' if tolerated else ''))
     else:
         print('[*] No --model given: random-init weights')
 
@@ -196,7 +203,7 @@ def main(argv=None):
             outputs = {'query': query, 'temperature': args.temperature, 'images': images, 'clip_scores': clip_scores}
             pickle.dump(outputs, f)
 
-    run_queries(queries, list(zip(models, clip_models, devices)), work)
+    run_queries(queries, list(zip(models, clip_models, devices)), work, device_of=lambda ctx: ctx[2])
 
 
 if __name__ == '__main__':

@@ -103,6 +103,10 @@ class BatchingGenerator:
 
     def _loop(self):
         torch.set_grad_enabled(False)
+        if self.device.type == "cuda":
+            # this thread's current device = the generator's: streams, hipGraph captures and the native
+            # ops' stream lookups must bind to that GPU, not to GPU 0
+            torch.cuda.set_device(self.device)
         while True:
             first = self._next(None)
             if first is None:

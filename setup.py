@@ -23,6 +23,7 @@ hip_sources = [
     "csrc/kernels/xent.hip",
     "csrc/kernels/decode.hip",
     "csrc/kernels/gemm.hip",
+    "csrc/kernels/gemm_pt.hip",
     "csrc/kernels/quant.hip",
     "csrc/kernels/skinny.hip",
     "csrc/kernels/sample.hip",

@@ -85,3 +85,34 @@ def test_state_zip_and_optimizer_state(tmp_path):
     for n, p in model.named_parameters():
         assert torch.equal(p, before[n]), n
     assert opt.local_epoch == 1
+
+
+def test_mis_keyed_checkpoints_are_rejected(tmp_path):
+    """Both loaders are strict (reference inference/run_inference.py:119): a checkpoint with a renamed
+    key must raise instead of silently keeping the current weights for that key -- the inference loader
+    (with its explicit allow-list of recomputed buffers) and the backup restore (whose optimizer state
+    would otherwise be loaded next to stale weights)."""
+    import pytest
+
+    from callback import CollaborativeCallback
+    from dalle_amd.utils.checkpoint import load_state_dict_checked
+
+    task, peer = _task(tmp_path)
+    sd = task.model.state_dict()
+    # the full key set loads; a derived buffer may be absent (it is recomputed from the config)
+    assert load_state_dict_checked(task.model, sd) == []
+    no_buf = {k: v for k, v in sd.items() if not k.endswith("pos_emb")}
+    assert all(k.endswith("pos_emb") for k in load_state_dict_checked(task.model, no_buf))
+    bad = dict(sd)
+    key = next(k for k in bad if k.endswith("to_qkv.weight"))
+    bad[key.replace("to_qkv", "to_qkv_renamed")] = bad.pop(key)
+    with pytest.raises(RuntimeError, match="does not match"):
+        load_state_dict_checked(task.model, bad)
+
+    cb = CollaborativeCallback(task, peer)
+    cb.backup_state()
+    snap = torch.load(peer.state_path, weights_only=True)
+    snap["model"] = bad
+    torch.save(snap, peer.state_path)
+    with pytest.raises(RuntimeError):
+        cb.restore_from_backup(peer.state_path)

@@ -260,10 +260,12 @@ def test_heterogeneous_peers_contribute_at_their_own_pace():
 
 
 # ------------------------------------------------------------------------------------------------
-def _dead_peer_worker(rank, world, port, q):
+def _dead_peer_worker(rank, world, port, q, recovery, coord_port):
     try:
         if rank == 2:
             os.environ["DALLE_AMD_FAULT_KILL_IN_AVERAGING"] = "1"
+        if coord_port:
+            os.environ["DALLE_AMD_COORDINATOR"] = f"127.0.0.1:{coord_port}"
         _init(rank, world, port)
         from dalle_amd.parallel.optimizer import CollaborativeOptimizer
 
@@ -272,7 +274,8 @@ def _dead_peer_worker(rank, world, port, q):
         p.grad = torch.zeros_like(p)
         opt = CollaborativeOptimizer(run_id="dead", params=[p], optimizer=lambda ps: torch.optim.SGD(ps, lr=1.0),
                                      target_batch_size=3, batch_size_per_step=1, reuse_grad_buffers=True,
-                                     averaging_timeout=20.0, tracker_mode="static")
+                                     averaging_timeout=20.0, allreduce_timeout=10.0, matchmaking_time=1.0,
+                                     tracker_mode="static", recovery=recovery)
         epochs_grads = []
         while opt.local_epoch < 4:
             g = torch.full_like(p, float(rank + 1) * (opt.local_epoch + 1))
@@ -281,31 +284,64 @@ def _dead_peer_worker(rank, world, port, q):
             e = opt.local_epoch
             opt.step()
             epochs_grads.append((e, (before - p.detach()).mean().item()))
-        q.put(pickle.dumps((rank, opt.detached, epochs_grads)))
+        regroups = opt.elastic.regroups if opt.elastic is not None else 0
+        world_after = opt.elastic.world_size if opt.elastic is not None else 1
+        q.put(pickle.dumps((rank, opt.detached, epochs_grads, p.detach().clone(), regroups, world_after)))
     except Exception:  # pragma: no cover
         import traceback
 
         q.put(pickle.dumps(("error", rank, traceback.format_exc())))
 
 
-def test_dead_peer_mid_averaging_survivors_fall_back_and_continue():
-    """Non-elastic path: a rank SIGKILLed inside the epoch-1 averaging round. The survivors' round fails,
-    the communicator is aborted, they apply their OWN gradients for that epoch and keep training alone."""
+def _run_with_dead_peer(recovery, coordinator):
     port = _free_port()
+    server = None
+    coord_port = 0
+    if coordinator:  # a store that outlives every trainer (the torchrun agent's role)
+        coord_port = _free_port()
+        server = dist.TCPStore("127.0.0.1", coord_port, world_size=None, is_master=True, wait_for_workers=False)
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 3, port, q)) for r in range(3)]
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 3, port, q, recovery, coord_port)) for r in range(3)]
     for p in procs:
         p.start()
     res = sorted([pickle.loads(q.get()) for _ in range(2)], key=lambda r: r[0])
     for p in procs:
         p.join(60)
+        if p.is_alive():
+            p.kill()
+    del server
     for r in res:
         assert r[0] != "error", r[2]
-    for rank, detached, steps in res:
+    return res
+
+
+def test_dead_peer_survivors_regroup_and_keep_averaging():
+    """Default path with a store that outlives the trainers: a rank SIGKILLed inside the epoch-1 averaging
+    round. The survivors' round fails (each applies its own gradient), they abort the communicator,
+    re-form a 2-peer group, sync from the donor (rank 0) and average WITH EACH OTHER from epoch 2 on."""
+    res = _run_with_dead_peer("auto", coordinator=True)
+    (_, d0, s0, p0, n0, w0), (_, d1, s1, p1, n1, w1) = res
+    assert not d0 and not d1
+    assert n0 == n1 == 1 and w0 == w1 == 2
+    assert torch.equal(p0, p1)
+    u0, u1 = dict(s0), dict(s1)
+    for upd in (u0, u1):
+        assert abs(upd[0] - 2.0) < 1e-5, upd            # 3 peers: (1 + 2 + 3) / 3
+        # failed round: each survivor applied its own gradient, then the new group synced from its donor
+        assert min(abs(upd[1] - 2.0), abs(upd[1] - 4.0)) < 1e-5, upd
+        assert abs(upd[2] - 1.5 * 3) < 1e-5, upd        # 2 peers: (1 + 2) / 2 * (e + 1)
+        assert abs(upd[3] - 1.5 * 4) < 1e-5, upd
+    assert u0[1] == u1[1]
+
+
+def test_dead_peer_without_recovery_store_detaches():
+    """recovery="detach" (or no store that outlives the trainers): the survivors abort the communicator,
+    apply their OWN gradients for that epoch and keep training alone."""
+    res = _run_with_dead_peer("detach", coordinator=False)
+    for rank, detached, steps, _, _, _ in res:
         assert detached
         upd = dict(steps)
-        # epoch 0: averaged over 3 peers -> mean grad (1+2+3)/3 = 2 ; epoch >= 1: own grad (rank+1)*(e+1)
         assert abs(upd[0] - 2.0) < 1e-5, upd
         assert abs(upd[1] - (rank + 1) * 2.0) < 1e-5, upd
         assert abs(upd[3] - (rank + 1) * 4.0) < 1e-5, upd

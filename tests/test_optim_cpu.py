@@ -238,3 +238,46 @@ def test_delegating_optimizer():
     opt.zero_grad()
     assert p.grad is None
     assert "Counting(" in repr(opt)
+
+
+class _FakeDevice:
+    """A device timeline that runs each step in `dev_ms` while the host enqueues every `host_ms`."""
+
+    def __init__(self, dev_ms):
+        self.dev_ms, self.t_dev, self.t_host = dev_ms, 0.0, 0.0
+
+    def record(self):
+        dev = self
+        self.t_dev = max(self.t_dev, self.t_host) + self.dev_ms  # the step's kernels finish at t_dev
+        done_at = self.t_dev
+
+        class Ev:
+            t = done_at
+
+            def query(self_):
+                return dev.t_host >= self_.t
+
+            def elapsed_time(self_, other):
+                return other.t - self_.t
+
+            def synchronize(self_):
+                dev.t_host = max(dev.t_host, self_.t)
+        return Ev()
+
+
+def test_performance_ema_measures_device_time_not_enqueue_rate():
+    """The reference's metric (tracker.performance_ema, callback.py:63): with a GPU stream that takes 10 ms
+    per step while the host enqueues a step every 1 ms, the EMA must report the device's 100 steps/s
+    (host perf_counter deltas would report ~1000)."""
+    from dalle_amd.parallel.progress import PerformanceEMA
+
+    fake = _FakeDevice(dev_ms=10.0)
+    ema = PerformanceEMA(alpha=0.1, warmup=2)
+    ema._events = True
+    ema._record = fake.record
+    for _ in range(60):
+        fake.t_host += 1.0  # the host runs ahead
+        ema.update(task_size=4)
+    ema.flush()
+    assert abs(ema.samples_per_second - 4 / 0.010) / (4 / 0.010) < 0.01, ema.samples_per_second
+    assert ema.num_updates == 59 - 2  # 59 intervals, the first 2 dropped as warm-up

@@ -166,3 +166,17 @@ def test_tokenizer_core_under_sanitizers(kind, t5_dir, tmp_path):
     assert "WARNING: ThreadSanitizer" not in report and "ERROR: AddressSanitizer" not in report, report[-4000:]
     assert "runtime error:" not in report, report[-4000:]
     assert "tokenizer fuzz ok" in r.stdout
+
+
+def test_encode_batch_worker_errors_raise_in_python():
+    """A worker thread's exception is re-raised on the calling thread as a Python exception (ADVICE r2:
+    it used to std::terminate the data-loader process); an unconfigured pipeline raises instead of
+    dereferencing an empty model."""
+    import pytest
+
+    tok = pytest.importorskip("dalle_amd._tokenizer")
+    p = tok.Pipeline()
+    with pytest.raises(RuntimeError, match="no model"):
+        p.encode("abc")
+    with pytest.raises(RuntimeError, match="no model"):
+        p.encode_batch(["abc def"] * 200, threads=4)
