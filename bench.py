@@ -46,6 +46,7 @@ METRIC = "training samples/sec (whole node), DALL-E d_model=1024 at 1/2/4/8 MI35
 MODEL_NAMES = {
     "bench24": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
     "dalle-1024-24l": "DALL-E d_model=1024, 24 layers, 256 text + 32x32 image tokens",
+    "dalle-1024-24l-unshared": "DALL-E d_model=1024, 24 layers (no weight sharing), 256 text + 32x32 image tokens",
     "reference": "DALL-E d_model=1024, 64 layers (5 shared blocks), reversible, 256 text + 32x32 image tokens",
     "dalle-1.3b": "DALL-E ~1.3B, reversible, 256 text + 32x32 image tokens",
     "tiny": "DALL-E tiny (2 layers, 64 text + 16x16 image tokens)",
@@ -94,14 +95,32 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpu_count():
+    """GPUs this process may use, WITHOUT any HIP call (the launcher must not initialise the runtime):
+    the *_VISIBLE_DEVICES lists if set, else the KFD topology's GPU nodes; None if unknown."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(root):
+            with open(os.path.join(root, node, "gpu_id")) as fh:
+                n += int(fh.read().strip() or 0) != 0
+        return n
+    except OSError:
+        return None
+
+
 def spawn_workers(n: int) -> int:
     """Run this script as ``n`` ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* like torchrun) and return
-    the first non-zero exit code (the others are terminated), or 0. The parent never initialises
-    HIP: ``torch.cuda.device_count()`` only reads the device list on this stack."""
+    the first non-zero exit code (the others are terminated), or 0. The parent never touches HIP: the
+    device count comes from the environment / sysfs (visible_gpu_count)."""
     backend = os.environ.get("BENCH_BACKEND", "nccl")
     if backend == "nccl":
-        ndev = torch.cuda.device_count()
-        if ndev < n:
+        ndev = visible_gpu_count()
+        if ndev is not None and ndev < n:
             print(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible", file=sys.stderr)
             return 2
     port = _free_port()
@@ -261,6 +280,12 @@ def run_rank(args) -> None:
     if world > 1:
         dist.barrier()
     sync()
+    comm = sync_grads if (args.engine == "step" and world > 1 and args.compression == "none") else None
+    if comm is not None:
+        comm.reset_stats()
+        comm.timing = use_cuda
+    if use_cuda:
+        torch.cuda.reset_peak_memory_stats(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
@@ -281,6 +306,36 @@ def run_rank(args) -> None:
         names = names_all
     elapsed = max(per_rank)
     final_loss = float(loss.item())
+    peak_gb = round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2) if use_cuda else None
+    comm_stats = None
+    if comm is not None:
+        comm.timing = False
+        exposed = comm.exposed_ms() / args.steps if use_cuda else None
+        step_bytes = comm.bytes_reduced / args.steps
+        overlapped = round(comm.last_early_elems / max(1, arena.numel), 3)
+        # the same all-reduce (same buckets) alone, to price the bytes: bus bandwidth as nccl-tests reports it
+        g = arena.grad
+        saved = g.clone()
+        sync()
+        dist.barrier()
+        ta = time.perf_counter()
+        for _ in range(3):
+            comm.all_reduce()
+        sync()
+        t_ar = (time.perf_counter() - ta) / 3
+        g.copy_(saved)
+        del saved
+        t_all = [None] * world
+        dist.all_gather_object(t_all, t_ar)
+        t_ar = max(t_all)
+        comm_stats = {"bytes_per_step": int(step_bytes), "standalone_ms": round(t_ar * 1e3, 3),
+                      "busbw_GBps": round(2 * (world - 1) / world * step_bytes / t_ar / 1e9, 1),
+                      "exposed_ms_per_step": None if exposed is None else round(exposed, 3),
+                      "overlapped_frac": overlapped}
+    peaks = [peak_gb]
+    if world > 1:
+        peaks = [None] * world
+        dist.all_gather_object(peaks, peak_gb)
     ema = None
     if args.engine == "collab":
         mine = copt.tracker.performance_ema.flush()  # every recorded step's device interval folded in
@@ -337,11 +392,14 @@ def run_rank(args) -> None:
         if ema is not None:
             out["collab_performance_ema_samples_per_s"] = round(ema, 3)
             out["collab_ema_over_wall"] = round(ema / value, 4)
+            out["collab_backward_overlapped_rounds"] = copt.grad_averager.overlapped_rounds
             if use_cuda and args.steps >= 5 and abs(ema / value - 1.0) > 0.03:
                 # the reference's metric (callback.py:63) must report what the wall clock sees
                 raise SystemExit(f"performance_ema {ema:.2f} samples/s deviates > 3 % from the wall clock {value:.2f}")
-        if args.engine == "step" and world > 1 and args.compression == "none":
-            out["grad_allreduce_overlapped_frac"] = round(sync_grads.last_early_elems / max(1, arena.numel), 3)
+        out["per_rank_peak_mem_gb"] = peaks
+        if comm_stats is not None:
+            out["grad_allreduce"] = comm_stats
+            out["grad_allreduce_overlapped_frac"] = comm_stats["overlapped_frac"]
         if os.environ.get("BENCH_DUMP_PARAMS"):
             out["param_checksum"] = float(arena.data.double().sum())
         print(json.dumps(out), flush=True)

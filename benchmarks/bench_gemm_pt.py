@@ -49,8 +49,11 @@ def main():
         B = torch.randn(N, K, device=dev).bfloat16()
         v = {"hipblaslt": lambda: torch.mm(A, B.t()), "8ph": lambda: C.gemm_nt(A, B, None, 300)}
         for g in groups:
-            v[f"pt_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 0, g))
-        v["pt_mainloop"] = lambda: C.gemm_pt(A, B, None, 5, 0)
+            v[f"pt_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 20, g))
+            v[f"np_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 10, g))
+        v["pt_mainloop"] = lambda: C.gemm_pt(A, B, None, 25, 0)
+        v["np_mainloop"] = lambda: C.gemm_pt(A, B, None, 15, 0)
+        v["8ph_mainloop"] = lambda: C.gemm_nt(A, B, None, 350)
         t = run(v)
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": f"M{M}_N{N}_K{K}", "us": t, "TF": {k: round(fl / x / 1e6) for k, x in t.items()}}), flush=True)
@@ -68,6 +71,7 @@ def main():
     cs = hip_ops.rope_cs_table(geom, 64, dev)
     t = run({"qkv_rope_8ph": lambda: C.qkv_rope(h, wq, cos, sin, T, S, H, n, False, 0.125),
              "qkv_rope_pt": lambda: C.qkv_rope_pt(h, wq, cs, T, S, H, n, False, 0.125),
+             "qkv_rope_pt_persist": lambda: C.qkv_rope_pt(h, wq, cs, T, S, H, n, False, 0.125, 1),
              "hipblaslt+rope": lambda: C.rope_fwd(torch.mm(h, wq.t()).view(B, n, -1), cos, sin, T, S, H, False, 0.125)})
     print(json.dumps({"op": "qkv_rope", "us": t}), flush=True)
 
@@ -77,14 +81,16 @@ def main():
     w1b, b1b = w1.bfloat16(), b1.bfloat16()
     w1i, b1i = w1[perm].bfloat16().contiguous(), b1[perm].bfloat16().contiguous()
     t = run({"hipblaslt+geglu": lambda: C.geglu_fwd(torch.addmm(b1b, h, w1b.t())),
-             "ff_in_geglu_pt": lambda: C.ff_in_geglu_pt(h, w1i, b1i)})
+             "ff_in_geglu_pt": lambda: C.ff_in_geglu_pt(h, w1i, b1i),
+             "ff_in_geglu_pt_persist": lambda: C.ff_in_geglu_pt(h, w1i, b1i, 1)})
     print(json.dumps({"op": "ff_in_geglu", "us": t}), flush=True)
 
     dy = (0.5 * torch.randn(B * n, D, device=dev)).bfloat16()
     w2t = (0.03 * torch.randn(F, D, device=dev)).bfloat16()
     a = torch.randn(B * n, 2 * F, device=dev).bfloat16()
     t = run({"ff_dgrad_geglu_8ph": lambda: C.ff_dgrad_geglu(dy, w2t, a),
-             "ff_dgrad_geglu_pt": lambda: C.ff_dgrad_geglu_pt(dy, w2t, a)})
+             "ff_dgrad_geglu_pt": lambda: C.ff_dgrad_geglu_pt(dy, w2t, a),
+             "ff_dgrad_geglu_pt_persist": lambda: C.ff_dgrad_geglu_pt(dy, w2t, a, None, 1)})
     print(json.dumps({"op": "ff_dgrad_geglu", "us": t}), flush=True)
 
 

@@ -76,9 +76,9 @@ bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, i
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
-                      hipStream_t);
-bool gemm_pt_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
-bool gemm_pt_geglu_fwd(const void*, const void*, const void*, void*, void*, int, int, int, hipStream_t);
+                      hipStream_t, int);
+bool gemm_pt_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
+bool gemm_pt_geglu_fwd(const void*, const void*, const void*, void*, void*, int, int, int, hipStream_t, int);
 void permlane16_probe(unsigned*, hipStream_t);
 void rope_pad_zero(void*, void*, void*, int, int, int, int, hipStream_t);
 void lamb_grad_norm(const float*, long, float*, float, float*, float*, hipStream_t);
@@ -510,7 +510,7 @@ Tensor gemm_pt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant, 
 
 // QKV projection + rotary (persistent kernel): cs = (n + 1, 32, 2) fp32 (cos, sin) per rotary pair
 std::vector<Tensor> qkv_rope_pt(Tensor h, Tensor w, Tensor cs, int64_t T, int64_t S, int64_t H, int64_t n, bool col_major,
-                                double qscale) {
+                                double qscale, int64_t persist) {
   CHECK_IN(h, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16); CHECK_IN(cs, torch::kFloat32);
   TORCH_CHECK(h.dim() == 2 && w.dim() == 2 && w.size(0) == 3 * H * 64 && w.size(1) == h.size(1), "qkv_rope_pt: shapes");
   const int M = h.size(0), K = h.size(1);
@@ -523,14 +523,14 @@ std::vector<Tensor> qkv_rope_pt(Tensor h, Tensor w, Tensor cs, int64_t T, int64_
   auto k = torch::empty({B * H, g.Np, 64}, opts);
   auto v = torch::empty({B * H, g.Np, 64}, opts);
   TORCH_CHECK(dalle::gemm_pt_qkv_rope(h.data_ptr(), w.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cs.data_ptr<float>(), M,
-                                      K, H, T, S, n, col_major ? 1 : 0, (float)qscale, cur_stream()),
+                                      K, H, T, S, n, col_major ? 1 : 0, (float)qscale, cur_stream(), (int)persist),
               "qkv_rope_pt: unsupported shape");
   dalle::rope_pad_zero(q.data_ptr(), k.data_ptr(), v.data_ptr(), g.Tp, T, g.Np, B * H, cur_stream());
   return {q, k, v};
 }
 
 // FF-out dgrad + GEGLU backward (persistent kernel): dy (M, K), w2t = W2^T (F, K), h (M, 2F) -> (dh, dbias)
-std::vector<Tensor> ff_dgrad_geglu_pt(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
+std::vector<Tensor> ff_dgrad_geglu_pt(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb, int64_t persist) {
   CHECK_IN(dy, torch::kBFloat16); CHECK_IN(w2t, torch::kBFloat16); CHECK_IN(h, torch::kBFloat16);
   TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2, "ff_dgrad_geglu_pt: 2-D operands");
   const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
@@ -545,7 +545,7 @@ std::vector<Tensor> ff_dgrad_geglu_pt(Tensor dy, Tensor w2t, Tensor h, c10::opti
     pb = db.data_ptr<float>();
   }
   TORCH_CHECK(dalle::gemm_pt_geglu_bwd(dy.data_ptr(), w2t.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), M, F, K,
-                                       cur_stream()), "ff_dgrad_geglu_pt: unsupported shape");
+                                       cur_stream(), (int)persist), "ff_dgrad_geglu_pt: unsupported shape");
   dalle::column_sum(part.data_ptr<float>(), M / 64, 2 * F, dalle::GradSink{pb, nullptr, nullptr, (int)(2 * F), db.defined() ? 0 : 1},
                     cur_stream());
   return {dh, db};
@@ -553,7 +553,7 @@ std::vector<Tensor> ff_dgrad_geglu_pt(Tensor dy, Tensor w2t, Tensor h, c10::opti
 
 // FF-in GEMM + GEGLU forward (persistent kernel): x (M, K), w1i / b1i = W1 / b1 rows interleaved per 64-row
 // group ([32 value | 32 gate]) -> a (M, 2F) pre-activation in the original [value | gate] order, u (M, F)
-std::vector<Tensor> ff_in_geglu_pt(Tensor x, Tensor w1i, c10::optional<Tensor> b1i) {
+std::vector<Tensor> ff_in_geglu_pt(Tensor x, Tensor w1i, c10::optional<Tensor> b1i, int64_t persist) {
   CHECK_IN(x, torch::kBFloat16); CHECK_IN(w1i, torch::kBFloat16);
   TORCH_CHECK(x.dim() == 2 && w1i.dim() == 2 && x.size(1) == w1i.size(1), "ff_in_geglu_pt: x (M, K), w1i (2F, K)");
   const int M = x.size(0), K = x.size(1), F2 = w1i.size(0);
@@ -566,7 +566,8 @@ std::vector<Tensor> ff_in_geglu_pt(Tensor x, Tensor w1i, c10::optional<Tensor> b
   }
   auto a = torch::empty({M, F2}, x.options());
   auto u = torch::empty({M, F2 / 2}, x.options());
-  TORCH_CHECK(dalle::gemm_pt_geglu_fwd(x.data_ptr(), w1i.data_ptr(), bp, a.data_ptr(), u.data_ptr(), M, F2 / 2, K, cur_stream()),
+  TORCH_CHECK(dalle::gemm_pt_geglu_fwd(x.data_ptr(), w1i.data_ptr(), bp, a.data_ptr(), u.data_ptr(), M, F2 / 2, K, cur_stream(),
+                                       (int)persist),
               "ff_in_geglu_pt: unsupported shape");
   return {a, u};
 }
@@ -1168,9 +1169,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
-  m.def("qkv_rope_pt", &qkv_rope_pt);
-  m.def("ff_dgrad_geglu_pt", &ff_dgrad_geglu_pt, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
-  m.def("ff_in_geglu_pt", &ff_in_geglu_pt, py::arg("x"), py::arg("w1i"), py::arg("b1i") = py::none());
+  m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),
+        py::arg("n"), py::arg("col_major"), py::arg("qscale"), py::arg("persist") = -1);
+  m.def("ff_dgrad_geglu_pt", &ff_dgrad_geglu_pt, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none(),
+        py::arg("persist") = -1);
+  m.def("ff_in_geglu_pt", &ff_in_geglu_pt, py::arg("x"), py::arg("w1i"), py::arg("b1i") = py::none(), py::arg("persist") = -1);
   m.def("permlane16_probe", &permlane16_probe);
   m.def("gemm_wgrad_", &gemm_wgrad_, py::arg("G"), py::arg("X"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);

@@ -343,7 +343,10 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
   }
 }
 
-template <int EPI>
+// PERSIST = false: one tile per workgroup (grid = tile count), the same main loop and register-direct
+// epilogue -- a workgroup's stores then drain while the NEXT workgroup on that CU already streams its
+// first K-tiles (the epilogue ends with the store issue; nothing waits for completion)
+template <int EPI, bool PERSIST = true>
 __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                  int M, int N, int K, PtArgs e) {
   using namespace pt;
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   const int tiles_m = M / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
   const int nk = K / BK;  // >= 2 (host-checked)
   const int G = gridDim.x;
-  const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
+  const int my_tiles = PERSIST ? (ntiles - (int)blockIdx.x + G - 1) / G : 1;
   const int total = my_tiles * nk;
 
   auto origin = [&](int it, int& r0, int& c0) {
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
       const __bf16* Bhi = slot(buf, 2);
       const __bf16* Ahi = slot(buf, 3);
       // sources of K-steps g + 1 and g + 2 (the next tile's first K-steps near the end of a tile)
-      const bool x1 = kt + 1 >= nk, x2 = kt + 2 >= nk;
+      const bool x1 = PERSIST && kt + 1 >= nk, x2 = PERSIST && kt + 2 >= nk;
       const int r1 = x1 ? nr : cr, c1 = x1 ? nc : cc, k1 = x1 ? kt + 1 - nk : kt + 1;
       const int r2 = x2 ? nr : cr, c2 = x2 ? nc : cc, k2 = x2 ? kt + 2 - nk : kt + 2;
       const bool s1 = g + 1 < total, s2 = g + 2 < total;
@@ -532,11 +535,24 @@ static int pt_grid(int ntiles) {
   return g;
 }
 
+static int pt_persist_default() {
+  static const int v = [] {
+    const char* s = getenv("DALLE_AMD_PT_PERSIST");
+    return s ? atoi(s) : 0;
+  }();
+  return v;
+}
+
 template <int EPI>
-static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st) {
+static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist = -1) {
   const int ntiles = (M / pt::BM) * (N / pt::BN);
-  hipLaunchKernelGGL((gemm_pt_kernel<EPI>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
-                     (const __bf16*)B, M, N, K, e);
+  if (persist < 0) persist = pt_persist_default();
+  if (persist)
+    hipLaunchKernelGGL((gemm_pt_kernel<EPI, true>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
+                       (const __bf16*)B, M, N, K, e);
+  else
+    hipLaunchKernelGGL((gemm_pt_kernel<EPI, false>), dim3(ntiles), dim3(pt::THREADS), 0, st, (const __bf16*)A,
+                       (const __bf16*)B, M, N, K, e);
 }
 
 static bool pt_shape_ok(int M, int N, int K) { return M > 0 && N > 0 && M % pt::BM == 0 && N % pt::BN == 0 && K % pt::BK == 0 && K >= 2 * pt::BK; }
@@ -558,14 +574,16 @@ bool gemm_pt(const void* A, const void* B, void* C, const void* bias, int M, int
   e.bias = (const __bf16*)bias;
   e.ldc = ldc;
   e.group = group ? group : pt_group_default();
-  if (epi == 5) pt_launch<5>(A, B, M, N, K, e, st);
-  else pt_launch<0>(A, B, M, N, K, e, st);
+  // epi: 0 plain, 5 main loop only; +10 = one tile per workgroup, +20 = persistent (default: env)
+  const int persist = epi >= 20 ? 1 : (epi >= 10 ? 0 : -1);
+  if (epi % 10 == 5) pt_launch<5>(A, B, M, N, K, e, st, persist);
+  else pt_launch<0>(A, B, M, N, K, e, st, persist);
   return true;
 }
 
 // QKV projection + rotary into the attention storage layout (q pre-scaled); cs = (n + 1, 32, 2) fp32
 bool gemm_pt_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, const float* cs, int M, int K, int H, int T,
-                      int S, int n, int col_major, float qscale, hipStream_t st) {
+                      int S, int n, int col_major, float qscale, hipStream_t st, int persist) {
   const int N = 3 * H * 64;
   if (!pt_shape_ok(M, N, K) || M % n) return false;
   int logS = 0;
@@ -585,13 +603,14 @@ bool gemm_pt_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, c
   e.col_major = col_major;
   e.qscale = qscale;
   e.group = pt_group_default();
-  pt_launch<1>(A, W, M, N, K, e, st);
+  pt_launch<1>(A, W, M, N, K, e, st, persist);
   return true;
 }
 
 // FF-out dgrad + GEGLU backward: du = dy (M, K) . W2 with w2t = W2^T (F, K); h (M, 2F) -> dh (M, 2F) and
 // part (M / 64, 2F) partial bias grads
-bool gemm_pt_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, float* part, int M, int F, int K, hipStream_t st) {
+bool gemm_pt_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, float* part, int M, int F, int K, hipStream_t st,
+                       int persist) {
   if (!pt_shape_ok(M, F, K)) return false;
   PtArgs e{};
   e.h = (const __bf16*)h;
@@ -599,14 +618,15 @@ bool gemm_pt_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh,
   e.part = part;
   e.F = F;
   e.group = pt_group_default();
-  pt_launch<2>(dy, w2t, M, F, K, e, st);
+  pt_launch<2>(dy, w2t, M, F, K, e, st, persist);
   return true;
 }
 
 // FF-in GEMM + GEGLU forward: x (M, K) . W1i^T where W1i (2F, K) holds W1's rows interleaved per
 // 64-row group ([32 value rows | the 32 matching gate rows]) and b1i the same permutation of b1 ->
 // a (M, 2F) in the original [value | gate] order and u = value * gelu(gate) (M, F)
-bool gemm_pt_geglu_fwd(const void* x, const void* w1i, const void* b1i, void* a, void* u, int M, int F, int K, hipStream_t st) {
+bool gemm_pt_geglu_fwd(const void* x, const void* w1i, const void* b1i, void* a, void* u, int M, int F, int K, hipStream_t st,
+                       int persist) {
   if (!pt_shape_ok(M, 2 * F, K) || F % 32) return false;
   PtArgs e{};
   e.bias = (const __bf16*)b1i;
@@ -614,7 +634,7 @@ bool gemm_pt_geglu_fwd(const void* x, const void* w1i, const void* b1i, void* a,
   e.u = (__bf16*)u;
   e.F = F;
   e.group = pt_group_default();
-  pt_launch<3>(x, w1i, M, 2 * F, K, e, st);
+  pt_launch<3>(x, w1i, M, 2 * F, K, e, st, persist);
   return true;
 }
 

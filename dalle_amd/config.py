@@ -156,6 +156,20 @@ def bench24() -> DALLEConfig:
     )
 
 
+def bench24_unshared() -> DALLEConfig:
+    """BASELINE config 2 without weight sharing: 24 layers with their own attention / FF weights
+    (~444M unique parameters), so the data-parallel gradient all-reduce moves every layer's bytes
+    (bench24 shares 5 blocks, 126M gradients, which flatters a scaling curve's comm/compute overlap)."""
+    depth = 24
+    return DALLEConfig(
+        depth=depth,
+        attn_types=reference_attn_types(depth),
+        shared_attn_ids=list(range(depth)),
+        shared_ff_ids=list(range(depth)),
+        reversible=False,
+    )
+
+
 def tiny(reversible: bool = True) -> DALLEConfig:
     """BASELINE config 1: 2 layers, 64 text + 16x16 image tokens."""
     depth = 2
@@ -197,6 +211,7 @@ PRESETS = {
     "dalle-1024-64l": reference,
     "bench24": bench24,
     "dalle-1024-24l": bench24,
+    "dalle-1024-24l-unshared": bench24_unshared,
     "tiny": tiny,
     "dalle-1.3b": large_1p3b,
 }

@@ -17,8 +17,8 @@ what is left (tied embedding / head, final LayerNorm) and waits. In the bench24 
 backward; in an unshared model almost everything overlaps. Requires one ``all_reduce()`` per
 ``backward()`` (no local accumulation across micro-batches while attached).
 
-``grad_dtype='bf16'`` halves the bytes on the wire (the averaged gradient is accumulated in fp32
-by RCCL's reduction of bf16 inputs is bf16 -- use for large worlds only).
+``grad_dtype='bf16'`` halves the bytes on the wire (RCCL then reduces in bf16, so the averaged gradient
+carries bf16 rounding -- use for large worlds only).
 """
 from __future__ import annotations
 
@@ -49,6 +49,9 @@ class GradSync:
         self._attached = False
         self.early_elems = 0  # elements launched from inside backward in the current step
         self.last_early_elems = 0  # ... and in the last completed step (diagnostics)
+        self.bytes_reduced = 0     # bytes all-reduced since the last reset_stats()
+        self._exposed = []         # (start, end) device events around the post-backward wait (timing on)
+        self.timing = False
 
     # -------------------------------------------------------------------- overlap with backward
     def attach(self):
@@ -99,11 +102,30 @@ class GradSync:
             out.append((cur, self.arena.numel))
         return out
 
+    def reset_stats(self):
+        self.bytes_reduced = 0
+        self._exposed = []
+
+    def exposed_ms(self) -> float:
+        """Device time the compute stream spent between the end of backward and the completion of the
+        step's gradient all-reduce (the part NOT hidden under backward), summed since reset_stats();
+        synchronises the events."""
+        tot = 0.0
+        for a, b in self._exposed:
+            b.synchronize()
+            tot += a.elapsed_time(b)
+        return tot
+
     @torch.no_grad()
     def all_reduce(self):
         if self.world_size <= 1:
             return
         g = self.arena.grad
+        ev0 = None
+        if self.timing and g.is_cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        self.bytes_reduced += g.numel() * (2 if self.grad_dtype == "bf16" else 4)
         if self.grad_dtype == "bf16":
             if self._lowp is None:
                 self._lowp = torch.empty(g.numel(), dtype=torch.bfloat16, device=g.device)
@@ -120,5 +142,9 @@ class GradSync:
                 w.wait()
             self._works, self._sent = [], []
             self.last_early_elems, self.early_elems = self.early_elems, 0
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._exposed.append((ev0, ev1))
         if self.average:
             g.mul_(1.0 / self.world_size)

@@ -84,6 +84,10 @@ class GradientAverager:
         self.last_round_exact = False  # the last round was an uncompressed all-reduce that succeeded
         self.detached = False          # the communicator was aborted: this peer continues alone
         self.comm_failed = False       # set when a collective failed (timeout / dead peer)
+        self._backup_buf: Optional[torch.Tensor] = None  # one preallocated restore buffer (no clone per round)
+        self._overlap = None           # GradSync: the round's all-reduce launched from inside backward
+        self._armed = False
+        self.overlapped_rounds = 0
 
     def _world(self):
         return (1, 0) if self.detached else _group_world(self.group)
@@ -101,6 +105,87 @@ class GradientAverager:
             if p.grad is not None:
                 a.add_(p.grad)
 
+    def _backup_of(self, flat: torch.Tensor) -> torch.Tensor:
+        """Copy of ``flat`` in a buffer allocated once (a failed round restores from it)."""
+        if self._backup_buf is None or self._backup_buf.shape != flat.shape or self._backup_buf.device != flat.device:
+            self._backup_buf = torch.empty_like(flat)
+        self._backup_buf.copy_(flat)
+        return self._backup_buf
+
+    # -- backward-overlapped rounds ------------------------------------------------------------------
+    def overlap_eligible(self) -> bool:
+        return (self.arena is not None and self.reuse_grad_buffers and self.powersgd is None
+                and isinstance(self.compression, NoCompression) and not self.detached and self._world()[0] > 1)
+
+    @torch.no_grad()
+    def arm(self, next_closes_round: bool):
+        """Called between micro-steps: if the NEXT backward completes this epoch's accumulation, hand the
+        fused backward a GradSync hook so every gradient range that becomes final during that backward is
+        all-reduced right away, overlapped with the remaining layers (parallel/dp.py) -- the round itself
+        then only sends the tail (tied head, final LN) and rescales. Uncompressed rounds of homogeneous
+        peers only (equal samples per peer: the sum over peers / (t * world) is the weighted mean)."""
+        if not next_closes_round or not self.overlap_eligible():
+            self.disarm()
+            return
+        if self._armed:
+            return
+        from .dp import GradSync
+
+        if self._overlap is None or self._overlap.group is not self.group:
+            self._overlap = GradSync(self.arena, world_size=self._world()[0], group=self.group, average=False)
+        # the grads accumulated so far: a failed round falls back to them (the closing micro-batch is dropped)
+        self._backup_of(self.arena.grad)
+        self._overlap.attach()
+        self._armed = True
+
+    def disarm(self):
+        if self._overlap is not None:
+            self._overlap.detach()
+        self._armed = False
+
+    @torch.no_grad()
+    def abandon_overlap(self):
+        """A round that will not average (overflow skip, resync): complete the collectives the backward
+        already launched -- every peer launched the same ones -- and drop the hook; the caller resets
+        the accumulated gradients."""
+        if self._armed:
+            try:
+                self._overlap.all_reduce()
+            except Exception as e:  # noqa: BLE001
+                logger.warning(f"abandoned overlapped round failed ({e!r})")
+                self.comm_failed = True
+                self._overlap._works, self._overlap._sent = [], []
+        self.disarm()
+
+    @torch.no_grad()
+    def _step_overlapped(self, epoch: int, batch_size: int) -> bool:
+        """Finish a round whose all-reduce was launched from inside the last backward."""
+        sync, self._armed = self._overlap, False
+        sync.detach()
+        world, _ = self._world()
+        t = max(1, self.local_times_accumulated)
+        g = self.arena.grad
+        deadline = Deadline(self.averaging_timeout)
+        try:
+            faults.before_averaging(epoch)
+            sync.all_reduce()  # the tail + wait (the backward-launched buckets are already in flight)
+            wait_device(g.device, deadline, "gradient averaging")
+            g.mul_(1.0 / (t * world))
+            self.overlapped_rounds += 1
+            self.last_averaging_ok, self.last_round_exact = True, True
+            return True
+        except Exception as e:  # noqa: BLE001
+            logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients "
+                           f"(without the closing micro-batch, whose grads were already in the collective)")
+            self.comm_failed = True  # the group's collectives were in flight: it must be re-formed / left
+            sync._works, sync._sent = [], []
+            g.copy_(self._backup_buf)
+            self.local_times_accumulated = max(1, t - 1)
+            self.local_samples_accumulated = max(0, self.local_samples_accumulated - int(batch_size))
+            g.div_(self.local_times_accumulated)
+            self.last_averaging_ok, self.last_round_exact = False, False
+            return False
+
     def _grads(self) -> List[torch.Tensor]:
         if self.reuse_grad_buffers:
             for p in self.params:
@@ -111,9 +196,11 @@ class GradientAverager:
 
     # -- averaging --------------------------------------------------------------------------------
     @torch.no_grad()
-    def step(self, total_samples: Optional[int] = None, epoch: int = 0) -> bool:
+    def step(self, total_samples: Optional[int] = None, epoch: int = 0, batch_size: int = 0) -> bool:
         """Replace the accumulated grads with the collaboration-wide weighted mean (in the params'
         ``.grad``). Returns False if averaging failed and this peer's own mean gradient was used."""
+        if self._armed:
+            return self._step_overlapped(epoch, batch_size)
         t = max(1, self.local_times_accumulated)
         s = float(self.local_samples_accumulated)
         world, _ = self._world()
@@ -136,7 +223,7 @@ class GradientAverager:
                 logger.warning(f"gradient averaging failed ({e!r}); falling back to local gradients")
                 ok, injected = False, True
             if not injected:
-                backup = flat.clone()
+                backup = self._backup_of(flat)
                 deadline = Deadline(self.averaging_timeout)
                 try:
                     if self.powersgd is not None:
@@ -393,7 +480,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                  client_mode: bool = False, auxiliary: bool = False, verbose: bool = False, process_group=None,
                  arena: Optional[FlatArena] = None, powersgd_rank: Optional[int] = None, tracker_mode: str = "auto",
                  device=None, elastic=None, skip_exact_state_averaging: bool = True, offload_device=None,
-                 recovery: str = "auto", state_check_every: int = 16, **kwargs):
+                 recovery: str = "auto", state_check_every: int = 16, overlap_grad_averaging: bool = True, **kwargs):
         self.dht, self.run_id = dht, run_id
         self.target_batch_size = target_batch_size
         self.batch_size_per_step = batch_size_per_step
@@ -467,6 +554,10 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                                                     skip_if_exact=skip_exact_state_averaging and offload_device is None,
                                                     check_every=state_check_every)
         self.detached = False
+        self.overlap_grad_averaging = overlap_grad_averaging
+        self._last_bs = int(batch_size_per_step or 0)
+        if self._last_bs:
+            self._arm_next(self._last_bs)  # the very first micro-step may already close epoch 0
         self.last_round_samples = 0  # this peer's samples in the last averaging round
         self.last_epoch_time = None
         if offload_optimizer and device.type == "cuda" and verbose:
@@ -529,6 +620,23 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if bs is None:
             raise ValueError("batch_size_per_step (ctor) or batch_size (step) is required")
         self.grad_averager.accumulate_grads_(bs)
+        self._last_bs = int(bs)
+        try:
+            return self._step_collective(grad_scaler, loss)
+        finally:
+            self._arm_next(bs)
+
+    def _arm_next(self, bs: int):
+        """Static homogeneous tracker: the next micro-step closes the epoch exactly when (accumulated +
+        bs) * world >= target -- then its backward launches the round's all-reduce (GradientAverager.arm)."""
+        ga = self.grad_averager
+        if self.tracker.mode != "static" or self.detached or not self.overlap_grad_averaging:
+            ga.disarm()
+            return
+        world = _group_world(self.group)[0]
+        ga.arm((ga.local_samples_accumulated + int(bs)) * world >= self.target_batch_size)
+
+    def _step_collective(self, grad_scaler, loss):
         if self.elastic is None:
             try:
                 self._collective_part(grad_scaler)
@@ -575,6 +683,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if lagging:
             logger.info(f"epochs {tr.min_epoch_seen if tr.mode == 'collective' else self.local_epoch}..{tr.max_epoch_seen} "
                         f"diverged (local {self.local_epoch}); loading state from the newest peer")
+            self.grad_averager.abandon_overlap()
             self.load_state_from_peers()
             self.grad_averager.reset_accumulated_grads_()
             return
@@ -626,6 +735,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         if min_epoch < max_epoch - 1:
             # some peer fell behind (e.g. restored an old local backup): everyone joins the resync
             logger.info(f"{self.run_id}: epochs {min_epoch}..{max_epoch} diverged; resynchronising from the newest peer")
+            self.grad_averager.abandon_overlap()
             self.load_state_from_peers()
             self.grad_averager.reset_accumulated_grads_()
             self.tracker.update_epoch(self.local_epoch)
@@ -636,11 +746,12 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             flat = self.arena.grad if (self.arena is not None and self.grad_averager.reuse_grad_buffers) else None
             if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group):
                 logger.warning(f"{self.run_id}: non-finite scaled gradients at epoch {self.local_epoch}; skipping update")
+                self.grad_averager.abandon_overlap()
                 self.grad_averager.reset_accumulated_grads_()
                 self.local_epoch = max_epoch + 1
                 self.tracker.update_epoch(self.local_epoch)
                 return
-        ok = self.grad_averager.step(total_samples=total, epoch=self.local_epoch)
+        ok = self.grad_averager.step(total_samples=total, epoch=self.local_epoch, batch_size=self._last_bs)
         exact = ok and self.grad_averager.last_round_exact and min_epoch == max_epoch
         self.state_averager.step(optimizer_step=True, averaging_round=True, exact=exact)
         if self.local_epoch < max_epoch + 1:  # a peer one epoch behind catches up on the count

@@ -31,10 +31,17 @@ def test_bench_spawns_n_ranks(tmp_path, engine):
     res, p0, p1 = _run(tmp_path, "--engine", engine)
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 4
     assert len(res["per_rank_ms_per_step"]) == 2 and res["value"] > 0
+    assert len(res["per_rank_peak_mem_gb"]) == 2
+    if engine == "step":  # the gradient all-reduce priced inside the run (bytes, bus bandwidth, overlap)
+        ar = res["grad_allreduce"]
+        assert ar["bytes_per_step"] > 0 and ar["busbw_GBps"] > 0 and ar["standalone_ms"] > 0
+        assert 0.0 <= ar["overlapped_frac"] <= 1.0
     assert torch.equal(p0, p1)  # replicas stay bitwise identical
     if engine == "collab":
         assert res["config"]["engine"] == "CollaborativeOptimizer.step"
         assert res["collab_performance_ema_samples_per_s"] > 0
+        # static homogeneous peers, uncompressed: every round is the backward-armed GradSync path
+        assert res["collab_backward_overlapped_rounds"] >= 3
 
 
 def test_bench_rejects_world_mismatch(tmp_path):

@@ -41,7 +41,8 @@ SHAPES = [(256, 256, 128), (512, 768, 320), (2048, 1024, 192), (4096, 2048, 256)
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("group", [0, 2, -3])
-def test_gemm_pt(cuda, M, N, K, group):
+@pytest.mark.parametrize("variant", [10, 20])  # one tile per workgroup | persistent
+def test_gemm_pt(cuda, M, N, K, group, variant):
     from dalle_amd.ops.hip_ops import C
 
     torch.manual_seed(0)
@@ -49,18 +50,19 @@ def test_gemm_pt(cuda, M, N, K, group):
     B = torch.randn(N, K, device=cuda).bfloat16()
     bias = torch.randn(N, device=cuda).bfloat16()
     ref = A.float() @ B.float().t()
-    got = C().gemm_pt(A, B, bias, 0, group)
+    got = C().gemm_pt(A, B, bias, variant, group)
     assert _rel(got, ref + bias.float()) < 5e-3
-    got = C().gemm_pt(A, B, None, 0, group)
+    got = C().gemm_pt(A, B, None, variant, group)
     assert _rel(got, ref) < 5e-3
     # every element is written (catch a missed tile / sub-tile): compare elementwise with a loose bound
     assert ((got.float() - ref).abs() <= 0.02 * ref.abs() + 0.5).all()
     # deterministic
-    assert torch.equal(got, C().gemm_pt(A, B, None, 0, group))
+    assert torch.equal(got, C().gemm_pt(A, B, None, variant, group))
 
 
 @pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like"])
-def test_qkv_rope_pt(cuda, attn_type):
+@pytest.mark.parametrize("persist", [0, 1])
+def test_qkv_rope_pt(cuda, attn_type, persist):
     from dalle_amd.ops.hip_ops import C, _rope_tables, rope_cs_table
 
     torch.manual_seed(0)
@@ -71,7 +73,7 @@ def test_qkv_rope_pt(cuda, attn_type):
     w = (0.05 * torch.randn(3 * H * 64, D, device=cuda)).bfloat16()
     cos, sin = _rope_tables(geom, 64, cuda)
     col = attn_type == "axial_col"
-    q, k, v = C().qkv_rope_pt(h, w, rope_cs_table(geom, 64, cuda), T, S, H, n, col, 0.125)
+    q, k, v = C().qkv_rope_pt(h, w, rope_cs_table(geom, 64, cuda), T, S, H, n, col, 0.125, persist)
     qkv = (h.float() @ w.float().t()).view(B, n, -1)
     # storage-layout reference: the unfused rotary kernel on the bf16-rounded product (the fused kernel
     # rotates in fp32 and rounds once, so the two differ by at most about one bf16 ulp)
@@ -85,7 +87,8 @@ def test_qkv_rope_pt(cuda, attn_type):
 
 
 @pytest.mark.parametrize("M,F,K", [(512, 1024, 256), (2560, 4096, 1024)])
-def test_ff_dgrad_geglu_pt(cuda, M, F, K):
+@pytest.mark.parametrize("persist", [0, 1])
+def test_ff_dgrad_geglu_pt(cuda, M, F, K, persist):
     from dalle_amd.ops import hip_ops
 
     torch.manual_seed(5)
@@ -94,7 +97,7 @@ def test_ff_dgrad_geglu_pt(cuda, M, F, K):
     w2 = torch.randn(K, F, device=cuda) * 0.03
     h = torch.randn(M, 2 * F, device=cuda).to(torch.bfloat16)
     w2t = w2.t().contiguous().to(torch.bfloat16)
-    dh, db = C.ff_dgrad_geglu_pt(dy, w2t, h)
+    dh, db = C.ff_dgrad_geglu_pt(dy, w2t, h, None, persist)
     dh_old, db_old = C.ff_dgrad_geglu(dy, w2t, h)
     assert _rel(dh, dh_old) < 1e-2 and _rel(db, db_old) < 1e-2
     hf = h.float().requires_grad_(True)
@@ -104,12 +107,13 @@ def test_ff_dgrad_geglu_pt(cuda, M, F, K):
     assert _rel(db, hf.grad.sum(0)) < 2e-2
     # bias-grad accumulation into a sink
     sink = torch.ones(2 * F, device=cuda)
-    C.ff_dgrad_geglu_pt(dy, w2t, h, sink)
+    C.ff_dgrad_geglu_pt(dy, w2t, h, sink, persist)
     assert _rel(sink - 1, db) < 1e-5
 
 
 @pytest.mark.parametrize("M,F,K", [(512, 1024, 256), (2560, 4096, 1024)])
-def test_ff_in_geglu_pt(cuda, M, F, K):
+@pytest.mark.parametrize("persist", [0, 1])
+def test_ff_in_geglu_pt(cuda, M, F, K, persist):
     from dalle_amd.ops import hip_ops
 
     torch.manual_seed(7)
@@ -118,10 +122,12 @@ def test_ff_in_geglu_pt(cuda, M, F, K):
     w1 = torch.randn(2 * F, K, device=cuda) * 0.03
     b1 = torch.randn(2 * F, device=cuda) * 0.1
     perm = hip_ops.geglu_interleave_index(F, cuda)
-    a, u = C.ff_in_geglu_pt(x, w1[perm].to(torch.bfloat16).contiguous(), b1[perm].to(torch.bfloat16).contiguous())
+    a, u = C.ff_in_geglu_pt(x, w1[perm].to(torch.bfloat16).contiguous(), b1[perm].to(torch.bfloat16).contiguous(), persist)
     a_ref = x.float() @ w1.to(torch.bfloat16).float().t() + b1.to(torch.bfloat16).float()
     assert _rel(a, a_ref) < 5e-3
     u_ref = a.float()[:, :F] * torch.nn.functional.gelu(a.float()[:, F:])
     assert _rel(u, u_ref) < 5e-3
-    # same as the unfused path's GEGLU kernel on the same pre-activation, bitwise
-    assert torch.equal(u, C.geglu_fwd(a))
+    # the unfused path's GEGLU kernel (ocml erff) on the same pre-activation: the fused epilogue's erf
+    # approximation (|error| <= 1.5e-7) differs by at most one bf16 rounding step
+    u_old = C.geglu_fwd(a).float()
+    assert ((u.float() - u_old).abs() <= 2 ** -7 * u_old.abs() + 1e-6).all()
