@@ -47,13 +47,12 @@ def main():
     for N, K in shapes:
         A = torch.randn(M, K, device=dev).bfloat16()
         B = torch.randn(N, K, device=dev).bfloat16()
-        v = {"hipblaslt": lambda: torch.mm(A, B.t()), "8ph": lambda: C.gemm_nt(A, B, None, 300)}
+        v = {"hipblaslt": lambda: torch.mm(A, B.t()), "8ph": lambda: C.gemm_nt(A, B, None, 300),
+             "8ph_stagger": lambda: C.gemm_nt(A, B, None, 390)}
         for g in groups:
-            v[f"pt_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 20, g))
-            v[f"np_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 10, g))
-        v["pt_mainloop"] = lambda: C.gemm_pt(A, B, None, 25, 0)
-        v["np_mainloop"] = lambda: C.gemm_pt(A, B, None, 15, 0)
-        v["8ph_mainloop"] = lambda: C.gemm_nt(A, B, None, 350)
+            v[f"np_stagger_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 10, g))
+            v[f"np_g{g}"] = (lambda g=g: C.gemm_pt(A, B, None, 30, g))
+        v["np_mainloop"] = lambda: C.gemm_pt(A, B, None, 35, 0)
         t = run(v)
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": f"M{M}_N{N}_K{K}", "us": t, "TF": {k: round(fl / x / 1e6) for k, x in t.items()}}), flush=True)
@@ -88,7 +87,8 @@ def main():
     dy = (0.5 * torch.randn(B * n, D, device=dev)).bfloat16()
     w2t = (0.03 * torch.randn(F, D, device=dev)).bfloat16()
     a = torch.randn(B * n, 2 * F, device=dev).bfloat16()
-    t = run({"ff_dgrad_geglu_8ph": lambda: C.ff_dgrad_geglu(dy, w2t, a),
+    t = run({"ff_dgrad_geglu_8ph": lambda: C.ff_dgrad_geglu(dy, w2t, a, None, 0),
+             "ff_dgrad_geglu_8ph_stagger": lambda: C.ff_dgrad_geglu(dy, w2t, a, None, -1),
              "ff_dgrad_geglu_pt": lambda: C.ff_dgrad_geglu_pt(dy, w2t, a),
              "ff_dgrad_geglu_pt_persist": lambda: C.ff_dgrad_geglu_pt(dy, w2t, a, None, 1)})
     print(json.dumps({"op": "ff_dgrad_geglu", "us": t}), flush=True)

@@ -72,7 +72,7 @@ void decode_rope(const void*, const float*, const float*, void*, void*, void*, c
 void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
 void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 bool sample_step(const SampleArgs&, hipStream_t);
-bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t);
+bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
@@ -384,7 +384,7 @@ std::vector<Tensor> geglu_bwd_bias(Tensor h, Tensor dout, c10::optional<Tensor> 
 
 // FF-out dgrad GEMM with the GEGLU backward + FF-in bias grad in its epilogue (csrc/kernels/gemm.hip
 // EPI 2): dy (M, K) bf16, w2t = W2^T (F, K) bf16, h = FF-in pre-activation (M, 2F) -> (dh, dbias).
-std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
+std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb, int64_t stagger) {
   CHECK_IN(dy, torch::kBFloat16); CHECK_IN(w2t, torch::kBFloat16); CHECK_IN(h, torch::kBFloat16);
   TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2, "ff_dgrad_geglu: 2-D operands");
   const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
@@ -399,7 +399,7 @@ std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optiona
     pb = db.data_ptr<float>();
   }
   TORCH_CHECK(dalle::gemm_geglu_bwd(dy.data_ptr(), w2t.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr<float>(), M, F, K,
-                                    cur_stream()), "ff_dgrad_geglu: unsupported shape");
+                                    cur_stream(), (int)stagger), "ff_dgrad_geglu: unsupported shape");
   dalle::column_sum(part.data_ptr<float>(), M / 128, 2 * F, dalle::GradSink{pb, nullptr, nullptr, (int)(2 * F), db.defined() ? 0 : 1},
                     cur_stream());
   return {dh, db};
@@ -1150,7 +1150,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
   m.def("geglu_bwd_bias", &geglu_bwd_bias, py::arg("h"), py::arg("dout"), py::arg("gb") = py::none());
-  m.def("ff_dgrad_geglu", &ff_dgrad_geglu, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
+  m.def("ff_dgrad_geglu", &ff_dgrad_geglu, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none(),
+        py::arg("stagger") = -1);
   m.def("scale_residual_", &scale_residual_);
   m.def("scale_residual_out", &scale_residual_out);
   m.def("transpose_bf16", &transpose_bf16, "fp32 (R, C) -> bf16 (C, R) in one pass");

@@ -45,6 +45,16 @@ __device__ __forceinline__ s16x4 pack4(const float* f) {
   return v;
 }
 
+// Desynchronise the first wave of a one-tile-per-workgroup GEMM: workgroup b < first_wave waits
+// ((b >> 3) & 3) * ticks of the 100 MHz real-time counter before it starts, so the CUs' tile boundaries
+// (and the HBM bursts of their epilogues) fall at four different phases instead of all at once; every
+// later workgroup inherits its CU's offset. Bounded spin, no inter-workgroup dependence.
+__device__ __forceinline__ void stagger_start(int ticks, int first_wave) {
+  if (ticks <= 0 || (int)blockIdx.x >= first_wave) return;
+  const unsigned long long until = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(((blockIdx.x >> 3) & 3) * ticks);
+  while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -197,6 +197,7 @@ struct RopeEpi {
   // non-temporal epilogue output stores (DALLE_AMD_GEMM_NT_STORE=1): -5 % on the plain-store kernel at
   // the large shapes, no gain on the fused epilogues or the full step (profiles/r2_gemm_epilogue_cost.jsonl)
   int nt = 0;
+  int stagger = 0, first_wave = 0;  // start-time stagger of the first wave (common.h stagger_start)
 };
 
 // 16-byte epilogue store, non-temporal when the launch asks for it (wave-uniform branch)
@@ -567,6 +568,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
                                                                    __bf16* __restrict__ C, const __bf16* __restrict__ bias,
                                                                    int M, int N, int K, RopeEpi rope, int group) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];  // [buf][A-lo | B-lo | B-hi | A-hi]
+  stagger_start(rope.stagger, rope.first_wave);
   constexpr bool STAGGER = !(OPT & 1);
   if (MN) {
     A += (size_t)blockIdx.y * K * M;
@@ -754,6 +756,7 @@ void rope_pad_zero(void* q, void* k, void* v, int Tp, int T, int Np, int BH, hip
   hipLaunchKernelGGL(rope_pad_zero_kernel, dim3(BH), dim3(256), 0, st, (__bf16*)q, (__bf16*)k, (__bf16*)v, Tp, T, Np, BH);
 }
 
+int gemm_stagger_ticks(int ntiles, int K);
 bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int epi, hipStream_t st) {
   if (M % GBM || N % GBN || K % GBK) return false;
   const int nwg = (M / GBM) * (N / GBN);
@@ -782,6 +785,14 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
                            (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, group);
         return true;
       }
+      if (epi == 390) {  // measurement: the 8-phase kernel with the first-wave start stagger
+        RopeEpi e{};
+        e.stagger = gemm_stagger_ticks(nwg, K);
+        e.first_wave = 256;
+        hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
+                           (__bf16*)C, (const __bf16*)bias, M, N, K, e, 4);
+        return true;
+      }
       if (epi == 350 || epi == 360 || epi == 370) {  // measurement: no epilogue / staging only / nt stores
         if (epi == 370)
           hipLaunchKernelGGL((gemm_nt_8ph_kernel<7, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
@@ -806,11 +817,14 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
 // FF-out dgrad with the GEGLU backward in the epilogue: du = dy (M, K) . W2^T where w2t = W2^T (F, K)
 // bf16, then dh (M, 2F) = GEGLU'(h, du) and part ((M / 128), 2F) = partial FF-in bias grads. The
 // (M, F) du intermediate never exists.
+int gemm_stagger_ticks(int ntiles, int K);
 bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, float* part, int M, int F, int K,
-                    hipStream_t st) {
+                    hipStream_t st, int stagger) {
   if (M % GBM || F % GBN || K % GBK) return false;
   RopeEpi e{};
   e.nt = gemm_nt_store_default();
+  e.stagger = stagger < 0 ? gemm_stagger_ticks((M / GBM) * (F / GBN), K) : stagger;
+  e.first_wave = 256;
   e.gh = (const __bf16*)h;
   e.gdh = (__bf16*)dh;
   e.gpart = part;

@@ -127,6 +127,7 @@ struct PtArgs {
   __bf16* a;
   __bf16* u;
   int group;
+  int stagger, first_wave;  // per-tile mode: start-time stagger of the first wave (stagger_start)
 };
 
 __device__ __forceinline__ int pt_seq2st(const PtArgs& e, int p) {
@@ -353,6 +354,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   // [buf][A-lo | B-lo | B-hi | A-hi] half-tile images, 128 KiB in ONE array (a second __shared__
   // object can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];
+  if constexpr (!PERSIST) stagger_start(e.stagger, e.first_wave);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_m = M / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
@@ -543,10 +545,37 @@ static int pt_persist_default() {
   return v;
 }
 
+static int pt_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// quarter of one tile's main-loop time in 10 ns ticks (~1.3 PF/s chip-wide bf16), when the grid has more
+// tiles than CUs (DALLE_AMD_GEMM_STAGGER=0 disables, a number overrides the fraction in percent)
+int gemm_stagger_ticks(int ntiles, int K) {
+  static const int pct = [] {
+    const char* s = getenv("DALLE_AMD_GEMM_STAGGER");
+    return s ? atoi(s) : 25;
+  }();
+  const int cus = pt_cus();
+  if (pct <= 0 || ntiles <= cus) return 0;
+  const double tile_s = 2.0 * 256.0 * 256.0 * K / (1.3e15 / cus);
+  return (int)(tile_s * pct / 100.0 * 1e8);
+}
+
 template <int EPI>
 static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist = -1) {
   const int ntiles = (M / pt::BM) * (N / pt::BN);
   if (persist < 0) persist = pt_persist_default();
+  if (!persist && e.stagger < 0) e.stagger = gemm_stagger_ticks(ntiles, K);
+  if (e.stagger < 0) e.stagger = 0;
+  e.first_wave = pt_cus();
   if (persist)
     hipLaunchKernelGGL((gemm_pt_kernel<EPI, true>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
                        (const __bf16*)B, M, N, K, e);
@@ -570,12 +599,15 @@ bool gemm_pt(const void* A, const void* B, void* C, const void* bias, int M, int
              hipStream_t st) {
   if (!pt_shape_ok(M, N, K) || ldc < N || ldc % 8) return false;
   PtArgs e{};
+  e.stagger = -1;
   e.C = (__bf16*)C;
   e.bias = (const __bf16*)bias;
   e.ldc = ldc;
   e.group = group ? group : pt_group_default();
-  // epi: 0 plain, 5 main loop only; +10 = one tile per workgroup, +20 = persistent (default: env)
-  const int persist = epi >= 20 ? 1 : (epi >= 10 ? 0 : -1);
+  // epi: 0 plain, 5 main loop only; +10 = one tile per workgroup, +20 = persistent (default: env),
+  // +30 = one tile per workgroup without the start stagger
+  const int persist = (epi >= 20 && epi < 30) ? 1 : (epi >= 10 ? 0 : -1);
+  if (epi >= 30) e.stagger = 0;
   if (epi % 10 == 5) pt_launch<5>(A, B, M, N, K, e, st, persist);
   else pt_launch<0>(A, B, M, N, K, e, st, persist);
   return true;
@@ -589,6 +621,7 @@ bool gemm_pt_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, c
   int logS = 0;
   while ((1 << logS) < S) ++logS;
   PtArgs e{};
+  e.stagger = -1;
   e.q = (__bf16*)q;
   e.k = (__bf16*)k;
   e.v = (__bf16*)v;
@@ -613,6 +646,7 @@ bool gemm_pt_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh,
                        int persist) {
   if (!pt_shape_ok(M, F, K)) return false;
   PtArgs e{};
+  e.stagger = -1;
   e.h = (const __bf16*)h;
   e.dh = (__bf16*)dh;
   e.part = part;
@@ -629,6 +663,7 @@ bool gemm_pt_geglu_fwd(const void* x, const void* w1i, const void* b1i, void* a,
                        int persist) {
   if (!pt_shape_ok(M, 2 * F, K) || F % 32) return false;
   PtArgs e{};
+  e.stagger = -1;
   e.bias = (const __bf16*)b1i;
   e.a = (__bf16*)a;
   e.u = (__bf16*)u;

@@ -141,6 +141,16 @@ def rope_cs_table(geom: AttnGeometry, dim_head: int, device) -> torch.Tensor:
     return t
 
 
+def _cs_from_tables(cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """rope_cs_table's packing from the (cos, sin) tables themselves (cached per table)."""
+    key = ("tab", cos.data_ptr(), tuple(cos.shape), str(cos.device))
+    t = _cs_tables.get(key)
+    if t is None:
+        t = torch.stack([cos[:, 0::2], sin[:, 1::2]], dim=-1).contiguous()
+        _cs_tables[key] = t
+    return t
+
+
 _perm_cache: Dict[tuple, torch.Tensor] = {}
 
 
@@ -182,8 +192,10 @@ SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
 WGRAD_TRANSPOSED = int(os.environ.get("DALLE_AMD_WGRAD_T", "0"))
 # weight grads on the hand-written MN-major GEMM (gemm_wgrad_) instead of hipBLASLt (opt-in, see weight_grad)
 OWN_WGRAD = int(os.environ.get("DALLE_AMD_OWN_WGRAD", "0"))
-# QKV projection through the hand-written GEMM with the rotary in its epilogue (csrc/kernels/gemm.hip)
-FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "1"))
+# QKV projection through the hand-written GEMM with the rotary in its epilogue: 2 = the register-epilogue
+# kernel (csrc/kernels/gemm_pt.hip: 427 us vs 449 us for the LDS-staged 8-phase one, 1 = csrc/kernels/gemm.hip,
+# and 473 us for hipBLASLt + a rotary pass at the bench24 B48 shape; profiles/r3_gemm_pt_vs_hipblaslt_8ph.jsonl)
+FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "2"))
 # rotary backward fused into the attention-backward epilogues (csrc/kernels/attention.hip RopeOut)
 FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
 # GEGLU backward fused into the FF-out dgrad GEMM epilogue (csrc/kernels/gemm.hip EPI 2)
@@ -538,7 +550,10 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     col = pattern == PATTERN_IDS["axial_col"]
     if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
         # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
-        q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
+        if FUSED_QKV_ROPE == 2 and d >= 128:
+            q, k, v = C().qkv_rope_pt(h2, wq, _cs_from_tables(cos, sin), T, S, H, n, col, 0.125)
+        else:
+            q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
         _count("qkv_rope")
     else:
         qkv = torch.mm(h2, wq.t()).view(B, n, -1)
