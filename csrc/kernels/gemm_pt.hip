@@ -556,12 +556,14 @@ static int pt_cus() {
   return cus;
 }
 
-// quarter of one tile's main-loop time in 10 ns ticks (~1.3 PF/s chip-wide bf16), when the grid has more
-// tiles than CUs (DALLE_AMD_GEMM_STAGGER=0 disables, a number overrides the fraction in percent)
+// DALLE_AMD_GEMM_STAGGER=<percent>: stagger the first wave by that fraction of one tile's main-loop time
+// (10 ns ticks at ~1.3 PF/s chip-wide bf16), when the grid has more tiles than CUs. Off by default: it
+// measured SLOWER on every training shape (e.g. M61440 N1024 K8192 874 vs 766 us, N3072 K1024 374 vs 359;
+// profiles/r3_gemm_stagger.jsonl) -- the stores' cost is not the simultaneity of the epilogues.
 int gemm_stagger_ticks(int ntiles, int K) {
   static const int pct = [] {
     const char* s = getenv("DALLE_AMD_GEMM_STAGGER");
-    return s ? atoi(s) : 25;
+    return s ? atoi(s) : 0;
   }();
   const int cus = pt_cus();
   if (pct <= 0 || ntiles <= cus) return 0;

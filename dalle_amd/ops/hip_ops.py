@@ -101,6 +101,25 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
 
 
 NT_INPUT_GRAD = os.environ.get("DALLE_AMD_NT_DGRAD", "1") != "0"
+# plain (epilogue-free) projection GEMMs on the hand-written register-epilogue kernel
+# (csrc/kernels/gemm_pt.hip, one tile per workgroup + first-wave start stagger) instead of hipBLASLt
+OWN_GEMM = int(os.environ.get("DALLE_AMD_OWN_GEMM", "0"))
+
+
+def _own_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+            and a.is_contiguous() and b.is_contiguous() and a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0
+            and a.shape[1] % 64 == 0 and a.shape[1] >= 128)
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor, bias=None) -> torch.Tensor:
+    """a (M, K) . b (N, K)^T (+ bias): the hand-written GEMM when OWN_GEMM and the shape tiles, else hipBLASLt."""
+    if OWN_GEMM and _own_gemm_ok(a, b):
+        _count("own_gemm")
+        return C().gemm_pt(a, b, bias, 10, 0)
+    if bias is not None:
+        return torch.addmm(bias, a, b.t())
+    return torch.mm(a, b.t())
 
 
 def input_grad(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -109,7 +128,7 @@ def input_grad(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     at every training input-gradient shape (M = 61440: 1041 vs 895, 1230 vs 1100, 1432 vs 1192 TF/s;
     ``benchmarks/bench_gemm_layouts.py``, profiles/r2_gemm_layouts.jsonl). DALLE_AMD_NT_DGRAD=0: NN form."""
     if NT_INPUT_GRAD:
-        return torch.mm(g, bf16_weight_t(w).t())
+        return mm_nt(g, bf16_weight_t(w))
     return torch.mm(g, bf16_weight(w))
 
 
@@ -149,6 +168,19 @@ def _cs_from_tables(cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         t = torch.stack([cos[:, 0::2], sin[:, 1::2]], dim=-1).contiguous()
         _cs_tables[key] = t
     return t
+
+
+# FF-in GEMM with the GEGLU forward in its epilogue (csrc/kernels/gemm_pt.hip EPI 3)
+FUSED_FF_IN = int(os.environ.get("DALLE_AMD_FUSED_FF_IN", "0"))
+
+
+def geglu_interleaved(t: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of W1 (2F, K) / b1 (2F,) with rows in the fused FF-in kernel's order (cached per forward)."""
+    def make():
+        F = t.shape[0] // 2
+        return t.detach().index_select(0, geglu_interleave_index(F, t.device)).to(torch.bfloat16).contiguous()
+
+    return _cached(("geglu_i", id(t)), t, make)
 
 
 _perm_cache: Dict[tuple, torch.Tensor] = {}
@@ -561,7 +593,7 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
         del qkv
     out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
     wo = bf16_weight(w_out)
-    y = torch.addmm(bf16_weight(b_out), out.view(-1, out.shape[-1]), wo.t())
+    y = mm_nt(out.view(-1, out.shape[-1]), wo, bf16_weight(b_out))
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None
@@ -595,11 +627,16 @@ def _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save: bool = T
     d = inp.shape[-1]
     h2 = h.view(-1, d)
     w1b, w2b = bf16_weight(w1), bf16_weight(w2)
-    a = torch.addmm(bf16_weight(b1), h2, w1b.t())
-    u = C().geglu_fwd(a)
+    if FUSED_FF_IN and _own_gemm_ok(h2, w1b) and w1b.shape[0] % 64 == 0:
+        # FF-in GEMM + bias + GEGLU in one kernel (W1 / b1 rows interleaved per 64-column group)
+        a, u = C().ff_in_geglu_pt(h2, geglu_interleaved(w1), geglu_interleaved(b1))
+        _count("ff_in_geglu")
+    else:
+        a = torch.addmm(bf16_weight(b1), h2, w1b.t())
+        u = C().geglu_fwd(a)
     if not save:
         del a
-    y = torch.addmm(bf16_weight(b2), u, w2b.t())
+    y = mm_nt(u, w2b, bf16_weight(b2))
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None

@@ -263,8 +263,8 @@ def test_fused_lamb_restore_before_first_step(cuda):
     assert torch.equal(arena2.data, ref)
 
 
-@pytest.mark.parametrize("reversible", [False, True])
-def test_reference_geometry_end_to_end(cuda, reversible):
+@pytest.mark.parametrize("reversible,own", [(False, False), (True, False), (False, True)])
+def test_reference_geometry_end_to_end(cuda, reversible, own, monkeypatch):
     """The bench / reference geometry (d=1024, 16 heads, 256 text + 32x32 image tokens, the attention /
     sharing cycle of the recipe) with the flat arena attached, B=2 (M = 2560 = 10 x 256), so every fused
     path runs: QKV GEMM + rotary epilogue, FF dgrad + GEGLU-backward epilogue, the fused sequential /
@@ -273,6 +273,9 @@ def test_reference_geometry_end_to_end(cuda, reversible):
     from dalle_amd.data.synthetic import synthetic_batch
     from dalle_amd.ops import hip_ops
 
+    if own:  # every projection GEMM on the hand-written kernels, FF-in with the GEGLU epilogue
+        monkeypatch.setattr(hip_ops, "OWN_GEMM", 1)
+        monkeypatch.setattr(hip_ops, "FUSED_FF_IN", 1)
     torch.manual_seed(0)
     cfg = DALLEConfig(depth=4, attn_types=reference_attn_types(4), shared_attn_ids=reference_shared_ids(4),
                       shared_ff_ids=reference_shared_ids(4), reversible=reversible)
@@ -287,7 +290,7 @@ def test_reference_geometry_end_to_end(cuda, reversible):
     loss.backward()
     torch.cuda.synchronize()
     stack = "reversible_stack" if reversible else "sequential_stack"
-    for path in ("qkv_rope", "ff_dgrad_geglu", stack):
+    for path in ("qkv_rope", "ff_dgrad_geglu", stack) + (("own_gemm", "ff_in_geglu") if own else ()):
         assert hip_ops.PATH_COUNTS.get(path, 0) > 0, (path, hip_ops.PATH_COUNTS)
     torch.set_num_threads(16)
     loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
