@@ -532,10 +532,19 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 self.elastic = elastic
                 self.adopted = True
                 tracker_store = dist.PrefixStore("progress", rstore)
+        if elastic is not None and not self.adopted:
+            # a peer that JOINS through the coordinator takes the tracker of the group it joins (an
+            # adopted torchrun world publishes its mode; pure elastic generations default to lockstep)
+            key = "elastic/tracker_mode"
+            if tracker_mode == "auto":
+                tracker_mode = elastic.store.get(key).decode() if elastic.store.check([key]) else "collective"
+            if tracker_mode == "store":
+                tracker_store = dist.PrefixStore("progress", elastic.store)
         if tracker_mode == "auto":
-            # asynchronous store records on a static (or adopted) group; pure elastic generations keep
-            # the lockstep tracker
-            tracker_mode = "collective" if (elastic is not None and not self.adopted) else "store"
+            # asynchronous store records on a static (or adopted) group
+            tracker_mode = "store"
+        if self.adopted:
+            elastic.store.set("elastic/tracker_mode", tracker_mode)
         self.tracker = ProgressTracker(dht=dht, prefix=run_id, target_batch_size=target_batch_size, group=process_group,
                                        device=device, client_mode=client_mode, peer_id=peer_id, mode=tracker_mode,
                                        store=tracker_store)

@@ -260,7 +260,7 @@ def test_heterogeneous_peers_contribute_at_their_own_pace():
 
 
 # ------------------------------------------------------------------------------------------------
-def _dead_peer_worker(rank, world, port, q, recovery, coord_port):
+def _dead_peer_worker(rank, world, port, q, recovery, coord_port, epochs=4):
     try:
         if rank == 2:
             os.environ["DALLE_AMD_FAULT_KILL_IN_AVERAGING"] = "1"
@@ -277,7 +277,7 @@ def _dead_peer_worker(rank, world, port, q, recovery, coord_port):
                                      averaging_timeout=20.0, allreduce_timeout=10.0, matchmaking_time=1.0,
                                      tracker_mode="static", recovery=recovery)
         epochs_grads = []
-        while opt.local_epoch < 4:
+        while opt.local_epoch < epochs:
             g = torch.full_like(p, float(rank + 1) * (opt.local_epoch + 1))
             p.grad.add_(g)
             before = p.detach().clone()
@@ -293,7 +293,41 @@ def _dead_peer_worker(rank, world, port, q, recovery, coord_port):
         q.put(pickle.dumps(("error", rank, traceback.format_exc())))
 
 
-def _run_with_dead_peer(recovery, coordinator):
+def _joiner_worker(coord_port, q):
+    """A replacement peer: joins the survivors' group through the coordinator, gets the state from a donor
+    and trains on with them."""
+    try:
+        os.environ["DALLE_AMD_COORDINATOR"] = f"127.0.0.1:{coord_port}"
+        torch.set_num_threads(1)
+        import datetime
+
+        from dalle_amd.parallel.elastic import ElasticGroup, recovery_store
+        from dalle_amd.parallel.optimizer import CollaborativeOptimizer
+
+        store = recovery_store("dead")
+        store.wait(["elastic/g0/frozen"], datetime.timedelta(seconds=120))  # the survivors regrouped once
+        eg = ElasticGroup(store, peer_id="joiner", backend="gloo", matchmaking_time=1.0, allreduce_timeout=10.0)
+        eg.join()
+        p = torch.nn.Parameter(torch.full((300, 300), 123.0))  # garbage until the donor's state arrives
+        p.grad = torch.zeros_like(p)
+        opt = CollaborativeOptimizer(run_id="dead", params=[p], optimizer=lambda ps: torch.optim.SGD(ps, lr=1.0),
+                                     target_batch_size=3, batch_size_per_step=1, reuse_grad_buffers=True,
+                                     averaging_timeout=20.0, allreduce_timeout=10.0, matchmaking_time=1.0, elastic=eg)
+        assert opt.tracker.mode == "static", opt.tracker.mode  # the adopted group's published mode
+        opt.load_state_from_peers()  # pairs with the members' regroup-time resync
+        joined_at = opt.local_epoch
+        while opt.local_epoch < 6:
+            p.grad.add_(3.0 * (opt.local_epoch + 1))
+            opt.step()
+        q.put(pickle.dumps(("joiner", joined_at, p.detach().clone(), eg.world_size)))
+        eg.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put(pickle.dumps(("error", "joiner", traceback.format_exc())))
+
+
+def _run_with_dead_peer(recovery, coordinator, epochs=4, joiner=False):
     port = _free_port()
     server = None
     coord_port = 0
@@ -302,10 +336,12 @@ def _run_with_dead_peer(recovery, coordinator):
         server = dist.TCPStore("127.0.0.1", coord_port, world_size=None, is_master=True, wait_for_workers=False)
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 3, port, q, recovery, coord_port)) for r in range(3)]
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 3, port, q, recovery, coord_port, epochs)) for r in range(3)]
+    if joiner:
+        procs.append(ctx.Process(target=_joiner_worker, args=(coord_port, q)))
     for p in procs:
         p.start()
-    res = sorted([pickle.loads(q.get()) for _ in range(2)], key=lambda r: r[0])
+    res = sorted([pickle.loads(q.get()) for _ in range(2 + int(joiner))], key=lambda r: str(r[0]))
     for p in procs:
         p.join(60)
         if p.is_alive():
@@ -333,6 +369,20 @@ def test_dead_peer_survivors_regroup_and_keep_averaging():
         assert abs(upd[2] - 1.5 * 3) < 1e-5, upd        # 2 peers: (1 + 2) / 2 * (e + 1)
         assert abs(upd[3] - 1.5 * 4) < 1e-5, upd
     assert u0[1] == u1[1]
+
+
+def test_replacement_peer_joins_survivors_and_gets_state_from_donor():
+    """After the survivors re-formed their group, a replacement peer joins through the same coordinator: the
+    members admit it at their next round boundary, it receives parameters / epoch from a donor, and from
+    then on the three train in lockstep (bitwise identical parameters)."""
+    res = _run_with_dead_peer("auto", coordinator=True, epochs=6, joiner=True)
+    for r in res:
+        assert r[0] != "error", r[2]
+    (r0, d0, s0, p0, n0, w0), (r1, d1, s1, p1, n1, w1), (_, joined_at, pj, wj) = res
+    assert not d0 and not d1 and w0 == w1 == wj == 3
+    assert n0 == n1 == 2  # death, then the join
+    assert 2 <= joined_at < 6
+    assert torch.equal(p0, p1) and torch.equal(p0, pj)
 
 
 def test_dead_peer_without_recovery_store_detaches():
