@@ -509,6 +509,11 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         want_master = factory and flat_params and (delay_optimizer_step or offload_device is not None)
         self._master = MasterParams(flat_params, arena, device=offload_device) if want_master else None
         inner = optimizer(self._master.substitute(param_groups) if self._master else param_groups) if factory else optimizer
+        if offload_device is not None and self._master is None and flat_params:
+            # an already-built optimizer (no factory to rebuild it over MasterParams): step it on pinned
+            # host copies through the generic wrapper
+            from ..optim.wrapper import HostOffloadOptimizer
+            inner = HostOffloadOptimizer(inner)
         if arena is not None and getattr(inner, "arena", "missing") is None:
             inner.arena = self._master.arena if self._master is not None else arena
         sched = scheduler(inner) if callable(scheduler) else scheduler

@@ -73,3 +73,20 @@ def test_host_offload_matches_hbm_optimizer(cuda, delay):
     rel = ((ar_ref.data - ar_off.data).norm() / ar_ref.data.norm()).item()
     assert rel < 1e-4, rel
     assert off.local_epoch == 4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_generic_host_offload_optimizer_on_hbm_params(cuda, dtype):
+    """HostOffloadOptimizer: any torch optimizer (Adam here) on pinned host copies of HBM parameters ==
+    the same optimizer stepping on the device (fp32: to rounding; bf16 params: fp32 host master per step)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_optim_cpu import _offload_vs_plain
+
+    a, b, off = _offload_vs_plain(cuda, dtype)
+    torch.cuda.synchronize()
+    assert off._host.is_pinned() and all(v["exp_avg"].device.type == "cpu" for v in off.inner.state.values())
+    for x, y in zip(a, b):
+        assert y.device.type == "cuda" and y.dtype == dtype
+        tol = dict(rtol=1e-5, atol=1e-6) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(x.float(), y.float(), **tol)

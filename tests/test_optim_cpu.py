@@ -240,6 +240,56 @@ def test_delegating_optimizer():
     assert "Counting(" in repr(opt)
 
 
+def _offload_vs_plain(dev, dtype=torch.float32, steps=4):
+    from dalle_amd.optim.wrapper import HostOffloadOptimizer
+
+    torch.manual_seed(0)
+    init = [torch.randn(7, 5), torch.randn(11), torch.randn(3, 2, 2)]
+    grads = [[torch.randn_like(t) for t in init] for _ in range(steps)]
+    a = [torch.nn.Parameter(t.clone().to(dev, dtype)) for t in init]
+    b = [torch.nn.Parameter(t.clone().to(dev, dtype)) for t in init]
+    plain = torch.optim.Adam([{"params": a[:2]}, {"params": a[2:], "lr": 3e-3}], lr=1e-2, weight_decay=0.1)
+    off = HostOffloadOptimizer(torch.optim.Adam([{"params": b[:2]}, {"params": b[2:], "lr": 3e-3}], lr=1e-2,
+                                                weight_decay=0.1))
+    for gs in grads:
+        for ps, opt in ((a, plain), (b, off)):
+            for p, g in zip(ps, gs):
+                p.grad = g.to(dev, dtype)
+            opt.step()
+            opt.zero_grad()
+    return a, b, off
+
+
+def test_host_offload_optimizer_matches_plain_step():
+    a, b, off = _offload_vs_plain("cpu")
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-6, atol=1e-7)
+    # the state lives with the host copies, keyed by the inner optimizer's parameter order
+    st = off.state_dict()
+    assert len(st["state"]) == 3 and st["state"][0]["exp_avg"].shape == (7, 5)
+    assert all(v["exp_avg"].device.type == "cpu" for v in off.inner.state.values())
+    off.load_state_dict(st)
+    assert off.param_groups[1]["lr"] == 3e-3 and off.param_groups[0]["params"][0] is b[0]
+    with pytest.raises(ValueError):
+        off.step(closure=lambda: 0.0)
+
+
+def test_collaborative_optimizer_offloads_a_prebuilt_optimizer():
+    """A built optimizer (no factory) + offload_device: the collaborative optimizer steps it through
+    HostOffloadOptimizer (world 1: no process group needed)."""
+    from dalle_amd.optim.wrapper import HostOffloadOptimizer
+    from dalle_amd.parallel.optimizer import CollaborativeOptimizer
+
+    p = torch.nn.Parameter(torch.ones(4))
+    opt = CollaborativeOptimizer(run_id="off", params=[p], optimizer=torch.optim.SGD([p], lr=0.5),
+                                 target_batch_size=1, batch_size_per_step=1, offload_device="cpu",
+                                 tracker_mode="static")
+    assert isinstance(opt.state_averager.optimizer, HostOffloadOptimizer)
+    p.grad = torch.ones(4)
+    opt.step()
+    assert torch.allclose(p.detach(), torch.full((4,), 0.5)) and opt.local_epoch == 1
+
+
 class _FakeDevice:
     """A device timeline that runs each step in `dev_ms` while the host enqueues every `host_ms`."""
 
