@@ -12,6 +12,12 @@ reference consumes is kept (``task.py:104-119``, ``callback.py:80-86``, ``run_au
 The first peer (no ``initial_peers``) hosts the store inside its own process (a native server
 thread); everybody else connects to a multiaddr such as ``/ip4/127.0.0.1/tcp/31337``. Values are
 msgpack-serialised; record validators run on every store (schema + owner-signed subkeys).
+
+Losing the hosting peer is not fatal to a client: the store only carries metrics and auxiliary-peer
+snapshots (training progress and recovery use the torchrun agent's c10d store), so once the native
+client's own reconnect attempt fails, ``store`` returns False, ``get`` None, ``keys`` [] and
+``wait_for`` 0, ``degraded`` is set, and every ``reconnect_period`` seconds the next call tries the
+address again (a restarted host peer re-binds the same port).
 """
 from __future__ import annotations
 
@@ -79,6 +85,9 @@ class DHT:
         self._initial_peers = list(initial_peers)
         self._connect_timeout = connect_timeout
         self.owner = bytes(self.peer_id, "utf8")
+        self.degraded = False        # the hosting peer is unreachable (client side only)
+        self.reconnect_period = 10.0
+        self._next_reconnect = 0.0
         for v in self.record_validators:
             if hasattr(v, "local_public_key"):
                 self.owner = v.local_public_key
@@ -142,6 +151,29 @@ class DHT:
                 return False
         return True
 
+    def _call(self, op: str, *args, default=None):
+        """One native client call; a lost hosting peer degrades a CLIENT to no-op answers (module doc)."""
+        if self.degraded and self._server is None:
+            now = time.monotonic()
+            if now < self._next_reconnect:
+                return default
+            self._next_reconnect = now + self.reconnect_period
+        try:
+            out = getattr(self._client, op)(*args)
+        except RuntimeError as e:
+            if self._server is not None:  # our own in-process server: a real error
+                raise
+            if not self.degraded:
+                logger.warning(f"DHT host {self._addr[0]}:{self._addr[1]} unreachable ({e}); metrics / snapshot "
+                               f"records are dropped until it is back (retry every {self.reconnect_period:.0f}s)")
+            self.degraded = True
+            self._next_reconnect = time.monotonic() + self.reconnect_period
+            return default
+        if self.degraded:
+            logger.info("DHT host reachable again")
+            self.degraded = False
+        return out
+
     def _store(self, key, subkey, value, expiration_time) -> bool:
         if not self._validate(key, subkey, value):
             logger.warning(f"record for key {key!r} rejected by validators")
@@ -152,7 +184,7 @@ class DHT:
             if hasattr(v, "sign_value"):
                 payload = v.sign_value(str(key), subkey, payload, float(expiration_time))
         owner = self.owner if subkey is not None else b""
-        return bool(self._client.store(str(key), sub, payload, float(expiration_time), owner))
+        return bool(self._call("store", str(key), sub, payload, float(expiration_time), owner, default=False))
 
     def _decode(self, key: str, sub, payload: bytes, exp: float):
         """Signature check + strip of one stored record; None when a validator rejects it."""
@@ -172,7 +204,7 @@ class DHT:
     def get(self, key: str, latest: bool = True, return_future: bool = False, **kw) -> Optional[ValueWithExpiration]:
         if return_future:
             return self._pool.submit(self.get, key, latest)
-        items = self._client.get(str(key))
+        items = self._call("get", str(key), default=None)
         if not items:
             return None
         key = str(key)
@@ -191,14 +223,14 @@ class DHT:
         return ValueWithExpiration(out, best) if out else None
 
     def delete(self, key: str):
-        self._client.delete(str(key))
+        self._call("delete", str(key))
 
     def keys(self, prefix: str = "") -> List[str]:
-        return list(self._client.keys(prefix))
+        return list(self._call("keys", prefix, default=[]))
 
     def wait_for(self, key: str, count: int, timeout: float) -> int:
         """Block until ``key`` has ``count`` live subkeys (server-side wait); returns the live count."""
-        return int(self._client.wait(str(key), int(count), float(timeout)))
+        return int(self._call("wait", str(key), int(count), float(timeout), default=0))
 
     def shutdown(self):
         self._pool.shutdown(wait=False)
