@@ -1,6 +1,7 @@
 """Multi-GPU data parallelism over RCCL (SURVEY §4 tier 6): ``torchrun --nproc-per-node N bench.py --gpus N``
 -- the driver's scaling launch -- with the gradient all-reduce handed off during backward and without.
-Runs only where at least two GPUs are visible (skipped on a one-GPU box; the same path is rehearsed there
+Runs only where at least two GPUs are visible: RCCL refuses two ranks on one device ("Duplicate GPU detected",
+profiles/r3_rccl_shared_gpu_probe.txt), so it is skipped on a one-GPU box; the same path is rehearsed there
 with gloo, tests/test_bench_cpu.py and scripts/gpu_handoff.sh)."""
 import json
 import os
