@@ -959,27 +959,35 @@ class _SequentialFused(torch.autograd.Function):
             else:
                 out = torch.empty_like(inp)
                 C().scale_residual_out(inp, y, s, out)
-        ctx.subs, ctx.saved_all, ctx.nparams = subs, saved_all, len(params)
+        ctx.subs, ctx.saved_all, ctx.params = subs, saved_all, params
         return out
 
     @staticmethod
     def backward(ctx, gout):
         subs, saved_all = ctx.subs, ctx.saved_all
         ctx.saved_all = None
+        # The forward chose this node because every parameter had an fp32 grad buffer. If they were reset
+        # since (``loss = model(x); opt.zero_grad(); loss.backward()``), give them fresh zero fp32 .grad
+        # buffers: every kernel and weight-grad GEMM below accumulates into .grad, exactly as into the arena
+        reset = False
+        for p in ctx.params:
+            if p.requires_grad and grad_sink(p) is None:
+                p.grad = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+                reset = True
         sinks = [[grad_sink(p) for p in prm] for _, _, prm in subs]
         g = gout.float().contiguous()
         overlap = _wgrad.begin(g.device)
         try:
-            g = _SequentialFused._backward(subs, saved_all, sinks, g)
+            g = _SequentialFused._backward(subs, saved_all, sinks, g, handoff=not reset)
         finally:
             if overlap:
                 _wgrad.end()
-        return (g, None, *([None] * ctx.nparams))
+        return (g, None, *([None] * len(ctx.params)))
 
     @staticmethod
-    def _backward(subs, saved_all, sinks, g):
+    def _backward(subs, saved_all, sinks, g, handoff: bool = True):
         # weight grads on the side stream (_wgrad) are not ordered before the hand-off: no early hand-off then
-        hook = _grad_ready_hook if _wgrad.stream is None else None
+        hook = _grad_ready_hook if (_wgrad.stream is None and handoff) else None
         final = _final_at([prm for _, _, prm in subs]) if hook is not None else None
         with torch.no_grad():
             kind, args, prm = subs[-1]
