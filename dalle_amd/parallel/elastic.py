@@ -50,7 +50,9 @@ def recovery_store(run_id: str, timeout: float = 300.0) -> Optional[dist.Store]:
     * a torchrun worker (``TORCHELASTIC_USE_AGENT_STORE=True``): the elastic AGENT hosts the job's
       TCPStore at ``MASTER_ADDR:MASTER_PORT`` -- not the rank-0 worker -- so it survives any worker.
 
-    Keys live under ``dalle_recovery/{run_id}``."""
+    Keys live under ``dalle_recovery/{run_id}``, and under a per-attempt suffix when torchrun restarts the
+    workers (``--max-restarts``: TORCHELASTIC_RESTART_COUNT > 0): the agent's store keeps the previous
+    attempt's generations, which must not leak into the fresh world (it resumes from its checkpoint)."""
     spec = os.environ.get("DALLE_AMD_COORDINATOR")
     try:
         if spec:
@@ -64,7 +66,8 @@ def recovery_store(run_id: str, timeout: float = 300.0) -> Optional[dist.Store]:
     except Exception as e:  # noqa: BLE001 - no recovery store: the caller falls back to detaching
         logger.warning(f"[elastic] recovery store unavailable ({e!r})")
         return None
-    return dist.PrefixStore(f"dalle_recovery/{run_id}", base)
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") if not spec else "0"
+    return dist.PrefixStore(f"dalle_recovery/{run_id}" + (f"/attempt{attempt}" if attempt not in ("", "0") else ""), base)
 
 
 class ElasticGroup:

@@ -111,3 +111,30 @@ def test_straggler_past_timeout_is_dropped_then_readmitted():
     assert all(r[3] >= 1 for r in res)  # everybody regrouped at least once
     ps = [r[5] for r in res]
     assert torch.allclose(ps[0], ps[1]) and torch.allclose(ps[0], ps[2])
+
+
+def test_recovery_store_is_namespaced_per_torchrun_attempt(monkeypatch):
+    """torchrun --max-restarts restarts every worker against the SAME agent store: each attempt's
+    generations live under their own prefix, so a restarted world never sees the previous one's keys."""
+    import datetime
+    import socket
+
+    import torch.distributed as dist
+
+    from dalle_amd.parallel.elastic import recovery_store
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    agent = dist.TCPStore("127.0.0.1", port, world_size=None, is_master=True, timeout=datetime.timedelta(seconds=10),
+                          wait_for_workers=False)
+    monkeypatch.delenv("DALLE_AMD_COORDINATOR", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_USE_AGENT_STORE", "True")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    for attempt in ("0", "2"):
+        monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", attempt)
+        recovery_store("job", timeout=10).set("elastic/gen", attempt)
+    assert agent.get("dalle_recovery/job/elastic/gen") == b"0"
+    assert agent.get("dalle_recovery/job/attempt2/elastic/gen") == b"2"
