@@ -14,6 +14,10 @@ optimizer and the trainer (all no-ops when unset):
                                               round opened (the survivors are already in the collective)
 * ``DALLE_AMD_DEBUG_SYNC=1``                 -- synchronise the device after every fused op (debug mode;
                                               pairs with ``AMD_SERIALIZE_KERNEL=3`` / ``HIP_LAUNCH_BLOCKING=1``)
+
+Under torchrun every worker inherits the same environment; ``DALLE_AMD_FAULT_RANK=<r>`` limits the faults to
+that ``RANK`` and ``DALLE_AMD_FAULT_ATTEMPT=<a>`` to that ``TORCHELASTIC_RESTART_COUNT`` (e.g. kill rank 1
+in the first attempt only, then let ``--max-restarts`` bring the world back).
 """
 from __future__ import annotations
 
@@ -23,9 +27,18 @@ import time
 import torch
 
 
+def _targeted() -> bool:
+    r, a = os.environ.get("DALLE_AMD_FAULT_RANK"), os.environ.get("DALLE_AMD_FAULT_ATTEMPT")
+    if r not in (None, "") and os.environ.get("RANK", "0") != r:
+        return False
+    if a not in (None, "") and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != a:
+        return False
+    return True
+
+
 def _int(name):
     v = os.environ.get(name)
-    return int(v) if v not in (None, "") else None
+    return int(v) if v not in (None, "") and _targeted() else None
 
 
 def debug_sync():

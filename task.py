@@ -129,7 +129,18 @@ class TrainingTask:
             backend = self.trainer_args.backend or ("nccl" if torch.cuda.is_available() else "gloo")
             if backend == "nccl":
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
-            dist.init_process_group(backend, timeout=timedelta(seconds=self.collab_args.averaging_timeout))
+            timeout = timedelta(seconds=self.collab_args.averaging_timeout)
+            attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+            if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True" and attempt not in ("", "0"):
+                # torchrun --max-restarts with a static rendezvous: the agent's store still holds the previous
+                # attempt's process-group keys (a dead rank's address), so a restarted rank could read a stale
+                # one before its peer overwrites it -- rendezvous under a per-attempt prefix instead
+                base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                                     timeout=timeout)
+                dist.init_process_group(backend, store=dist.PrefixStore(f"dalle_pg/attempt{attempt}", base),
+                                        rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]), timeout=timeout)
+            else:
+                dist.init_process_group(backend, timeout=timeout)
         return dist.group.WORLD if dist.is_initialized() else None
 
     @property

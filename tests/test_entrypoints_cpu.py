@@ -92,3 +92,29 @@ def test_nan_rollback_and_averaging_fallback(tmp_path):
     assert "falling back to local gradients" in r.stdout
     assert "Parameters became NaN/Inf: rolling back to the last backup" in r.stdout
     assert "Restored the backup of epoch" in r.stdout
+
+
+@pytest.mark.slow
+def test_torchrun_restart_resumes_from_backups_and_donor(tmp_path):
+    """torchrun --max-restarts 1: rank 1 dies at epoch 3 of the first attempt; the agent restarts the whole
+    world, every peer restores its own backup, then synchronises with the donor (load_state_from_peers), and
+    the two peers go on averaging together past the failure."""
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", DALLE_AMD_LOGLEVEL="INFO",
+               DALLE_AMD_FAULT_KILL_AT_EPOCH="3", DALLE_AMD_FAULT_RANK="1", DALLE_AMD_FAULT_ATTEMPT="0")
+    out = tmp_path / "out"
+    run = subprocess.run(
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--max-restarts", "1",
+         "--monitor-interval", "0.5", "--master-addr", "127.0.0.1", "--master-port", str(port),
+         os.path.join(ROOT, "run_trainer.py"), *COMMON, "--per_device_train_batch_size", "2", "--target_batch_size", "8",
+         "--max_steps", "24", "--warmup_steps", "2", "--total_steps", "100", "--output_dir", str(out),
+         "--backup_every_steps", "1", "--state_path", str(tmp_path / "state.zip"), "--averaging_timeout", "60"],
+        cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    tout = run.stdout
+    assert run.returncode == 0, tout[-4000:]
+    assert tout.count("Restored the backup of epoch") >= 2, tout[-4000:]  # both restarted peers
+    import re
+    after = [int(m) for m in re.findall(r"cfg1: epoch (\d+) \(averaged \d+ samples across 2 peers", tout)]
+    assert sum(e >= 6 for e in after) >= 4, tout[-3000:]  # both peers, several rounds past the restart
+    for r in (0, 1):
+        assert torch.load(tmp_path / f"state.rank{r}.zip", weights_only=True)["local_epoch"] >= 6
