@@ -51,9 +51,11 @@ def test_bench_rejects_world_mismatch(tmp_path):
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
 
 
-def test_bench_under_torchrun(tmp_path):
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_under_torchrun(tmp_path, n):
     """The driver's multi-GPU form: ``torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` (here
-    with gloo on CPU): the launcher's ranks are used as they are (no second spawn), one JSON line."""
+    with gloo on CPU): the launcher's ranks are used as they are (no second spawn), one JSON line, every
+    rank's parameters bitwise identical after the steps."""
     import socket
 
     s = socket.socket()
@@ -62,15 +64,15 @@ def test_bench_under_torchrun(tmp_path):
     s.close()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env.update(BENCH_BACKEND="gloo", BENCH_DUMP_PARAMS=str(tmp_path / "params"), HIP_VISIBLE_DEVICES="")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1",
            "--model", "tiny", "--batch", "2"]
     out = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["backend"] == "gloo" and len(res["per_rank_ms_per_step"]) == 2
-    p0 = torch.load(tmp_path / "params.rank0.pt", weights_only=True)
-    p1 = torch.load(tmp_path / "params.rank1.pt", weights_only=True)
-    assert torch.equal(p0, p1)
+    assert res["n_gpus"] == n and res["backend"] == "gloo" and len(res["per_rank_ms_per_step"]) == n
+    assert res["config"]["parallelism"] == f"dp{n}" and res["config"]["global_batch"] == 2 * n
+    ps = [torch.load(tmp_path / f"params.rank{r}.pt", weights_only=True) for r in range(n)]
+    assert all(torch.equal(ps[0], p) for p in ps[1:])
