@@ -725,6 +725,85 @@ def _ff_bwd(saved, params, needs, g, resid):
     return dx, dlw, dlb, dw1, db1, dw2, db2, dscale
 
 
+def _ln_spec(args, kind):
+    """(ln_w, ln_b, (T, S, shift)) of a reversible block's sublayer argument tuple."""
+    if kind == "attn":
+        meta = args[8]
+        return args[0], args[1], (meta[0], meta[1], meta[5])
+    return args[0], args[1], args[7]
+
+
+def _residual_chain(res, y, s, sign, nxt):
+    """res + sign * s * y (fp32) and, when ``nxt`` (the LN spec of the sublayer that reads it) is given, its
+    LayerNorm(+shift) in the same kernel (ln_shift_fwd_res: one read of the residual stream instead of two)."""
+    s = s if sign > 0 else -s
+    if nxt is None or not FUSED_SEQUENTIAL:
+        xo = torch.empty_like(res)
+        C().scale_residual_out(res.contiguous(), y, s, xo)
+        return xo, None
+    nw, nb, (T, S, shift) = nxt
+    xo, h, mean, rstd = C().ln_shift_fwd_res(res.contiguous(), y, s, nw.contiguous(), nb.contiguous(), T, S, shift, 1e-5)
+    return xo, (h, mean, rstd)
+
+
+def _attn_step(res, inp, args, pre, nxt, save: bool, sign: float = 1.0):
+    """``_attn_fwd`` whose LayerNorm may come precomputed (``pre`` = (h, mean, rstd) of ``inp``, from the
+    residual kernel that produced it) and whose residual update may carry the next sublayer's LayerNorm
+    (``nxt``). Returns (out, saved-or-None, LN of out or None)."""
+    ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta = args
+    T, S, K, H, pattern, shift = meta
+    inp = inp.contiguous()
+    h, mean, rstd = pre if pre is not None else C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    y, s, saved = _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, meta, save)
+    xo, ln_next = _residual_chain(res, y, s, sign, nxt)
+    return xo, saved, ln_next
+
+
+def _ff_step(res, inp, args, pre, nxt, save: bool, sign: float = 1.0):
+    """``_ff_fwd`` with the same LayerNorm hand-over as ``_attn_step``."""
+    ln_w, ln_b, w1, b1, w2, b2, scale, meta = args
+    T, S, shift = meta
+    inp = inp.contiguous()
+    h, mean, rstd = pre if pre is not None else C().ln_shift_fwd(inp, ln_w.contiguous(), ln_b.contiguous(), T, S, shift, 1e-5)
+    y, s, saved = _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save)
+    xo, ln_next = _residual_chain(res, y, s, sign, nxt)
+    return xo, saved, ln_next
+
+
+def _rev_sub_bwd(kind, saved, params, sk, g, resid, dy=None, prev=None):
+    """Reversible-stack sublayer backward on the arena sinks ``sk``. ``dy`` (bf16 grad of the pre-LayerScale
+    output) is either given -- the previous LN backward produced it -- or computed from the residual grad
+    ``g``; the LN backward adds ``resid`` into dx and, with ``prev`` = (y_prev, s_prev, dscale sink, dbias
+    sink) of the sublayer that produced this one's LN input, also runs that sublayer's LayerScale-residual
+    backward in the same kernel (ln_shift_bwd_sr). Returns (dx, dy_prev or None)."""
+    i_s, i_b = _SCALE_BIAS[kind]
+    if dy is None:
+        y, s = (saved[10], saved[12]) if kind == "attn" else (saved[8], saved[9])
+        dy, _, _ = C().scale_residual_bwd(g.contiguous(), y, s, sk[i_s], sk[i_b])
+    if kind == "attn":
+        dh, _, _ = _attn_core_bwd(saved, params, dy)
+        geo = saved[15]
+        T, S, shift = geo[2], geo[3], geo[7]
+    else:
+        dh, _, _, _ = _ff_core_bwd(saved, params, dy, sk)
+        T, S, shift = saved[10]
+    x, mean, rstd = saved[0], saved[1], saved[2]
+    if prev is None:
+        dx, _, _ = C().ln_shift_bwd(x, params[0].contiguous(), dh, mean, rstd, T, S, shift, resid.contiguous(), sk[0], sk[1])
+        return dx, None
+    yp, sp, gsp, gbp = prev
+    dx, dyp = C().ln_shift_bwd_sr(x, params[0].contiguous(), dh, mean, rstd, T, S, shift, resid.contiguous(), yp, sp,
+                                  sk[0], sk[1], gsp, gbp)
+    return dx, dyp
+
+
+def _res_of(kind, saved, sk):
+    """(y, s, dscale sink, dbias sink) of a sublayer's LayerScale residual, for ``_rev_sub_bwd(prev=...)``."""
+    i_s, i_b = _SCALE_BIAS[kind]
+    y, s = (saved[10], saved[12]) if kind == "attn" else (saved[8], saved[9])
+    return y, s, sk[i_s], sk[i_b]
+
+
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, w_qkv, w_out, b_out, scale, cos, sin, meta):
@@ -828,10 +907,13 @@ class _ReversibleFused(torch.autograd.Function):
         stored, used, storing = [], 0.0, budget > 0
         cuda = x.is_cuda
         with torch.no_grad():
-            for fa, ga in blocks:
+            pre = None  # LN of x2 for the next attention sublayer, computed by the residual kernel that wrote x2
+            for bi, (fa, ga) in enumerate(blocks):
                 before = torch.cuda.memory_allocated(x.device) if (cuda and storing and budget != float("inf")) else 0
-                x1, sf = _attn_fwd(x1, x2, *fa[0], save=storing)
-                x2, sg = _ff_fwd(x2, x1, *ga[0], save=storing)
+                nxt = _ln_spec(blocks[bi + 1][0][0], "attn") if bi + 1 < len(blocks) else None
+                x1, sf, pre_g = _attn_step(x1, x2, fa[0], pre, _ln_spec(ga[0], "ff"), save=storing)
+                x2, sg, pre = _ff_step(x2, x1, ga[0], pre_g, nxt, save=storing)
+                del pre_g
                 if storing:
                     if budget != float("inf") and cuda:
                         # this block's retained bytes; keep a second block's worth free for the backward
@@ -866,6 +948,11 @@ class _ReversibleFused(torch.autograd.Function):
         stored, ctx.stored = ctx.stored, None
         hook = _grad_ready_hook
         final = _final_at([fa[1] + ga[1] for fa, ga in blocks]) if hook is not None else None
+        sinks = [(_sinks(fa[1], [p.requires_grad for p in fa[1]]), _sinks(ga[1], [p.requires_grad for p in ga[1]]))
+                 for fa, ga in blocks]
+        if FUSED_SEQUENTIAL and all(a is not None and b is not None for a, b in sinks):
+            dx = _ReversibleFused._backward_chained(blocks, stored, sinks, y1, y2, dy1, dy2, hook, final)
+            return (dx, None, None, *([None] * len(ctx.params)))
         with torch.no_grad():
             for bi in reversed(range(len(blocks))):
                 fa, ga = blocks[bi]
@@ -873,7 +960,8 @@ class _ReversibleFused(torch.autograd.Function):
                 f_args, f_params = fa
                 rebuild = bi >= len(stored)  # blocks past the stored prefix are rebuilt from their outputs
                 if rebuild:
-                    x2, saved_g = _ff_fwd(y2, y1, *g_args, save=True, sign=-1.0)
+                    # x2 = y2 - g(y1), with f's LayerNorm of x2 from the same residual kernel
+                    x2, saved_g, pre_f = _ff_step(y2, y1, g_args, None, _ln_spec(f_args, "attn"), save=True, sign=-1.0)
                 else:
                     saved_f, saved_g = stored.pop()
                 res = _ff_bwd(saved_g, g_params, [p.requires_grad for p in g_params], dy2, dy1)
@@ -881,7 +969,8 @@ class _ReversibleFused(torch.autograd.Function):
                 dy1 = res[0]
                 collect(g_params, res[1:])
                 if rebuild:
-                    x1, saved_f = _attn_fwd(y1, x2, *f_args, save=True, sign=-1.0)
+                    x1, saved_f, _ = _attn_step(y1, x2, f_args, pre_f, None, save=True, sign=-1.0)
+                    del pre_f
                     y1, y2 = x1, x2
                 res = _attn_bwd(saved_f, f_params, [p.requires_grad for p in f_params], dy1, dy2)
                 del saved_f
@@ -891,6 +980,59 @@ class _ReversibleFused(torch.autograd.Function):
                     hook([p for p in final[bi] if id(p) not in pending])
         dx = dy1 + dy2
         return (dx, None, None, *[pending.get(id(p)) for p in ctx.params])
+
+    @staticmethod
+    def _backward_chained(blocks, stored, sinks, y1, y2, dy1, dy2, hook, final):
+        """Backward with every parameter grad in the arena and each LayerScale-residual backward fused into
+        the LayerNorm backward that produces its input grad (ln_shift_bwd_sr), as in the sequential stack:
+        g's LN backward (-> dy1) also yields f's dy; f's LN backward (-> dy2) also yields the PREVIOUS
+        block's g dy. So a block's f is rebuilt before g's backward, and the previous block's g one step
+        ahead (one more sublayer's activations alive at a time)."""
+        L = len(blocks)
+        ahead = None   # (x2, saved_g, pre_f) of the next block to process, rebuilt early
+        dyg = None     # g's dy of the block being processed, produced by the later block's f LN backward
+        with torch.no_grad():
+            for bi in reversed(range(L)):
+                fa, ga = blocks[bi]
+                f_args, f_params = fa
+                g_args, g_params = ga
+                sk_f, sk_g = sinks[bi]
+                rebuild = bi >= len(stored)
+                if rebuild:
+                    if ahead is not None:
+                        x2, saved_g, pre_f = ahead
+                        ahead = None
+                    else:
+                        x2, saved_g, pre_f = _ff_step(y2, y1, g_args, None, _ln_spec(f_args, "attn"), save=True, sign=-1.0)
+                    x1, saved_f, _ = _attn_step(y1, x2, f_args, pre_f, None, save=True, sign=-1.0)
+                    del pre_f
+                else:
+                    saved_f, saved_g = stored.pop()
+                    if ahead is not None:  # pragma: no cover - only rebuilt blocks are fetched ahead
+                        ahead = None
+                # g: LN backward adds dy1 and yields f's dy
+                dy1, dyf = _rev_sub_bwd("ff", saved_g, g_params, sk_g, dy2, dy1, dy=dyg,
+                                        prev=_res_of("attn", saved_f, sk_f))
+                del saved_g
+                # the previous block's g (its residual consumes f's input grad dy2)
+                prev = None
+                if bi > 0:
+                    pf_args, _ = blocks[bi - 1][0]
+                    pg_args, _ = blocks[bi - 1][1]
+                    psk_g = sinks[bi - 1][1]
+                    if bi - 1 >= len(stored):  # rebuilt: x2_prev = x2 - g_prev(x1), f_prev's LN on the way
+                        xs1, xs2 = (x1, x2) if rebuild else (y1, y2)
+                        ahead = _ff_step(xs2, xs1, pg_args, None, _ln_spec(pf_args, "attn"), save=True, sign=-1.0)
+                        prev = _res_of("ff", ahead[1], psk_g)
+                    else:
+                        prev = _res_of("ff", stored[-1][1], psk_g)
+                dy2, dyg = _rev_sub_bwd("attn", saved_f, f_params, sk_f, dy1, dy2, dy=dyf, prev=prev)
+                del saved_f
+                if rebuild:
+                    y1, y2 = x1, x2
+                if final is not None and final[bi]:
+                    hook(final[bi])
+        return dy1 + dy2
 
 
 def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: int, recompute=True):

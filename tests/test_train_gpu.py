@@ -94,3 +94,26 @@ def test_grads_reset_between_forward_and_backward(cuda):
     for n, p in m.named_parameters():
         assert p.grad is not None, n
         torch.testing.assert_close(p.grad, ref[n], rtol=1e-4, atol=1e-5, msg=n)
+
+
+@pytest.mark.parametrize("recompute", [True, False])
+def test_reversible_arena_backward_matches_autograd_grads(cuda, recompute):
+    """The reversible stack's chained backward (arena sinks: every LayerScale-residual backward fused into the
+    LN backward that produces its input grad, rebuilt blocks fetched one step ahead) against the per-op
+    backward that returns gradients to autograd (no arena), both from the same weights and batch."""
+    torch.manual_seed(0)
+    import dataclasses
+
+    cfg = dataclasses.replace(tiny(True), depth=4, attn_types=["axial_row", "axial_col", "axial_row", "conv_like"],
+                              shared_attn_ids=[0, 1, 2, 3], shared_ff_ids=[0, 1, 2, 3], reversible_recompute=recompute)
+    m = DALLE(cfg).to(cuda)
+    b = _batch(cfg, cuda)
+    _loss(m, b).backward()  # plain autograd grads (no .grad buffers existed in the forward)
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    arena = FlatArena(m.parameters(), device=cuda)
+    m.grad_arena = arena
+    arena.zero_grad()
+    _loss(m, b).backward()
+    for n, p in m.named_parameters():
+        torch.testing.assert_close(p.grad, ref[n], rtol=2e-3, atol=2e-5, msg=n)
