@@ -1004,12 +1004,13 @@ class _ReversibleFused(torch.autograd.Function):
                         ahead = None
                     else:
                         x2, saved_g, pre_f = _ff_step(y2, y1, g_args, None, _ln_spec(f_args, "attn"), save=True, sign=-1.0)
-                    x1, saved_f, _ = _attn_step(y1, x2, f_args, pre_f, None, save=True, sign=-1.0)
+                    # x1 = y1 - f(x2), with the previous block's g LayerNorm of x1 from the same kernel
+                    nxt_g = _ln_spec(blocks[bi - 1][1][0], "ff") if bi > 0 and bi - 1 >= len(stored) else None
+                    x1, saved_f, pre_gp = _attn_step(y1, x2, f_args, pre_f, nxt_g, save=True, sign=-1.0)
                     del pre_f
                 else:
                     saved_f, saved_g = stored.pop()
-                    if ahead is not None:  # pragma: no cover - only rebuilt blocks are fetched ahead
-                        ahead = None
+                    pre_gp = None
                 # g: LN backward adds dy1 and yields f's dy
                 dy1, dyf = _rev_sub_bwd("ff", saved_g, g_params, sk_g, dy2, dy1, dy=dyg,
                                         prev=_res_of("attn", saved_f, sk_f))
@@ -1021,11 +1022,11 @@ class _ReversibleFused(torch.autograd.Function):
                     pg_args, _ = blocks[bi - 1][1]
                     psk_g = sinks[bi - 1][1]
                     if bi - 1 >= len(stored):  # rebuilt: x2_prev = x2 - g_prev(x1), f_prev's LN on the way
-                        xs1, xs2 = (x1, x2) if rebuild else (y1, y2)
-                        ahead = _ff_step(xs2, xs1, pg_args, None, _ln_spec(pf_args, "attn"), save=True, sign=-1.0)
+                        ahead = _ff_step(x2, x1, pg_args, pre_gp, _ln_spec(pf_args, "attn"), save=True, sign=-1.0)
                         prev = _res_of("ff", ahead[1], psk_g)
                     else:
                         prev = _res_of("ff", stored[-1][1], psk_g)
+                pre_gp = None
                 dy2, dyg = _rev_sub_bwd("attn", saved_f, f_params, sk_f, dy1, dy2, dy=dyf, prev=prev)
                 del saved_f
                 if rebuild:
