@@ -58,7 +58,9 @@ def main():
           flush=True)
     if args.profile_steps:
         # image positions only (the text-key part of every sparse pattern is read from here on)
-        for _ in range(args.profile_steps):
+        if use_graph and hasattr(eng, "replay_steps"):
+            eng.replay_steps(args.profile_steps)
+        for _ in range(0 if (use_graph and hasattr(eng, "replay_steps")) else args.profile_steps):
             eng.graph.replay() if use_graph else eng._image_step()
         torch.cuda.synchronize()
         return
@@ -79,7 +81,9 @@ def main():
     prefill(tb)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(64):
+    if use_graph and hasattr(eng, "replay_steps"):
+        eng.replay_steps(64)
+    for _ in range(0 if (use_graph and hasattr(eng, "replay_steps")) else 64):
         eng.graph.replay() if use_graph else eng._step()
     torch.cuda.synchronize()
     per_tok = (time.perf_counter() - t1) / 64
