@@ -75,6 +75,10 @@ bool sample_step(const SampleArgs&, hipStream_t);
 bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
+void gemm_set_cpol(int);
+int gemm_cpol();
+void gemm_set_drain(int);
+int gemm_drain();
 bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
                       hipStream_t, int);
 bool gemm_pt_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
@@ -498,10 +502,16 @@ Tensor gemm_pt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant, 
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 128, "gemm_pt: M, N multiples of 256, K of 64 (>= 128)");
   const void* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
-    CHECK_IN((*bias), torch::kBFloat16);
-    TORCH_CHECK(bias->numel() == N, "gemm_pt: bias (N,)");
+    if (variant == 40 || variant == 41) {  // measurement: per-workgroup timestamps (int64, 5 per tile)
+      CHECK_IN((*bias), torch::kLong);
+      TORCH_CHECK(bias->numel() >= (int64_t)(M / 256) * (N / 256) * 5, "gemm_pt: stamps (tiles * 5,)");
+    } else {
+      CHECK_IN((*bias), torch::kBFloat16);
+      TORCH_CHECK(bias->numel() == N, "gemm_pt: bias (N,)");
+    }
     bp = bias->data_ptr();
   }
+  TORCH_CHECK(variant != 40 && variant != 41 || bp != nullptr, "gemm_pt: stamp variants need the stamp buffer");
   auto C = torch::empty({M, N}, A.options());
   TORCH_CHECK(dalle::gemm_pt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, N, (int)variant, (int)group, cur_stream()),
               "gemm_pt: unsupported shape");
@@ -1169,6 +1179,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zero_if_nonfinite_", &zero_if_nonfinite_);
   m.def("uq8_seg_dequant_", &uq8_seg_dequant_);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
+  m.def("gemm_set_cpol", [](int64_t c) { dalle::gemm_set_cpol((int)c); }, py::arg("cpol"),
+        "cache policy of the hand-written GEMMs' output stores: 0 plain, 1 sc0, 2 nt, 16 sc1, 17 sc0 sc1");
+  m.def("gemm_cpol", []() { return (int64_t)dalle::gemm_cpol(); });
+  m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),
+        "1: hand-written GEMM workgroups wait for their output stores before ending");
+  m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
   m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),
         py::arg("n"), py::arg("col_major"), py::arg("qscale"), py::arg("persist") = -1);

@@ -55,6 +55,41 @@ __device__ __forceinline__ void stagger_start(int ticks, int first_wave) {
   while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
 }
 
+// ---- epilogue stores with an explicit cache policy ----
+// GEMM epilogues write their whole output once and never read it back inside the kernel. Plain (and
+// `nt`) stores keep every written line in the XCD's 4 MB L2, so each wave of 256 x 256 output tiles
+// (4 MB per XCD) evicts the operand panels the next tiles stream from; `sc1` / `sc0 sc1` stores drop the
+// line from L2 after the write (MI355X_MICROARCH.md, "stores of each flavour"). cpol is the raw buffer
+// store's aux immediate: 1 = sc0, 2 = nt, 16 = sc1 (17 = sc0 sc1); 0 = a plain flat store.
+typedef unsigned u32x4_vs __attribute__((vector_size(16)));
+
+// whole-buffer descriptor over a wave-uniform base: the 32-bit per-lane byte offset addresses up to 4 GiB
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, -1, 0x00020000);
+}
+
+template <int AUX>
+__device__ __forceinline__ void bstore16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4_vs v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
+}
+
+// 16-byte store of v at base + off (bytes) under cache policy cpol (wave-uniform)
+__device__ __forceinline__ void cstore16(void* base, __amdgpu_buffer_rsrc_t r, uint32_t off, u32x4_vs v, int cpol) {
+  switch (cpol) {
+    case 0: *reinterpret_cast<u32x4_vs*>((char*)base + off) = v; break;
+    case 1: bstore16<1>(r, off, v); break;
+    case 2: bstore16<2>(r, off, v); break;
+    case 16: bstore16<16>(r, off, v); break;
+    case 17: bstore16<17>(r, off, v); break;
+    case 18: bstore16<18>(r, off, v); break;
+    case 19: bstore16<19>(r, off, v); break;
+    default: bstore16<0>(r, off, v); break;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -197,6 +197,8 @@ struct RopeEpi {
   // non-temporal epilogue output stores (DALLE_AMD_GEMM_NT_STORE=1): -5 % on the plain-store kernel at
   // the large shapes, no gain on the fused epilogues or the full step (profiles/r2_gemm_epilogue_cost.jsonl)
   int nt = 0;
+  int drain = 0;  // s_waitcnt vmcnt(0) after the epilogue (gemm_pt.hip DALLE_AMD_GEMM_DRAIN)
+  int cpol = 0;  // cache policy of the output stores (common.h cstore16; gemm_pt.hip DALLE_AMD_GEMM_CPOL)
   int stagger = 0, first_wave = 0;  // start-time stagger of the first wave (common.h stagger_start)
 };
 
@@ -346,6 +348,7 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_s_waitcnt(0xC07F);
   if (EPI == 0 || EPI == 6 || EPI == 7) {  // 6: measurement only, LDS staging without the global stores
+    const __amdgpu_buffer_rsrc_t oc = uniform_rsrc(C);
     __bf16* Cw = C + (size_t)(row0 + wm * 128) * N + col0 + wn * 64;
     int t = 0;
 #pragma unroll
@@ -354,7 +357,9 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
       const int row = idx >> 3, ch = idx & 7;
       const s16x8 v = *reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3));
       if (EPI == 0) {
-        epi_store16(reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8), v, rope.nt);
+        if (rope.cpol) cstore16(C, oc, (uint32_t)(((size_t)(row0 + wm * 128 + row) * N + col0 + wn * 64 + ch * 8) * 2),
+                                __builtin_bit_cast(u32x4_vs, v), rope.cpol);
+        else epi_store16(reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8), v, rope.nt);
       } else if (EPI == 7) {  // non-temporal stores
         __builtin_nontemporal_store(v, reinterpret_cast<s16x8*>(Cw + (size_t)row * N + ch * 8));
       } else {
@@ -370,6 +375,7 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
     // into one partial row per 128-row wave block.
     const int F = rope.F;
     const int c = gcol;
+    const __amdgpu_buffer_rsrc_t od = uniform_rsrc(rope.gdh);
     float sv[8] = {}, sg[8] = {};
     load_h(0);
     load_h(1);
@@ -389,8 +395,13 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
         dg[i] = d[i] * a[i] * gr;
       }
       const s16x8 pa = pack8(da), pg = pack8(dg);
-      epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + c), pa, rope.nt);
-      epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + F + c), pg, rope.nt);
+      if (rope.cpol) {
+        cstore16(rope.gdh, od, (uint32_t)((r * 2 * F + c) * 2), __builtin_bit_cast(u32x4_vs, pa), rope.cpol);
+        cstore16(rope.gdh, od, (uint32_t)((r * 2 * F + F + c) * 2), __builtin_bit_cast(u32x4_vs, pg), rope.cpol);
+      } else {
+        epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + c), pa, rope.nt);
+        epi_store16(reinterpret_cast<s16x8*>(rope.gdh + r * 2 * F + F + c), pg, rope.nt);
+      }
       unpack8(pa, da);
       unpack8(pg, dg);
 #pragma unroll
@@ -416,6 +427,7 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
     const int part = c0 / HD, h = (c0 - part * HD) >> 6;
     __bf16* dstT = part == 0 ? rope.q : (part == 1 ? rope.k : rope.v);
     const float sc = part == 0 ? rope.qscale : 1.0f;
+    const __amdgpu_buffer_rsrc_t oq = uniform_rsrc(dstT);
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {
       const int idx = it * 64 + lane;
@@ -437,7 +449,9 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
         x[i + 1] = (a1 * cs[i + 1] + a0 * sn[i + 1]) * sc;
       }
       const int srow = rope_epi_seq2st(rope, p);
-      epi_store16(reinterpret_cast<s16x8*>(dstT + ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8), pack8(x), rope.nt);
+      const size_t o = ((size_t)(b * rope.H + h) * rope.Np + srow) * 64 + ch * 8;
+      if (rope.cpol) cstore16(dstT, oq, (uint32_t)(o * 2), __builtin_bit_cast(u32x4_vs, pack8(x)), rope.cpol);
+      else epi_store16(reinterpret_cast<s16x8*>(dstT + o), pack8(x), rope.nt);
     }
   }
 }
@@ -736,6 +750,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_nt_8ph_kernel(const __bf16*
   } else {
     gemm_store_epilogue<EPI>(acc, smem, C, bias, N, row0, col0, wave, lane, rope);
   }
+  if (rope.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // zero the storage rows that have no sequence position (text padding [T, Tp) and the last image slot)
@@ -757,6 +772,8 @@ void rope_pad_zero(void* q, void* k, void* v, int Tp, int T, int Np, int BH, hip
 }
 
 int gemm_stagger_ticks(int ntiles, int K);
+int gemm_cpol();
+int gemm_drain();
 bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int epi, hipStream_t st) {
   if (M % GBM || N % GBN || K % GBK) return false;
   const int nwg = (M / GBM) * (N / GBN);
@@ -781,8 +798,11 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
       // column groups of (variant - 300), 400 + g -> row groups of g
       if (epi >= 300 && epi < 333) {
         const int group = epi == 300 ? 4 : epi - 300;
+        RopeEpi e{};
+        e.cpol = gemm_cpol();
+        e.drain = gemm_drain();
         hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
-                           (__bf16*)C, (const __bf16*)bias, M, N, K, RopeEpi{}, group);
+                           (__bf16*)C, (const __bf16*)bias, M, N, K, e, group);
         return true;
       }
       if (epi == 390) {  // measurement: the 8-phase kernel with the first-wave start stagger
@@ -818,6 +838,8 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
 // bf16, then dh (M, 2F) = GEGLU'(h, du) and part ((M / 128), 2F) = partial FF-in bias grads. The
 // (M, F) du intermediate never exists.
 int gemm_stagger_ticks(int ntiles, int K);
+int gemm_cpol();
+int gemm_drain();
 bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, float* part, int M, int F, int K,
                     hipStream_t st, int stagger) {
   if (M % GBM || F % GBN || K % GBK) return false;
@@ -829,6 +851,8 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   e.gdh = (__bf16*)dh;
   e.gpart = part;
   e.F = F;
+  e.cpol = gemm_cpol();
+  e.drain = gemm_drain();
   const int nwg = (M / GBM) * (F / GBN);
   hipLaunchKernelGGL((gemm_nt_8ph_kernel<2, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
                      (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);
@@ -840,11 +864,13 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
 // split accumulates (or stores) straight into `out`; more write fp32 slabs to `ws` (splits x N x K)
 // that splitk_accum folds in split order (deterministic).
 void splitk_accum(const float* part, float* acc, long n, int s, int accumulate, hipStream_t st);
+int gemm_drain();
 bool gemm_wgrad(const void* G, const void* X, float* out, float* ws, int Mtok, int Nout, int Kin, int splits, int accumulate,
                 hipStream_t st) {
   if (Nout % GBM || Kin % GBN || splits < 1 || Mtok % (splits * GBK)) return false;
   if (splits > 1 && ws == nullptr) return false;
   RopeEpi e{};
+  e.drain = gemm_drain();
   const int tiles = (Nout / GBM) * (Kin / GBN);
   const int kt = Mtok / splits;
   dim3 grid(tiles, splits);
@@ -875,6 +901,8 @@ bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, cons
   const int Tp = (T + 31) / 32 * 32;
   RopeEpi e{(__bf16*)q, (__bf16*)k, (__bf16*)v, cosT, sinT, T, Tp, S, logS, n, Tp + S * S, H, col_major, qscale};
   e.nt = gemm_nt_store_default();
+  e.cpol = gemm_cpol();
+  e.drain = gemm_drain();
   const int nwg = (M / GBM) * (N / GBN);
   // 8-phase staggered template: 1073 vs 1042 TF for the phased kernel at M=61440, N=3072, K=1024
   // (profiles/r1_gemm_8phase.jsonl)

@@ -26,6 +26,8 @@
 // pre-activation a = [value | gate] and u = value * gelu(gate)), 5 = none (measurement only).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dalle {
 
 namespace pt {
@@ -99,9 +101,17 @@ __device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
   y = r[1];
 }
 
-__device__ __forceinline__ void st16(void* p, unsigned x0, unsigned x1, unsigned y0, unsigned y1) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(x0, x1, y0, y1);
-}
+// epilogue output stream: a wave-uniform base, its buffer descriptor and the store cache policy
+struct Out {
+  __bf16* base;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int cpol;
+  __device__ __forceinline__ Out(__bf16* b, int cp) : base(b), rsrc(uniform_rsrc(b)), cpol(cp) {}
+  __device__ __forceinline__ void st(__bf16* p, unsigned x0, unsigned x1, unsigned y0, unsigned y1) const {
+    const u32x4_vs v = {x0, x1, y0, y1};
+    cstore16(base, rsrc, (uint32_t)((char*)p - (char*)base), v, cpol);
+  }
+};
 
 }  // namespace pt
 
@@ -128,6 +138,12 @@ struct PtArgs {
   __bf16* u;
   int group;
   int stagger, first_wave;  // per-tile mode: start-time stagger of the first wave (stagger_start)
+  int cpol;                 // cache policy of the output stores (common.h cstore16)
+  // measurement only (one tile per workgroup): per workgroup {start, epilogue start, stores issued,
+  // stores complete, CU id} in 10 ns real-time ticks; skip_odd = odd workgroups issue no stores
+  unsigned long long* stamps;
+  int skip_odd;
+  int drain;  // wait for the output stores before the workgroup ends (gemm_set_drain)
 };
 
 __device__ __forceinline__ int pt_seq2st(const PtArgs& e, int p) {
@@ -155,6 +171,8 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
     return;
   }
   if constexpr (EPI == 0) {
+    if (e.skip_odd && (blockIdx.x & 1)) return;
+    const pt::Out oc(e.C, e.cpol);
     float bv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -179,7 +197,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
         unsigned y1 = pk2(acc[i][j1][2] + bv[j1][2], acc[i][j1][3] + bv[j1][3]);
         swap16(x0, y0);
         swap16(x1, y1);
-        st16(rowp + ((q & 1) ? j1 : j0) * 16, x0, x1, y0, y1);
+        oc.st(rowp + ((q & 1) ? j1 : j0) * 16, x0, x1, y0, y1);
       }
     }
   } else if constexpr (EPI == 1) {
@@ -188,6 +206,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
     const int part = cw / HD, hh = (cw - part * HD) >> 6;
     __bf16* dstT = part == 0 ? e.q : (part == 1 ? e.k : e.v);
     const float sc = part == 0 ? e.qscale : 1.0f;
+    const pt::Out oc(dstT, e.cpol);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = r0 + wm * 128 + i * 16 + fr;
@@ -209,7 +228,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
         const int j0 = 2 * jp, j1 = j0 + 1;
         swap16(w[j0][0], w[j1][0]);
         swap16(w[j0][1], w[j1][1]);
-        st16(rowp + ((q & 1) ? j1 : j0) * 16, w[j0][0], w[j0][1], w[j1][0], w[j1][1]);
+        oc.st(rowp + ((q & 1) ? j1 : j0) * 16, w[j0][0], w[j0][1], w[j1][0], w[j1][1]);
       }
       __builtin_amdgcn_sched_barrier(0);  // bound the live loads to one row sub-tile
     }
@@ -219,6 +238,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
     // column sums of the (bf16) results over each 64-row half of the wave's 128 rows -> part. One
     // sub-tile pair (j0, j0 + 1) of one 64-row half at a time keeps the live set small.
     const int F = e.F;
+    const pt::Out od(e.dh, e.cpol);
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
@@ -271,8 +291,8 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
           }
           swap16(da[0][0], da[1][0]); swap16(da[0][1], da[1][1]);
           swap16(dg[0][0], dg[1][0]); swap16(dg[0][1], dg[1][1]);
-          pt::st16(e.dh + off, da[0][0], da[0][1], da[1][0], da[1][1]);
-          pt::st16(e.dh + off + F, dg[0][0], dg[0][1], dg[1][0], dg[1][1]);
+          od.st(e.dh + off, da[0][0], da[0][1], da[1][0], da[1][1]);
+          od.st(e.dh + off + F, dg[0][0], dg[0][1], dg[1][0], dg[1][1]);
         }
         // reduce over the 16 rows held by lanes 16q .. 16q+15 (fixed xor tree: deterministic)
 #pragma unroll
@@ -299,6 +319,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
     // (W1 / b1 rows interleaved on the host); j = 0, 1 value, j = 2, 3 the matching gate
     const int F = e.F;
     const int fb = cw >> 1;
+    const pt::Out oa(e.a, e.cpol), ou(e.u, e.cpol);
     float bv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -336,9 +357,9 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
       swap16(gg[0][0], gg[1][0]); swap16(gg[0][1], gg[1][1]);
       swap16(uu[0][0], uu[1][0]); swap16(uu[0][1], uu[1][1]);
       const int jo = (q & 1) * 16;
-      pt::st16(ap + jo, vv[0][0], vv[0][1], vv[1][0], vv[1][1]);
-      pt::st16(ap + F + jo, gg[0][0], gg[0][1], gg[1][0], gg[1][1]);
-      pt::st16(up + jo, uu[0][0], uu[0][1], uu[1][0], uu[1][1]);
+      oa.st(ap + jo, vv[0][0], vv[0][1], vv[1][0], vv[1][1]);
+      oa.st(ap + F + jo, gg[0][0], gg[0][1], gg[1][0], gg[1][1]);
+      ou.st(up + jo, uu[0][0], uu[0][1], uu[1][0], uu[1][1]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -355,6 +376,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   // object can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];
   if constexpr (!PERSIST) stagger_start(e.stagger, e.first_wave);
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_m = M / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
@@ -517,7 +539,18 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
     if (it + 2 < my_tiles) origin(it + 2, nr, nc);
   }
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
+  const unsigned long long t_epi = __builtin_amdgcn_s_memrealtime();
   pt_epilogue<EPI>(acc, pr, pc, wm, wn, lane, e);
+  if (e.drain && e.stamps == nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!PERSIST && e.stamps != nullptr) {
+    const unsigned long long t_issued = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t_done = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      unsigned long long* o = e.stamps + (size_t)blockIdx.x * 5;
+      o[0] = t_start; o[1] = t_epi; o[2] = t_issued; o[3] = t_done; o[4] = (unsigned long long)__smid();
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -571,6 +604,26 @@ int gemm_stagger_ticks(int ntiles, int K) {
   return (int)(tile_s * pct / 100.0 * 1e8);
 }
 
+// DALLE_AMD_GEMM_CPOL: cache policy of every hand-written GEMM's output stores (common.h cstore16);
+// gemm_set_cpol overrides it at run time (benchmarks)
+static int g_gemm_cpol = [] {
+  const char* s = getenv("DALLE_AMD_GEMM_CPOL");
+  return s ? atoi(s) : 0;
+}();
+void gemm_set_cpol(int c) { g_gemm_cpol = c; }
+int gemm_cpol() { return g_gemm_cpol; }
+
+// DALLE_AMD_GEMM_DRAIN=1: every hand-written GEMM workgroup waits for its output stores (s_waitcnt
+// vmcnt(0)) before it ends. Measured: a one-tile-per-workgroup GEMM whose waves end with their
+// epilogue stores still in flight runs 4-11 % slower than the same kernel draining them first
+// (profiles/r3_gemm_epilogue_stamps.jsonl); gemm_set_drain overrides it at run time
+static int g_gemm_drain = [] {
+  const char* s = getenv("DALLE_AMD_GEMM_DRAIN");
+  return s ? atoi(s) : 1;
+}();
+void gemm_set_drain(int d) { g_gemm_drain = d; }
+int gemm_drain() { return g_gemm_drain; }
+
 template <int EPI>
 static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist = -1) {
   const int ntiles = (M / pt::BM) * (N / pt::BN);
@@ -578,6 +631,8 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
   if (!persist && e.stagger < 0) e.stagger = gemm_stagger_ticks(ntiles, K);
   if (e.stagger < 0) e.stagger = 0;
   e.first_wave = pt_cus();
+  e.cpol = g_gemm_cpol;
+  e.drain = g_gemm_drain;
   if (persist)
     hipLaunchKernelGGL((gemm_pt_kernel<EPI, true>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
                        (const __bf16*)B, M, N, K, e);
@@ -610,6 +665,12 @@ bool gemm_pt(const void* A, const void* B, void* C, const void* bias, int M, int
   // +30 = one tile per workgroup without the start stagger
   const int persist = (epi >= 20 && epi < 30) ? 1 : (epi >= 10 ? 0 : -1);
   if (epi >= 30) e.stagger = 0;
+  if (epi == 40 || epi == 41) {  // measurement: per-workgroup timestamps into bias (as int64 buffer)
+    e.stamps = (unsigned long long*)bias;
+    e.bias = nullptr;
+    e.skip_odd = epi == 41;
+    epi = 30;
+  }
   if (epi % 10 == 5) pt_launch<5>(A, B, M, N, K, e, st, persist);
   else pt_launch<0>(A, B, M, N, K, e, st, persist);
   return true;
