@@ -564,7 +564,10 @@ static int pt_grid(int ntiles) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  // one workgroup per CU (128 KiB of LDS); a multiple of 8 keeps each workgroup on one XCD's range
+  // one workgroup per CU (128 KiB of LDS); a multiple of 8 keeps each workgroup on one XCD's range.
+  // DALLE_AMD_PT_GRID caps the workgroup count (measurement: epilogue cost vs concurrent storers)
+  const char* gcap = getenv("DALLE_AMD_PT_GRID");
+  if (gcap && atoi(gcap) > 0 && atoi(gcap) < cus) return atoi(gcap) < ntiles ? atoi(gcap) : ntiles;
   int g = cus < ntiles ? cus : ntiles;
   if (g > 8 && ntiles > g) g &= ~7;
   return g;

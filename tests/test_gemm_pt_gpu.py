@@ -131,3 +131,43 @@ def test_ff_in_geglu_pt(cuda, M, F, K, persist):
     # approximation (|error| <= 1.5e-7) differs by at most one bf16 rounding step
     u_old = C.geglu_fwd(a).float()
     assert ((u.float() - u_old).abs() <= 2 ** -7 * u_old.abs() + 1e-6).all()
+
+
+@pytest.mark.parametrize("cpol", [0, 1, 2, 16, 17])
+@pytest.mark.parametrize("drain", [0, 1])
+def test_store_policy_and_drain_bitwise(cuda, cpol, drain):
+    """Output-store cache policies (gemm_set_cpol: plain / sc0 / nt / sc1 / sc0 sc1 buffer stores) and the
+    end-of-workgroup store drain (gemm_set_drain) change how the epilogue writes, never what: every
+    hand-written GEMM form is bitwise equal to the plain-store, no-drain result."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(1)
+    M, N, K = 2048, 1024, 256
+    A = torch.randn(M, K, device=cuda).bfloat16()
+    B = torch.randn(N, K, device=cuda).bfloat16()
+    bias = torch.randn(N, device=cuda).bfloat16()
+    dy = (0.5 * torch.randn(M, K, device=cuda)).bfloat16()
+    w2t = (0.05 * torch.randn(N, K, device=cuda)).bfloat16()
+    a = torch.randn(M, 2 * N, device=cuda).bfloat16()
+
+    def run_all():
+        outs = [C.gemm_pt(A, B, bias, 10, 0), C.gemm_pt(A, B, bias, 20, 0), C.gemm_nt(A, B, None, 300)]
+        dh8 = C.ff_dgrad_geglu(dy, w2t, a, None, 0)
+        dhp = C.ff_dgrad_geglu_pt(dy, w2t, a)
+        outs += list(dh8) if isinstance(dh8, (tuple, list)) else [dh8]
+        outs += list(dhp) if isinstance(dhp, (tuple, list)) else [dhp]
+        return [o.clone() for o in outs]
+
+    try:
+        C.gemm_set_cpol(0)
+        C.gemm_set_drain(0)
+        ref = run_all()
+        C.gemm_set_cpol(cpol)
+        C.gemm_set_drain(drain)
+        got = run_all()
+    finally:
+        C.gemm_set_cpol(0)
+        C.gemm_set_drain(1)
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
