@@ -799,7 +799,7 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
       if (epi >= 300 && epi < 333) {
         const int group = epi == 300 ? 4 : epi - 300;
         RopeEpi e{};
-        e.cpol = gemm_cpol();
+        e.cpol = (size_t)M * N * 2 < (1ull << 32) ? gemm_cpol() : 0;  // buffer stores: 32-bit byte offsets
         e.drain = gemm_drain();
         hipLaunchKernelGGL((gemm_nt_8ph_kernel<0, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)A, (const __bf16*)B,
                            (__bf16*)C, (const __bf16*)bias, M, N, K, e, group);
@@ -851,7 +851,7 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   e.gdh = (__bf16*)dh;
   e.gpart = part;
   e.F = F;
-  e.cpol = gemm_cpol();
+  e.cpol = (size_t)M * F * 4 < (1ull << 32) ? gemm_cpol() : 0;  // buffer stores: 32-bit byte offsets
   e.drain = gemm_drain();
   const int nwg = (M / GBM) * (F / GBN);
   hipLaunchKernelGGL((gemm_nt_8ph_kernel<2, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
@@ -901,7 +901,7 @@ bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, cons
   const int Tp = (T + 31) / 32 * 32;
   RopeEpi e{(__bf16*)q, (__bf16*)k, (__bf16*)v, cosT, sinT, T, Tp, S, logS, n, Tp + S * S, H, col_major, qscale};
   e.nt = gemm_nt_store_default();
-  e.cpol = gemm_cpol();
+  e.cpol = (size_t)M * N * 4 < (1ull << 32) ? gemm_cpol() : 0;  // buffer stores: 32-bit byte offsets
   e.drain = gemm_drain();
   const int nwg = (M / GBM) * (N / GBN);
   // 8-phase staggered template: 1073 vs 1042 TF for the phased kernel at M=61440, N=3072, K=1024

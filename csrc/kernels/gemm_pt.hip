@@ -634,7 +634,8 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
   if (!persist && e.stagger < 0) e.stagger = gemm_stagger_ticks(ntiles, K);
   if (e.stagger < 0) e.stagger = 0;
   e.first_wave = pt_cus();
-  e.cpol = g_gemm_cpol;
+  // buffer-store policies address the output with a 32-bit byte offset: plain stores past 2 GiB of output
+  e.cpol = (size_t)M * N * 4 < (1ull << 32) ? g_gemm_cpol : 0;
   e.drain = g_gemm_drain;
   if (persist)
     hipLaunchKernelGGL((gemm_pt_kernel<EPI, true>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
