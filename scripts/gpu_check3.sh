@@ -13,5 +13,5 @@ timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --engine collab > gpuru
 grep '^{' gpurun_out/${TAG}_bench_collab.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d.get(k) for k in ('value','ms_per_step','collab_performance_ema_samples_per_s','collab_ema_over_wall','collab_backward_overlapped_rounds')})"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 rm -f gpurun_out/prof_$TAG/run_kernel_trace.csv
-python3 scripts/prof_summary.py gpurun_out/prof_$TAG/run_kernel_stats.csv 40 7 > gpurun_out/prof_${TAG}_top.txt
+python3 scripts/prof_summary.py gpurun_out/prof_$TAG/run_kernel_stats.csv 40 ${PROF_STEPS:-7} > gpurun_out/prof_${TAG}_top.txt
 head -30 gpurun_out/prof_${TAG}_top.txt
