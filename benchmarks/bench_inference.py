@@ -64,6 +64,10 @@ def main():
             eng.graph.replay() if use_graph else eng._image_step()
         torch.cuda.synchronize()
         return
+    # one more untimed generate: the first one after the standalone prefill above runs ~0.3 s slow
+    # (profiles/r3_decode_partials_cols.txt), which is not the steady-state rate
+    model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.iters):
         out = model.generate_images(text, top_k=args.top_k, use_graph=use_graph)
