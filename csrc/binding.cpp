@@ -56,7 +56,8 @@ void gn_apply(const void*, const float*, const float*, const float*, const float
 bool conv_out(const void*, const void*, const float*, const float*, const float*, const float*, const float*, float*, int, int,
               int, int, hipStream_t);
 void softmax_rows(const float*, void*, long, int, float, hipStream_t);
-long xent_colsum_blocks(long);
+long xent_colsum_blocks(long, int);
+void xent_set_reg(int);
 void embed_bwd(const float*, const int*, const int*, const int*, float*, float*, int, int, hipStream_t);
 void decode_ln_shift(float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int, hipStream_t,
                      const float*, const void*, const float*, int);
@@ -820,7 +821,7 @@ Tensor xent_colsum_(Tensor logits, Tensor labels, double gscale, Tensor dbias) {
   const int V = logits.size(1);
   auto loss = torch::empty({R}, logits.options().dtype(torch::kFloat32));
   if (R == 0) return loss;
-  auto part = torch::empty({dalle::xent_colsum_blocks(R), V}, logits.options().dtype(torch::kFloat32));
+  auto part = torch::empty({dalle::xent_colsum_blocks(R, V), V}, logits.options().dtype(torch::kFloat32));
   TORCH_CHECK(dalle::xent_colsum(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), part.data_ptr<float>(),
                                  R, V, (float)gscale, cur_stream()), "xent_colsum: vocabulary split too wide for LDS");
   dalle::GradSink sink{dbias.data_ptr<float>(), nullptr, nullptr, V, 1};
@@ -1196,6 +1197,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("embed_fwd", &embed_fwd);
   m.def("xent_colsum_", &xent_colsum_);
+  m.def("xent_set_reg", &dalle::xent_set_reg, "1: register-resident cross-entropy kernels where the vocabulary fits, 0: LDS form");
   m.def("conv3x3", &conv3x3, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("res") = py::none(),
         py::arg("mean") = py::none(), py::arg("rstd") = py::none(), py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
         py::arg("ups") = false);

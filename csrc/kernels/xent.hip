@@ -199,7 +199,133 @@ __global__ __launch_bounds__(XENT_T) void xent_colsum_kernel(__bf16* __restrict_
   for (int c = tid; c < V; c += XENT_T) prow[c] = colacc[xpad(c)];
 }
 
+// Register-resident form: a row is spread over the W waves of one workgroup (image vocabulary: W = 4, 4
+// x 16 B per lane; text: W = 16, 8 x 8 B per lane), so it is read from HBM exactly once -- max, sum of
+// exponentials and the gradient all come from registers -- and each lane keeps the column sums of its
+// own columns in registers (no LDS accumulator: the LDS form above fits one workgroup, one row in flight,
+// per CU at the text vocabulary; this one keeps several rows per CU in flight). Every wave owns fixed
+// columns, so the workgroup's partial row is written without a combine. Fixed-order reductions
+// throughout: deterministic.
+template <int NV, int W, int E>
+__global__ __launch_bounds__(64 * W) void xent_reg_kernel(__bf16* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                          float* __restrict__ loss, float* __restrict__ part, long R, int V,
+                                                          float gscale) {
+  typedef short vecE __attribute__((ext_vector_type(E)));
+  __shared__ float xs[2][W];  // per-wave row max / sum of exponentials
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  float acc[NV][E];
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[j][e] = 0.f;
+  for (long row = blockIdx.x; row < R; row += gridDim.x) {
+    const bf16_raw* lr = reinterpret_cast<const bf16_raw*>(logits) + row * (long)V;
+    vecE d[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = ((j * W + wave) * 64 + lane) * E;
+      d[j] = c < V ? *reinterpret_cast<const vecE*>(lr + c) : vecE{};
+    }
+    const int lab = (int)labels[row];
+    float m = NEG_BIG;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = ((j * W + wave) * 64 + lane) * E;
+      if (c < V) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) m = fmaxf(m, bf2f((bf16_raw)d[j][e]));
+      }
+    }
+    m = wave_max(m);
+    if (lane == 0) xs[0][wave] = m;
+    __syncthreads();
+    m = xs[0][0];
+#pragma unroll
+    for (int k = 1; k < W; ++k) m = fmaxf(m, xs[0][k]);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = ((j * W + wave) * 64 + lane) * E;
+      if (c < V) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) s += __expf(bf2f((bf16_raw)d[j][e]) - m);
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) xs[1][wave] = s;  // a different slot than the max: no wave can overwrite what another still reads
+    __syncthreads();
+    s = 0.f;
+#pragma unroll
+    for (int k = 0; k < W; ++k) s += xs[1][k];
+    const float lse = m + __logf(s);
+    bf16_raw* lw = reinterpret_cast<bf16_raw*>(logits) + row * (long)V;
+    float xl = 0.f;
+    bool own = false;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = ((j * W + wave) * 64 + lane) * E;
+      if (c < V) {
+        vecE q;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float f = bf2f((bf16_raw)d[j][e]);
+          const bool hit = c + e == lab;
+          const float g = __expf(f - lse) - (hit ? 1.0f : 0.0f);
+          xl = hit ? f : xl;
+          own |= hit;
+          q[e] = (short)f2bf(g * gscale);
+          acc[j][e] += bf2f((bf16_raw)q[e]);  // the bias gradient sums the bf16 values the GEMMs consume
+        }
+        *reinterpret_cast<vecE*>(lw + c) = q;
+      }
+    }
+    if (own) loss[row] = lse - xl;
+  }
+  float* prow = part + (size_t)blockIdx.x * V;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = ((j * W + wave) * 64 + lane) * E;
+    if (c < V) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) prow[c + e] = acc[j][e];
+    }
+  }
+}
+
+// which form runs: 2 = register-resident, 4 waves (V <= 8192, 16-B rows), 1 = register-resident, 16
+// waves (V <= 32768, 8-B rows), 0 = the LDS-accumulator kernel. DALLE_AMD_XENT_REG=0 forces the latter.
+static int g_xent_reg = -1;  // -1: DALLE_AMD_XENT_REG (default 1); xent_set_reg overrides (tests, A/B)
+void xent_set_reg(int v) { g_xent_reg = v; }
+static int xent_form(int V) {
+  if (g_xent_reg < 0) {
+    const char* e = getenv("DALLE_AMD_XENT_REG");
+    g_xent_reg = e ? atoi(e) : 1;
+  }
+  if (!g_xent_reg) return 0;
+  if (V % 8 == 0 && V <= 4 * 4 * 64 * 8) return 2;
+  if (V % 4 == 0 && V <= 8 * 16 * 64 * 4) return 1;
+  return 0;
+}
+
+long xent_colsum_blocks(long R, int V) {
+  const int form = xent_form(V);
+  if (form == 0) return (R + XENT_RB - 1) / XENT_RB;
+  const long cap = form == 2 ? 1024 : 512;  // 4 / 2 workgroups per CU; partial rows are 4 V bytes each
+  return R < cap ? R : cap;
+}
+
 bool xent_colsum(void* logits, const int64_t* labels, float* loss, float* part, long R, int V, float gscale, hipStream_t st) {
+  const int form = xent_form(V);
+  if (form == 2) {
+    hipLaunchKernelGGL((xent_reg_kernel<4, 4, 8>), dim3(xent_colsum_blocks(R, V)), dim3(256), 0, st, (__bf16*)logits, labels,
+                       loss, part, R, V, gscale);
+    return true;
+  }
+  if (form == 1) {
+    hipLaunchKernelGGL((xent_reg_kernel<8, 16, 4>), dim3(xent_colsum_blocks(R, V)), dim3(1024), 0, st, (__bf16*)logits, labels,
+                       loss, part, R, V, gscale);
+    return true;
+  }
   if (V > XENT_MAXV) return false;
   const long nblk = (R + XENT_RB - 1) / XENT_RB;
   const size_t lds = (size_t)(((xpad(V) + 3) & ~3) + 2 * (XENT_T / 64)) * sizeof(float);
@@ -211,7 +337,5 @@ bool xent_colsum(void* logits, const int64_t* labels, float* loss, float* part, 
   hipLaunchKernelGGL(xent_colsum_kernel, dim3(nblk), dim3(XENT_T), lds, st, (__bf16*)logits, labels, loss, part, R, V, gscale);
   return true;
 }
-
-long xent_colsum_blocks(long R) { return (R + XENT_RB - 1) / XENT_RB; }
 
 }  // namespace dalle

@@ -368,3 +368,39 @@ def test_transpose_cast_bf16_bitwise(cuda, shape):
     w = torch.randn(*shape, device=cuda) * 3.0
     got = C().transpose_bf16(w)
     assert torch.equal(got, w.bfloat16().t().contiguous())
+
+
+@pytest.mark.parametrize("V", [8192, 32356, 1064, 516, 1000])
+@pytest.mark.parametrize("reg", [1, 0])
+def test_xent_colsum(cuda, V, reg):
+    """Fused CE + in-place dlogits + bias-gradient column sums (both kernel forms: register-resident and
+    LDS accumulator) against fp32 PyTorch; the column sums are of the bf16 dlogits the GEMMs consume."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(6)
+    R = 2000
+    logits = (torch.randn(R, V, device=cuda) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, V, (R,), device=cuda)
+    ref_logits = logits.float().requires_grad_(True)
+    loss_ref = F.cross_entropy(ref_logits, labels, reduction="none")
+    (loss_ref.sum() * 0.25).backward()
+    buf = logits.clone()
+    db = torch.full((V,), 0.5, device=cuda)
+    try:
+        C.xent_set_reg(reg)
+        loss = C.xent_colsum_(buf, labels, 0.25, db)
+        torch.cuda.synchronize()
+    finally:
+        C.xent_set_reg(1)
+    assert torch.allclose(loss, loss_ref, atol=2e-3, rtol=1e-3)
+    assert _rel(buf, ref_logits.grad) < 1e-2
+    assert torch.allclose(db - 0.5, buf.float().sum(0), atol=1e-4, rtol=1e-4)  # += into the sink
+    buf2 = logits.clone()
+    db2 = torch.full((V,), 0.5, device=cuda)
+    C.xent_set_reg(reg)
+    try:
+        C.xent_colsum_(buf2, labels, 0.25, db2)
+    finally:
+        C.xent_set_reg(1)
+    assert torch.equal(buf2, buf) and torch.equal(db2, db)  # deterministic
