@@ -209,11 +209,12 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
     """Split-K factor for a weight-grad GEMM (N x K output, reduction over M tokens). Measured on
     MI355X at M = 61440 (profiles/r1_gemm_wgrad_m61440.jsonl, TF at 1/2/4/8 splits): 1024x1024
     405/533/687/834, 3072x1024 718/929/1009/984, 1024x4096 965/1007/1083/1032, 8192x1024
-    1077/1125/1114/1053."""
+    1077/1125/1114/1053; at M = 81920 (micro-batch 64, profiles/r3_wgrad_splits_m81920.txt) the same
+    choices win except 1024x1024, where 16 splits beat 8 (936 vs 904 TF)."""
     if SPLITK_WGRAD == 0:
         return 1
     nk = N * K
-    s = 8 if nk <= 1536 * 1024 else (4 if nk <= 4608 * 1024 else 2)
+    s = (16 if M >= 81920 else 8) if nk <= 1536 * 1024 else (4 if nk <= 4608 * 1024 else 2)
     while s > 1 and (M % s or M // s < 1024):
         s //= 2
     return s
