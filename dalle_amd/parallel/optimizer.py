@@ -362,6 +362,7 @@ class TrainingStateAverager:
         self._unapplied = False      # an update exists in the master copy but not in the model yet
         self._averaging_due = False  # the state-averaging round of the last delayed epoch has not run yet
         self._exact = False          # the gradient round of the pending epoch was exact
+        self._backup_buf: Optional[torch.Tensor] = None  # restore buffer of a failed round, allocated once
 
     def _inner_step(self):
         self.optimizer.step()
@@ -450,7 +451,10 @@ class TrainingStateAverager:
             logger.warning(f"replica parameters differ after an exact round (epoch {self.local_epoch}); averaging them")
         buf = self.arena.data if self.arena is not None else torch.cat([p.detach().reshape(-1).float() for p in self.params])
         segs = self.arena.segments() if self.arena is not None else _segments_of(self.params)
-        backup = buf.clone()
+        if self._backup_buf is None or self._backup_buf.shape != buf.shape or self._backup_buf.device != buf.device:
+            self._backup_buf = torch.empty_like(buf)
+        backup = self._backup_buf
+        backup.copy_(buf)
         deadline = Deadline(self.averaging_timeout)
         try:
             allreduce_weighted(buf, 1.0, self.group, self.compression, total_weight=float(world), segments=segs)
