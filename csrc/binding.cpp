@@ -49,6 +49,7 @@ void embed_fwd(const int64_t*, const int64_t*, const float*, float*, int*, int*,
                hipStream_t);
 bool xent_colsum(void*, const int64_t*, float*, float*, long, int, float, hipStream_t);
 void transpose_cast_bf16(const float* w, void* wt, int R, int C, hipStream_t st);
+void transpose_bf16(const void* x, void* xt, int R, int C, hipStream_t st);
 bool conv3x3(const ConvArgs&, hipStream_t);
 bool gn_stats(const void*, float*, float*, float*, int, int, int, float, hipStream_t);
 size_t gn_part_floats(int);
@@ -425,6 +426,16 @@ Tensor transpose_bf16(Tensor w) {
   auto wt = torch::empty({w.size(1), w.size(0)}, w.options().dtype(torch::kBFloat16));
   if (w.numel()) dalle::transpose_cast_bf16(w.data_ptr<float>(), wt.data_ptr(), (int)w.size(0), (int)w.size(1), cur_stream());
   return wt;
+}
+
+Tensor transpose_act_bf16(Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+              "transpose_act_bf16: contiguous bf16 matrix expected");
+  TORCH_CHECK(x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose_act_bf16: both dims must be multiples of 64");
+  TORCH_CHECK(x.size(0) < (1L << 31) && x.size(1) < (1L << 31), "transpose_act_bf16: matrix too large");
+  auto xt = torch::empty({x.size(1), x.size(0)}, x.options());
+  if (x.numel()) dalle::transpose_bf16(x.data_ptr(), xt.data_ptr(), (int)x.size(0), (int)x.size(1), cur_stream());
+  return xt;
 }
 
 void scale_residual_out(Tensor x, Tensor y, Tensor scale, Tensor out) {
@@ -1166,6 +1177,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_residual_", &scale_residual_);
   m.def("scale_residual_out", &scale_residual_out);
   m.def("transpose_bf16", &transpose_bf16, "fp32 (R, C) -> bf16 (C, R) in one pass");
+  m.def("transpose_act_bf16", &transpose_act_bf16, "bf16 (R, C) -> bf16 (C, R), 64 x 64 LDS tiles (R, C multiples of 64)");
   m.def("scale_residual_bwd", &scale_residual_bwd, py::arg("g"), py::arg("y"), py::arg("scale"),
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);

@@ -337,4 +337,40 @@ void transpose_cast_bf16(const float* w, void* wt, int R, int C, hipStream_t st)
   hipLaunchKernelGGL(transpose_cast_bf16_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, st, w, (__bf16*)wt, R, C);
 }
 
+// bf16 X (R x C) -> X^T (C x R): the token-contiguous copy of a saved GEMM input (hip_ops WGRAD_XT). The
+// weight-grad product g^T x runs 18-33 % faster on hipBLASLt when x arrives token-contiguous
+// (profiles/r3s5_wgrad_nt_vs_tn_m81920.txt), so the LN output is kept transposed for the backward.
+// 64 x 64 tiles through LDS (row stride 66 bf16: the column gathers spread over the banks); every global
+// access is a 16-byte vector, 8 lanes per 128-byte tile row.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ xt, int R,
+                                                             int C) {
+  __shared__ uint16_t tile[64][66];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int seg = threadIdx.x & 7, row = threadIdx.x >> 3;  // 8 x 16-byte segments per row, 32 rows per pass
+#pragma unroll
+  for (int k = 0; k < 64; k += 32) {
+    const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)(r0 + row + k) * C + c0 + 8 * seg);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      tile[row + k][8 * seg + 2 * i] = (uint16_t)(w[i] & 0xffffu);
+      tile[row + k][8 * seg + 2 * i + 1] = (uint16_t)(w[i] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 64; k += 32) {
+    const int c = row + k;  // output row (input column)
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (uint32_t)tile[8 * seg + 2 * i][c] | ((uint32_t)tile[8 * seg + 2 * i + 1][c] << 16);
+    *reinterpret_cast<uint4*>(xt + (size_t)(c0 + c) * R + r0 + 8 * seg) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
+void transpose_bf16(const void* x, void* xt, int R, int C, hipStream_t st) {
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)xt, R, C);
+}
+
 }  // namespace dalle

@@ -235,13 +235,73 @@ FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
 FUSED_GEGLU_DGRAD = int(os.environ.get("DALLE_AMD_FUSED_GEGLU_DGRAD", "1"))
 
 
-def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
+# weight-grad inputs kept token-contiguous: the LN outputs feeding the QKV and FF-in GEMMs are saved as
+# X^T (one bf16 transpose kernel, ~60 us per 168 MB) instead of X, and dW = g^T X runs on hipBLASLt with
+# a token-contiguous B operand: 3072x1024 1128 vs 847 TF/s, 8192x1024 1334 vs 1130 at M = 81920
+# (profiles/r3s5_wgrad_nt_vs_tn_m81920.txt). DALLE_AMD_WGRAD_XT=0 restores the token-major form.
+WGRAD_XT = int(os.environ.get("DALLE_AMD_WGRAD_XT", "1"))
+
+
+class XT:
+    """A saved GEMM input held transposed: ``t`` is X^T (K x M, contiguous bf16) of the logical X (M x K)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+    @property
+    def shape(self):
+        return (self.t.shape[1], self.t.shape[0])
+
+
+def saved_gemm_input(x2: torch.Tensor):
+    """``x2`` as the weight-grad GEMM will want it in the backward: ``XT`` when WGRAD_XT applies."""
+    if (WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.is_contiguous()
+            and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0):
+        _count("wgrad_xt")
+        return XT(C().transpose_act_bf16(x2))
+    return x2
+
+
+def wgrad_xt_splits(M: int, N: int, K: int) -> int:
+    """Split-K factor of the token-contiguous-X weight-grad form (measured at M = 81920, TF at 2/4/8/16
+    splits: 3072x1024 884/1050/1088/1128, 1024x1024 515/670/1000/1112, 8192x1024 1334/1309/1294/1222,
+    1024x4096 1208/1241/1209/1142)."""
+    nk = N * K
+    s = 16 if nk <= 3072 * 1024 else (4 if nk <= 4608 * 1024 else 2)
+    while s > 1 and (M % s or M // s < 1024):
+        s //= 2
+    return s
+
+
+def _weight_grad_xt(w, gw, fused: bool, g2: torch.Tensor, xt: torch.Tensor):
+    K, M = xt.shape
+    N = g2.shape[1]
+    s = wgrad_xt_splits(M, N, K)
+    if s > 1:
+        ms = M // s
+        out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
+        part = torch.bmm(g2.view(s, ms, N).transpose(1, 2), xt.view(K, s, ms).transpose(0, 1).transpose(1, 2),
+                         out_dtype=torch.float32)
+        C().splitk_accum_(out, part, fused)
+        return None if fused else out
+    if fused:
+        torch.addmm(gw, g2.t(), xt.t(), out_dtype=torch.float32, out=gw)
+        return None
+    return torch.mm(g2.t(), xt.t(), out_dtype=torch.float32)
+
+
+def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2):
     """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate into it
     and return None: no temporary dW and no autograd add kernel, and the shared blocks' grads (one per
     reusing layer) sum in fp32. Small outputs run as a split-K batched GEMM (fp32 partials) + one
-    deterministic fold kernel; large ones accumulate inside the GEMM (hipBLASLt beta = 1)."""
+    deterministic fold kernel; large ones accumulate inside the GEMM (hipBLASLt beta = 1). ``x2`` may be
+    an ``XT`` (token-contiguous X^T, see saved_gemm_input)."""
     gw = w.grad
     fused = FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape
+    if isinstance(x2, XT):
+        return _weight_grad_xt(w, gw, fused, g2, x2.t)
     M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
     if OWN_WGRAD and N % 256 == 0 and K % 256 == 0 and g2.is_contiguous() and x2.is_contiguous():
         # hand-written MN-major MFMA kernel; 15-20 % slower than hipBLASLt on the training shapes
@@ -598,6 +658,7 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None
+    h2 = saved_gemm_input(h2)  # the QKV weight grad's input, token-contiguous
     return y, s, (inp, mean, rstd, h2, wq, q, k, v, out, lse, y, wo, s, cos, sin, (B, n, T, S, K, H, pattern, shift, col))
 
 
@@ -641,6 +702,7 @@ def _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save: bool = T
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None
+    h2 = saved_gemm_input(h2)  # the FF-in weight grad's input, token-contiguous
     return y, s, (inp, mean, rstd, h2, w1b, a, u, w2b, y, s, meta)
 
 
