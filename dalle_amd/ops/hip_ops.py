@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import os
 import weakref
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -255,53 +255,73 @@ class XT:
         return (self.t.shape[1], self.t.shape[0])
 
 
-def saved_gemm_input(x2: torch.Tensor):
+# optionally the FF-out weight grad also takes its output grad token-contiguous (dy^T: one 62 us transpose;
+# the 1024x4096 product runs at 1265 vs 1106 TF/s in isolation) -- the full step measured neutral
+# (229.50 / 229.41 vs 229.54 / 229.63 ms, same box, profiles/r3s5_wgrad_xt_ab.txt), so off by default
+WGRAD_GT = int(os.environ.get("DALLE_AMD_WGRAD_GT", "0"))
+
+
+def saved_gemm_input(x2: torch.Tensor, enabled: Optional[bool] = None):
     """``x2`` as the weight-grad GEMM will want it in the backward: ``XT`` when WGRAD_XT applies."""
-    if (WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.is_contiguous()
+    if ((WGRAD_XT if enabled is None else enabled) and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.is_contiguous()
             and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0):
         _count("wgrad_xt")
         return XT(C().transpose_act_bf16(x2))
     return x2
 
 
-def wgrad_xt_splits(M: int, N: int, K: int) -> int:
-    """Split-K factor of the token-contiguous-X weight-grad form (measured at M = 81920, TF at 2/4/8/16
-    splits: 3072x1024 884/1050/1088/1128, 1024x1024 515/670/1000/1112, 8192x1024 1334/1309/1294/1222,
-    1024x4096 1208/1241/1209/1142)."""
+def wgrad_t_splits(M: int, N: int, K: int, form: str) -> int:
+    """Split-K factor of the token-contiguous weight-grad forms, measured at M = 81920 (TF/s at 2/4/8/16
+    splits, profiles/r3s5_wgrad_xt_ab.txt). ``xt`` (X^T given): 3072x1024 884/1050/1088/1128, 1024x1024
+    515/670/1000/1112, 8192x1024 1334/1309/1294/1222, 1024x4096 1208/1241/1209/1142. ``gt`` (G^T given):
+    3072x1024 884/1083/1108/1192, 1024x1024 535/664/942/1108, 8192x1024 1316/1283/1246/1195, 1024x4096
+    1232/1238/1265/1148. ``nt`` (both): 3072x1024 1140/1255/1239/1237, 8192x1024 1406/1416/1377/1288,
+    1024x4096 1285/1348/1365/1281."""
     nk = N * K
-    s = 16 if nk <= 3072 * 1024 else (4 if nk <= 4608 * 1024 else 2)
+    if form == "gt":
+        s = 16 if nk <= 3072 * 1024 else (8 if nk <= 4608 * 1024 else 2)
+    elif form == "nt":
+        s = 16 if nk <= 1536 * 1024 else (8 if nk <= 4608 * 1024 else 4)
+    else:
+        s = 16 if nk <= 3072 * 1024 else (4 if nk <= 4608 * 1024 else 2)
     while s > 1 and (M % s or M // s < 1024):
         s //= 2
     return s
 
 
-def _weight_grad_xt(w, gw, fused: bool, g2: torch.Tensor, xt: torch.Tensor):
-    K, M = xt.shape
-    N = g2.shape[1]
-    s = wgrad_xt_splits(M, N, K)
+def _weight_grad_t(gw, fused: bool, g2, x2):
+    """dW = g^T x with G and/or X given token-contiguous (XT): split-K batched hipBLASLt GEMM whose
+    operands are strided views of the transposed copies (no gather), fp32 partials + the fold kernel."""
+    gt = g2.t if isinstance(g2, XT) else None
+    xt = x2.t if isinstance(x2, XT) else None
+    M, N = g2.shape
+    K = x2.shape[1]
+    form = "nt" if (gt is not None and xt is not None) else ("gt" if gt is not None else "xt")
+    s = wgrad_t_splits(M, N, K, form)
+    ms = M // s
+    a = gt.view(N, s, ms).transpose(0, 1) if gt is not None else g2.view(s, ms, N).transpose(1, 2)
+    b = xt.view(K, s, ms).transpose(0, 1).transpose(1, 2) if xt is not None else x2.view(s, ms, K)
     if s > 1:
-        ms = M // s
-        out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
-        part = torch.bmm(g2.view(s, ms, N).transpose(1, 2), xt.view(K, s, ms).transpose(0, 1).transpose(1, 2),
-                         out_dtype=torch.float32)
+        out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=a.device)
+        part = torch.bmm(a, b, out_dtype=torch.float32)
         C().splitk_accum_(out, part, fused)
         return None if fused else out
     if fused:
-        torch.addmm(gw, g2.t(), xt.t(), out_dtype=torch.float32, out=gw)
+        torch.addmm(gw, a[0], b[0], out_dtype=torch.float32, out=gw)
         return None
-    return torch.mm(g2.t(), xt.t(), out_dtype=torch.float32)
+    return torch.mm(a[0], b[0], out_dtype=torch.float32)
 
 
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2):
     """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate into it
     and return None: no temporary dW and no autograd add kernel, and the shared blocks' grads (one per
     reusing layer) sum in fp32. Small outputs run as a split-K batched GEMM (fp32 partials) + one
-    deterministic fold kernel; large ones accumulate inside the GEMM (hipBLASLt beta = 1). ``x2`` may be
-    an ``XT`` (token-contiguous X^T, see saved_gemm_input)."""
+    deterministic fold kernel; large ones accumulate inside the GEMM (hipBLASLt beta = 1). ``x2`` and / or
+    ``g2`` may be an ``XT`` (token-contiguous transposed copy, see saved_gemm_input)."""
     gw = w.grad
     fused = FUSE_WGRAD and gw is not None and gw.dtype == torch.float32 and gw.is_contiguous() and gw.shape == w.shape
-    if isinstance(x2, XT):
-        return _weight_grad_xt(w, gw, fused, g2, x2.t)
+    if isinstance(x2, XT) or isinstance(g2, XT):
+        return _weight_grad_t(gw, fused, g2, x2)
     M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
     if OWN_WGRAD and N % 256 == 0 and K % 256 == 0 and g2.is_contiguous() and x2.is_contiguous():
         # hand-written MN-major MFMA kernel; 15-20 % slower than hipBLASLt on the training shapes
@@ -716,7 +736,7 @@ def _ff_core_bwd(saved, params, dy, sk):
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
         da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
         _count("ff_dgrad_geglu")
-        dw2 = _wgrad(w2, dy, u)
+        dw2 = _wgrad(w2, saved_gemm_input(dy, WGRAD_GT), u)
     else:
         du = input_grad(dy, w2)
         dw2 = _wgrad(w2, dy, u)

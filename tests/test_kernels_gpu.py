@@ -421,9 +421,11 @@ def test_transpose_act_bf16(cuda, R, Cc):
 
 @pytest.mark.parametrize("M,N,K", [(81920 // 16, 3072, 1024), (20480, 8192, 1024), (2048, 1024, 4096), (512, 256, 128)])
 @pytest.mark.parametrize("fused", [True, False])
-def test_weight_grad_token_contiguous_input(cuda, M, N, K, fused):
-    """dW = g^T x from a saved XT input (split-K over token-contiguous x^T, fp32 partials + fold) matches the
-    fp32 reference, accumulating into an existing fp32 grad (the arena) or returning a fresh one."""
+@pytest.mark.parametrize("form", ["xt", "gt", "nt"])
+def test_weight_grad_token_contiguous_input(cuda, M, N, K, fused, form):
+    """dW = g^T x with x and / or g given as token-contiguous XT copies (split-K over strided views, fp32
+    partials + fold) matches the fp32 reference, accumulating into an existing fp32 grad (the arena) or
+    returning a fresh one."""
     from dalle_amd.ops import hip_ops
 
     torch.manual_seed(0)
@@ -433,9 +435,10 @@ def test_weight_grad_token_contiguous_input(cuda, M, N, K, fused):
     base = torch.randn(N, K, device=cuda)
     if fused:
         w.grad = base.clone()
-    sx = hip_ops.saved_gemm_input(x)
-    assert isinstance(sx, hip_ops.XT) and sx.shape == (M, K)
-    r = hip_ops.weight_grad(w, g, sx)
+    sx = hip_ops.saved_gemm_input(x, True) if form != "gt" else x
+    sg = hip_ops.saved_gemm_input(g, True) if form != "xt" else g
+    assert isinstance(sx, hip_ops.XT) == (form != "gt") and sx.shape == (M, K) and sg.shape == (M, N)
+    r = hip_ops.weight_grad(w, sg, sx)
     want = g.float().t() @ x.float() + (base if fused else 0)
     got = w.grad if fused else r
     assert (r is None) == fused
