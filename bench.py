@@ -59,10 +59,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 64)),
-                    help="per-GPU micro-batch (64: 95 GB of 288; same box, samples/s: B48 259.7, B64 264.9, B80 258.5, "
-                         "B96 263.8, B128 267.8 -- multiples of 64 keep every GEMM / attention grid a whole number of "
-                         "waves; profiles/r3_batch_sweep.txt)")
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 128)),
+                    help="per-GPU micro-batch (128: 187 GB of 288; with the token-contiguous weight-grad inputs B128 "
+                         "beats B64 on the same box, 280.7/279.2/280.6 vs 275.1/276.8/275.8 samples/s, "
+                         "profiles/r3s5_batch_ab.txt; earlier sweep: B48 259.7, B64 264.9, B80 258.5, B96 263.8, "
+                         "B128 267.8, profiles/r3_batch_sweep.txt -- multiples of 64 keep every GEMM / attention grid a "
+                         "whole number of waves)")
     ap.add_argument("--model", default="bench24")
     ap.add_argument("--engine", default="step", choices=["step", "collab"],
                     help="step: model + GradSync + fused LAMB; collab: the CollaborativeOptimizer.step() loop")
