@@ -255,10 +255,11 @@ class XT:
         return (self.t.shape[1], self.t.shape[0])
 
 
-# optionally the FF-out weight grad also takes its output grad token-contiguous (dy^T: one 62 us transpose;
-# the 1024x4096 product runs at 1265 vs 1106 TF/s in isolation) -- the full step measured neutral
-# (229.50 / 229.41 vs 229.54 / 229.63 ms, same box, profiles/r3s5_wgrad_xt_ab.txt), so off by default
-WGRAD_GT = int(os.environ.get("DALLE_AMD_WGRAD_GT", "0"))
+# the FF-out weight grad also takes its output grad token-contiguous (dy^T: one transient transpose, 54-62 us
+# per 168 MB; the 1024x4096 product runs at 1265 vs 1106 TF/s in isolation): small but consistent in the full
+# step -- micro-batch 64 229.50 / 229.41 vs 229.54 / 229.63 ms, micro-batch 128 459.41 / 458.95 vs 460.09 /
+# 461.66 ms (same box each, profiles/r3s5_wgrad_xt_ab.txt)
+WGRAD_GT = int(os.environ.get("DALLE_AMD_WGRAD_GT", "1"))
 
 
 def saved_gemm_input(x2: torch.Tensor, enabled: Optional[bool] = None):
