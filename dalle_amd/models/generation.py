@@ -521,114 +521,6 @@ class SplitDecodeEngine:
             p.prefill_parallel(text_bos[i * b:(i + 1) * b])
 
     def _capture(self):
-        """Capture one image step into a hipGraph (warm-up on a side stream as torch requires)."""
-        if self.graph is not None and self._graph_cfg == (self.temperature, self.top_k, self.top_p):
-            return
-        # warm-up on a side stream (allocator / library handles), then capture; the caller resets the
-        # state (pos, tokens, caches) afterwards, so the warm-up steps leave no trace
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._step()
-        torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with _CAPTURE_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self._static_logits = self._step()
-        self.graph = g
-        self._graph_cfg = (self.temperature, self.top_k, self.top_p)
-
-    @torch.no_grad()
-    def teacher_forced_logits(self, text_bos: torch.Tensor, image: torch.Tensor) -> torch.Tensor:
-        """Image-vocab logits at every position >= T-1 when feeding the given image codes (tests)."""
-        self.prefill(text_bos)
-        outs = []
-        for i in range(self.cfg.image_seq_len):
-            outs.append(self._forward_position())
-            if i + 1 < self.cfg.image_seq_len:
-                self.tok.copy_(image[:, i] + self.Vt)
-                self.pos.add_(1)
-        return torch.stack(outs, dim=1)
-
-
-class SplitDecodeEngine:
-    """The batch split into ``parts`` independent :class:`DecodeEngine` s whose steps run on separate
-    HIP streams inside ONE captured graph. At batch 64 a decode step is a chain of short kernels
-    whose time is mostly fixed latency (a skinny GEMM takes 8-10 us whether it streams 2 or 16 MB of
-    weights), so two half-batch chains interleaved on the GPU overlap one chain's latency with the
-    other's work. The parts share the bf16 weight copies; each has its own KV caches, LN histories,
-    device position and sampler seed (``seed + part``), so the parts never touch the same buffer."""
-
-    def __init__(self, model, batch_size: int, device=None, parts: int = 2):
-        if batch_size % parts:
-            raise ValueError(f"batch {batch_size} is not divisible into {parts} parts")
-        self.model, self.B, self.nparts = model, batch_size, parts
-        self.parts = [DecodeEngine(model, batch_size // parts, device=device) for _ in range(parts)]
-        for p in self.parts[1:]:
-            p._w = self.parts[0]._w  # one bf16 copy of every weight, refreshed by part 0 only
-            p._refresh_weights = False
-        self.device = self.parts[0].device
-        self.use_hip = self.parts[0].use_hip
-        self.graph = None
-        self._graph_cfg = None
-
-    @property
-    def codes(self) -> torch.Tensor:
-        return torch.cat([p.codes for p in self.parts])
-
-    def _start_all(self, text_bos: torch.Tensor):
-        b = self.B // self.nparts
-        for i, p in enumerate(self.parts):
-            p._start(text_bos[i * b:(i + 1) * b])
-
-    _start = _start_all
-
-    def _step(self):
-        for p in self.parts:
-            p._step()
-
-    _image_step = _step
-
-    @torch.no_grad()
-    def prefill(self, text_bos: torch.Tensor):
-        b = self.B // self.nparts
-        for i, p in enumerate(self.parts):
-            p.prefill(text_bos[i * b:(i + 1) * b])
-
-    @torch.no_grad()
-    def prefill_parallel(self, text_bos: torch.Tensor):
-        b = self.B // self.nparts
-        for i, p in enumerate(self.parts):
-            p.prefill_parallel(text_bos[i * b:(i + 1) * b])
-
-    # DALLE_AMD_DECODE_GRAPHS=joint (default): one graph, the parts as parallel branches joined at the end of
-    # every step; "per-part": one graph per part, each replayed on its own stream with no per-step join
-    # (the parts share nothing but read-only weights), so one part's step never waits for the other's
-    graph_mode = os.environ.get("DALLE_AMD_DECODE_GRAPHS", "joint")
-
-    def _capture_per_part(self):
-        cfg = (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p)
-        if getattr(self, "_graphs", None) is not None and self._graph_cfg == cfg:
-            return
-        main = torch.cuda.current_stream()
-        warm = torch.cuda.Stream()
-        warm.wait_stream(main)
-        with torch.cuda.stream(warm):
-            for _ in range(2):
-                for p in self.parts:
-                    p._step()
-        main.wait_stream(warm)
-        graphs = []
-        for p in self.parts:
-            g = torch.cuda.CUDAGraph()
-            with _CAPTURE_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
-                p._step()
-            graphs.append(g)
-        self._graphs = graphs
-        self._part_streams = [torch.cuda.Stream() for _ in self.parts]
-        self._graph_cfg = cfg
-
-    def _capture(self):
         if self.graph is not None and self._graph_cfg == (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p):
             return
         main = torch.cuda.current_stream()

@@ -82,6 +82,12 @@ class GradSync:
         if self.world_size <= 1:
             return
         rs = sorted(self._range[id(p)] for p in params if id(p) in self._range)
+        for o, n in rs:
+            if any(o < e and s < o + n for s, e in self._sent):
+                # a second hooked backward before all_reduce(): its grads would be summed across peers
+                # twice and accumulate into buffers whose collective is still in flight
+                raise RuntimeError("GradSync: a gradient range was handed over twice in one step -- one backward() "
+                                   "per all_reduce() while attached (disable the overlap for gradient accumulation)")
         merged = []
         for o, n in rs:
             if merged and o <= merged[-1][1]:

@@ -193,9 +193,14 @@ class ElasticGroup:
         self.regroups += 1
         self.join()
 
+    def join_requested(self) -> bool:
+        """Local view of the join flag (one store round trip, no collective)."""
+        return bool(self.store.check(["elastic/join_pending"]))
+
     def poll_join(self) -> bool:
-        """Collective: True (on every member) if a peer asked to join; the caller then regroups."""
-        local = 1.0 if self.store.check(["elastic/join_pending"]) else 0.0
+        """Collective: True (on every member) if a peer asked to join; the caller then regroups. The
+        collaborative optimizer folds this flag into its round-opening all-gather instead where it has one."""
+        local = 1.0 if self.join_requested() else 0.0
         flag = torch.tensor([local], device=self.device)
         self.guarded(lambda: dist.all_reduce(flag, op=dist.ReduceOp.MAX, async_op=True))
         return bool(flag.item() > 0)

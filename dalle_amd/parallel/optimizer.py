@@ -573,6 +573,10 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                                                     check_every=state_check_every)
         self.detached = False
         self.overlap_grad_averaging = overlap_grad_averaging
+        # backward() calls per .step() (a trainer's gradient_accumulation_steps): the backward-overlapped
+        # all-reduce needs exactly one, since the hook fires in every hooked backward
+        self.backwards_per_step = 1
+        self._join_seen: Optional[bool] = None
         self._last_bs = int(batch_size_per_step or 0)
         if self._last_bs:
             self._arm_next(self._last_bs)  # the very first micro-step may already close epoch 0
@@ -644,11 +648,21 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         finally:
             self._arm_next(bs)
 
+    def set_backwards_per_step(self, n: int):
+        """Declare the number of backward() calls per .step() (gradient accumulation); anything but one
+        disables the backward-overlapped all-reduce, which the hook would otherwise launch per backward."""
+        self.backwards_per_step = max(1, int(n))
+        if self.backwards_per_step != 1:
+            self.grad_averager.disarm()
+        elif self._last_bs:
+            self._arm_next(self._last_bs)
+
     def _arm_next(self, bs: int):
         """Static homogeneous tracker: the next micro-step closes the epoch exactly when (accumulated +
         bs) * world >= target -- then its backward launches the round's all-reduce (GradientAverager.arm)."""
         ga = self.grad_averager
-        if self.tracker.mode != "static" or self.detached or not self.overlap_grad_averaging:
+        if self.tracker.mode != "static" or self.detached or not self.overlap_grad_averaging \
+                or int(getattr(self, "backwards_per_step", 1)) != 1:
             ga.disarm()
             return
         world = _group_world(self.group)[0]
@@ -728,13 +742,17 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         identical on every rank, so the weighting and the resync decision are collective."""
         world, _ = (1, 0) if self.detached else _group_world(self.group)
         s = float(self.grad_averager.local_samples_accumulated)
+        self._join_seen = None
         if world == 1 or self.tracker.mode not in ("store", "dht"):
             gp = self.tracker.global_progress
             total = gp.samples_accumulated if world > 1 else s
             return total, self.local_epoch, self.local_epoch, max(1, gp.num_peers if world > 1 else 1)
         dt = torch.float64 if self.device.type == "cpu" else torch.float32
-        mine = torch.tensor([s, float(self.local_epoch)], dtype=dt, device=self.device)
-        out = torch.empty(world * 2, dtype=dt, device=self.device)
+        # the third field is this peer's view of the elastic join flag: the round's one all-gather
+        # replaces a separate per-round join poll (an all-reduce + host sync)
+        join = 1.0 if (self.elastic is not None and self.elastic.join_requested()) else 0.0
+        mine = torch.tensor([s, float(self.local_epoch), join], dtype=dt, device=self.device)
+        out = torch.empty(world * 3, dtype=dt, device=self.device)
         deadline = Deadline(self.averaging_timeout)
         if self.device.type == "cuda":
             dist.all_gather_into_tensor(out, mine, group=self.group)
@@ -742,9 +760,10 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         else:
             work = dist.all_gather(list(out.chunk(world)), mine, group=self.group, async_op=True)
             work.wait(timeout=__import__("datetime").timedelta(seconds=max(1.0, deadline.remaining())))
-        v = out.view(world, 2).tolist()
+        v = out.view(world, 3).tolist()
         total = sum(r[0] for r in v)
         epochs = [int(round(r[1])) for r in v]
+        self._join_seen = any(r[2] > 0 for r in v)
         return total, min(epochs), max(epochs), world
 
     def _update_global_epoch(self, grad_scaler=None):
@@ -758,9 +777,15 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
             self.grad_averager.reset_accumulated_grads_()
             self.tracker.update_epoch(self.local_epoch)
             return
+        averaged = None
         if grad_scaler is not None and grad_scaler.is_enabled():
             # deferred AMP unscale + collaboration-wide overflow check (D28): skip the whole update
             # (and the averaging round) if any peer's accumulated grads overflowed
+            if self.grad_averager._armed:
+                # the last backward already launched this round's all-reduce on the (scaled) arena grads:
+                # RCCL is still reading and writing them, so finish the round first and unscale the
+                # averaged grads (unscaling is linear; an overflow on any peer is non-finite in the sum)
+                averaged = self.grad_averager.step(total_samples=total, epoch=self.local_epoch, batch_size=self._last_bs)
             flat = self.arena.grad if (self.arena is not None and self.grad_averager.reuse_grad_buffers) else None
             if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group):
                 logger.warning(f"{self.run_id}: non-finite scaled gradients at epoch {self.local_epoch}; skipping update")
@@ -769,7 +794,8 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 self.local_epoch = max_epoch + 1
                 self.tracker.update_epoch(self.local_epoch)
                 return
-        ok = self.grad_averager.step(total_samples=total, epoch=self.local_epoch, batch_size=self._last_bs)
+        ok = averaged if averaged is not None else \
+            self.grad_averager.step(total_samples=total, epoch=self.local_epoch, batch_size=self._last_bs)
         exact = ok and self.grad_averager.last_round_exact and min_epoch == max_epoch
         self.state_averager.step(optimizer_step=True, averaging_round=True, exact=exact)
         if self.local_epoch < max_epoch + 1:  # a peer one epoch behind catches up on the count
@@ -787,7 +813,7 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         # step(), finished peers from leave()), so the poll's all-reduce always matches; a failed round
         # regroups anyway -- never poll over a broken communicator
         if self.elastic is not None and not self._comm_failed() and self.grad_averager.last_averaging_ok \
-                and self.elastic.poll_join():
+                and (self._join_seen if self._join_seen is not None else self.elastic.poll_join()):
             logger.info(f"{self.run_id}: a peer asked to join; regrouping at epoch {self.local_epoch}")
             self._regroup()
 

@@ -192,6 +192,8 @@ class CollaborativeHFTrainer:
         args = self.args
         dev = self._device()
         accum = max(1, int(args.gradient_accumulation_steps))
+        if hasattr(self.collaborative_optimizer, "set_backwards_per_step"):
+            self.collaborative_optimizer.set_backwards_per_step(accum)
         self._call("on_train_begin")
         loader = iter(self.get_train_dataloader())
         max_steps = int(args.max_steps)
