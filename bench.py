@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--optim-bits", type=int, default=None, choices=[8, 32],
                     help="LAMB moment storage (default: 32 for --engine step, 8 = the reference's CPULAMB8Bit for collab)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--allreduce-algo", default=os.environ.get("DALLE_AMD_ALLREDUCE_ALGO", "rccl"), choices=["rccl", "rs_ag"],
+                    help="gradient all-reduce: one RCCL all_reduce per 64 MB bucket, or reduce-scatter + all-gather "
+                         "per bucket (the explicit direct-mesh form, average fused into the reduce-scatter)")
     ap.add_argument("--compression", default="none", choices=["none", "powersgd", "uniform8bit"],
                     help="gradient averaging: plain bucketed all-reduce, PowerSGD rank-4 with error feedback "
                          "(BASELINE config 3) or the hivemind size-adaptive fp16 / uniform-8-bit butterfly")
@@ -237,7 +240,7 @@ def run_rank(args) -> None:
         zero = None  # the collaborative optimizer resets the accumulated grads after each global step
     else:
         opt = _lamb(groups, bits, arena=arena)
-        sync_grads = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype)
+        sync_grads = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype, algo=args.allreduce_algo)
         if args.compression == "powersgd":
             # compression work runs at every world size (the all-reduces are skipped only when world == 1)
             from dalle_amd.parallel.powersgd import PowerSGD
@@ -333,7 +336,8 @@ def run_rank(args) -> None:
         t_all = [None] * world
         dist.all_gather_object(t_all, t_ar)
         t_ar = max(t_all)
-        comm_stats = {"bytes_per_step": int(step_bytes), "standalone_ms": round(t_ar * 1e3, 3),
+        comm_stats = {"algo": args.allreduce_algo, "buckets": comm.bucket_busbw(),
+                      "bytes_per_step": int(step_bytes), "standalone_ms": round(t_ar * 1e3, 3),
                       "busbw_GBps": round(2 * (world - 1) / world * step_bytes / t_ar / 1e9, 1),
                       "exposed_ms_per_step": None if exposed is None else round(exposed, 3),
                       "overlapped_frac": overlapped}
@@ -380,7 +384,8 @@ def run_rank(args) -> None:
                        "unique_params": cfg.unique_param_count(),
                        "engine": "CollaborativeOptimizer.step" if args.engine == "collab" else "GradSync + fused LAMB",
                        "optimizer": f"LAMB ({bits}-bit moments) + global clip 4.0",
-                       "grad_allreduce_dtype": args.grad_dtype, "gemm_selection": tuning,
+                       "grad_allreduce_dtype": args.grad_dtype, "grad_allreduce_algo": args.allreduce_algo,
+                       "gemm_selection": tuning,
                        "reversible": ({True: "recompute", False: "stored activations"}.get(cfg.reversible_recompute, "auto: stored while HBM allows")
                                       if cfg.reversible else "no"),
                        "grad_compression": args.compression if args.compression != "powersgd"

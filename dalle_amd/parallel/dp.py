@@ -17,6 +17,12 @@ what is left (tied embedding / head, final LayerNorm) and waits. In the bench24 
 backward; in an unshared model almost everything overlaps. Requires one ``all_reduce()`` per
 ``backward()`` (no local accumulation across micro-batches while attached).
 
+``algo``: ``"rccl"`` runs one ``all_reduce`` per bucket (RCCL picks ring / tree over the xGMI mesh);
+``"rs_ag"`` runs the direct mesh form of SURVEY §5.8 explicitly -- per bucket a ``reduce_scatter_tensor``
+(each rank reduces 1/N of the bucket, with the 1/N average fused into the reduction as RCCL's ``AVG`` op
+where it applies) followed by an ``all_gather_into_tensor`` of the reduced shards. Every rank then holds
+the SAME bits for every element (each shard is reduced once, by one rank).
+
 ``grad_dtype='bf16'`` halves the bytes on the wire (RCCL then reduces in bf16, so the averaged gradient
 carries bf16 rounding -- use for large worlds only).
 """
@@ -32,7 +38,10 @@ DEFAULT_BUCKET_BYTES = 64 * 1024 * 1024
 
 class GradSync:
     def __init__(self, arena: FlatArena, world_size: int = 1, group=None, grad_dtype: str = "fp32",
-                 bucket_bytes: int = DEFAULT_BUCKET_BYTES, average: bool = True):
+                 bucket_bytes: int = DEFAULT_BUCKET_BYTES, average: bool = True, algo: str = "rccl"):
+        if algo not in ("rccl", "rs_ag"):
+            raise ValueError(f"unknown all-reduce algorithm {algo!r} (rccl | rs_ag)")
+        self.algo = algo
         self.arena = arena
         self.world_size = world_size
         self.group = group
@@ -52,6 +61,9 @@ class GradSync:
         self.bytes_reduced = 0     # bytes all-reduced since the last reset_stats()
         self._exposed = []         # (start, end) device events around the post-backward wait (timing on)
         self.timing = False
+        self._pending_ag = []      # rs_ag without a fused average: (work, slice, shard) awaiting scale + gather
+        self._keep = []            # rs_ag on RCCL: shards alive until their gathers complete
+        self._fallback_ranges = []  # rs_ag: buckets that went through a plain all_reduce (length % world)
 
     # -------------------------------------------------------------------- overlap with backward
     def attach(self):
@@ -73,8 +85,69 @@ class GradSync:
     def _launch(self, s: int, e: int):
         g = self.arena.grad
         for b in range(s, e, self.bucket_elems):
-            self._works.append(dist.all_reduce(g[b:min(e, b + self.bucket_elems)], group=self.group, async_op=True))
+            sl = g[b:min(e, b + self.bucket_elems)]
+            if self.algo == "rs_ag" and sl.numel() % self.world_size == 0:
+                self._launch_rs_ag(sl)
+            else:
+                if self.algo == "rs_ag":
+                    self._fallback_ranges.append((b, b + sl.numel()))
+                self._works.append(dist.all_reduce(sl, group=self.group, async_op=True))
         self._sent.append((s, e))
+
+    def _launch_rs_ag(self, sl: torch.Tensor):
+        """Reduce-scatter the bucket into this rank's shard, then all-gather the reduced shards back into
+        the bucket. On RCCL both are queued at once (one communicator stream orders them) and the 1/N
+        average rides in the reduce-scatter (ReduceOp.AVG); elsewhere the gather waits for the reduction."""
+        n = sl.numel() // self.world_size
+        shard = torch.empty(n, dtype=sl.dtype, device=sl.device)
+        avg = self.average and sl.is_cuda and dist.get_backend(self.group) == "nccl"
+        w = dist.reduce_scatter_tensor(shard, sl, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=self.group,
+                                       async_op=True)
+        if sl.is_cuda and dist.get_backend(self.group) == "nccl":
+            self._works.append(w)
+            self._works.append(dist.all_gather_into_tensor(sl, shard, group=self.group, async_op=True))
+            self._keep.append(shard)
+        else:
+            self._pending_ag.append((w, sl, shard))
+
+    def _finish_rs_ag(self):
+        for w, sl, shard in self._pending_ag:
+            w.wait()
+            if self.average:
+                shard.mul_(1.0 / self.world_size)
+            self._works.append(dist.all_gather_into_tensor(sl, shard, group=self.group, async_op=True))
+        self._pending_ag = []
+
+    @torch.no_grad()
+    def bucket_busbw(self, reps: int = 3):
+        """Every bucket's collective alone under the configured algorithm (the arena grads are restored
+        afterwards): ``[{"mb", "ms", "busbw_GBps"}]``, bus bandwidth as nccl-tests reports it."""
+        import time
+
+        g = self.arena.grad
+        saved = g.clone()
+        out = []
+        sync = torch.cuda.synchronize if g.is_cuda else (lambda: None)
+        for s, e in self.buckets:
+            sync()
+            dist.barrier(group=self.group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                self._launch(s, e)
+                self._finish_rs_ag()
+                for w in self._works:
+                    w.wait()
+                self._works, self._sent, self._keep, self._fallback_ranges = [], [], [], []
+            sync()
+            t = (time.perf_counter() - t0) / reps
+            ts = [None] * self.world_size
+            dist.all_gather_object(ts, t, group=self.group)
+            t = max(ts)
+            nbytes = (e - s) * g.element_size()
+            out.append({"mb": round(nbytes / 2 ** 20, 1), "ms": round(t * 1e3, 3),
+                        "busbw_GBps": round(2 * (self.world_size - 1) / self.world_size * nbytes / t / 1e9, 1)})
+        g.copy_(saved)
+        return out
 
     @torch.no_grad()
     def notify(self, params):
@@ -144,13 +217,24 @@ class GradSync:
         else:
             for s, e in self._remaining():
                 self._launch(s, e)
+            self._finish_rs_ag()
             for w in self._works:
                 w.wait()
-            self._works, self._sent = [], []
+            self._works, self._sent, self._keep = [], [], []
             self.last_early_elems, self.early_elems = self.early_elems, 0
         if ev0 is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self._exposed.append((ev0, ev1))
         if self.average:
-            g.mul_(1.0 / self.world_size)
+            if self.algo == "rs_ag" and self.grad_dtype == "fp32":
+                # buckets that went through rs_ag are averaged already; all_reduce fallbacks (a bucket whose
+                # length is not a multiple of the world) still need the scale
+                self._scale_fallbacks(g)
+            else:
+                g.mul_(1.0 / self.world_size)
+
+    def _scale_fallbacks(self, g):
+        for b0, b1 in self._fallback_ranges:
+            g[b0:b1].mul_(1.0 / self.world_size)
+        self._fallback_ranges = []

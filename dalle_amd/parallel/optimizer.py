@@ -869,20 +869,35 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         else:
             for p in self._params:
                 dist.broadcast(p.data, src=donor_global, group=self.group)
-        objs = [self.state_dict() if rank == donor else None]
-        # optimizer state is small relative to params for the 8-bit path; ship it as an object
-        if dev.type == "cuda":
-            objs_cpu = [_to_cpu(objs[0]) if rank == donor else None]
-            dist.broadcast_object_list(objs_cpu, src=donor_global, group=self.group, device=dev)
-            objs = objs_cpu
-        else:
-            dist.broadcast_object_list(objs, src=donor_global, group=self.group)
-        sched = [self.scheduler.state_dict() if (rank == donor and self.scheduler is not None) else None]
-        dist.broadcast_object_list(sched, src=donor_global, group=self.group, device=dev if dev.type == "cuda" else None)
+        # optimizer + scheduler state: only the skeleton (scalars, hyper-parameters, tensor shapes / dtypes)
+        # goes through pickle; the state tensors (8-bit moments, absmax, fp32 moments) are packed into one
+        # flat buffer per dtype and broadcast as tensors on the group (RCCL over xGMI on the GPU)
+        sd = self.state_dict() if rank == donor else None
+        tensors: List[torch.Tensor] = []
+        meta = [(_strip_tensors(sd, tensors), self.scheduler.state_dict() if self.scheduler is not None else None)
+                if rank == donor else None]
+        dist.broadcast_object_list(meta, src=donor_global, group=self.group, device=dev if dev.type == "cuda" else None)
+        skeleton, sched = meta[0]
+        specs = _tensor_specs(skeleton)
+        for dtype in sorted({sp[1] for sp in specs}, key=str):
+            idx = [i for i, sp in enumerate(specs) if sp[1] == dtype]
+            total = sum(specs[i][2] for i in idx)
+            if rank == donor:
+                flat = torch.cat([tensors[i].detach().reshape(-1).to(dev) for i in idx]) if idx else None
+            else:
+                flat = torch.empty(total, dtype=dtype, device=dev)
+            dist.broadcast(flat, src=donor_global, group=self.group)
+            if rank != donor:
+                off = 0
+                for i in idx:
+                    n = specs[i][2]
+                    tensors.append((i, flat[off:off + n].view(specs[i][0])))
+                    off += n
         if rank != donor:
-            self.load_state_dict(objs[0])
-            if self.scheduler is not None and sched[0] is not None:
-                self.scheduler.load_state_dict(sched[0])
+            by_id = dict(tensors)
+            self.load_state_dict(_fill_tensors(skeleton, by_id))
+            if self.scheduler is not None and sched is not None:
+                self.scheduler.load_state_dict(sched)
         self.tracker.update_epoch(self.local_epoch)
         return rank != donor
 
@@ -920,6 +935,51 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
     def shutdown(self):
         self.apply_pending()
         self.tracker.shutdown()
+
+
+class _TensorSlot:
+    """Placeholder for a state tensor in the pickled skeleton of a state transfer."""
+
+    def __init__(self, idx: int, shape, dtype):
+        self.idx, self.shape, self.dtype = idx, tuple(shape), dtype
+
+
+def _strip_tensors(obj, out: list):
+    if torch.is_tensor(obj):
+        out.append(obj)
+        return _TensorSlot(len(out) - 1, obj.shape, obj.dtype)
+    if isinstance(obj, dict):
+        return {k: _strip_tensors(v, out) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_strip_tensors(v, out) for v in obj)
+    return obj
+
+
+def _tensor_specs(obj, acc=None):
+    """(shape, dtype, numel) of every slot, indexed by slot id."""
+    acc = {} if acc is None else acc
+    if isinstance(obj, _TensorSlot):
+        n = 1
+        for d in obj.shape:
+            n *= d
+        acc[obj.idx] = (obj.shape, obj.dtype, n)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _tensor_specs(v, acc)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _tensor_specs(v, acc)
+    return [acc[i] for i in range(len(acc))]
+
+
+def _fill_tensors(obj, by_id: dict):
+    if isinstance(obj, _TensorSlot):
+        return by_id[obj.idx]
+    if isinstance(obj, dict):
+        return {k: _fill_tensors(v, by_id) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_fill_tensors(v, by_id) for v in obj)
+    return obj
 
 
 def _to_cpu(obj):

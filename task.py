@@ -150,13 +150,12 @@ class TrainingTask:
             host_maddrs = list(self.peer_args.host_maddrs)
             rank = int(os.environ.get("RANK", "0"))
             if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not initial_peers:
-                # torchrun job without an external store: rank 0 hosts it next to the rendezvous port
-                addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-                port = int(os.environ.get("MASTER_PORT", "29500")) + 1
-                if rank == 0:
-                    host_maddrs = [f"/ip4/{addr if addr != 'localhost' else '127.0.0.1'}/tcp/{port}"]
-                else:
-                    initial_peers = [f"/ip4/{addr if addr != 'localhost' else '127.0.0.1'}/tcp/{port}"]
+                # torchrun job without an external store: rank 0 starts one that lives as long as the torchrun
+                # agent, so the metrics outlive a dead rank 0 (dalle_amd/parallel/dht_host.py)
+                from dalle_amd.parallel.dht_host import torchrun_endpoints
+
+                initial_peers, hm = torchrun_endpoints(rank)
+                host_maddrs = hm or host_maddrs
             self._dht = DHT(
                 start=True,
                 initial_peers=initial_peers,

@@ -44,6 +44,33 @@ def test_bench_spawns_n_ranks(tmp_path, engine):
         assert res["collab_backward_overlapped_rounds"] >= 3
 
 
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_allreduce_algorithms(tmp_path, n):
+    """--allreduce-algo rs_ag (bucketed reduce-scatter + all-gather) against the plain all_reduce: every
+    rank bitwise identical under both; at 2 ranks the two algorithms agree bitwise (one add per element),
+    at 4 to rounding (a different reduction order); the JSON names the algorithm and prices every bucket."""
+    outs = {}
+    for algo in ("rccl", "rs_ag"):
+        d = tmp_path / algo
+        d.mkdir()
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+        env.update(BENCH_BACKEND="gloo", BENCH_DUMP_PARAMS=str(d / "params"), HIP_VISIBLE_DEVICES="")
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1",
+                              "--model", "tiny", "--batch", "2", "--allreduce-algo", algo], env=env, cwd=str(d),
+                             capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-3000:]
+        res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+        assert res["config"]["grad_allreduce_algo"] == algo and res["grad_allreduce"]["algo"] == algo
+        assert res["grad_allreduce"]["buckets"] and all(b["busbw_GBps"] > 0 for b in res["grad_allreduce"]["buckets"])
+        ps = [torch.load(d / f"params.rank{r}.pt", weights_only=True) for r in range(n)]
+        assert all(torch.equal(ps[0], p) for p in ps[1:])
+        outs[algo] = ps[0]
+    if n == 2:
+        assert torch.equal(outs["rccl"], outs["rs_ag"])
+    else:
+        assert torch.allclose(outs["rccl"], outs["rs_ag"], rtol=1e-5, atol=1e-6)
+
+
 def test_bench_rejects_world_mismatch(tmp_path):
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", BENCH_BACKEND="gloo", HIP_VISIBLE_DEVICES="")
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny"], env=env,
