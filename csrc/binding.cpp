@@ -79,6 +79,8 @@ void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 void gemm_set_cpol(int);
 int gemm_cpol();
+void gemm_set_lines(int);
+int gemm_lines();
 void gemm_set_drain(int);
 int gemm_drain();
 bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
@@ -429,8 +431,8 @@ Tensor transpose_bf16(Tensor w) {
 }
 
 Tensor transpose_act_bf16(Tensor x) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
-              "transpose_act_bf16: contiguous bf16 matrix expected");
+  CHECK_IN(x, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 2, "transpose_act_bf16: bf16 matrix expected");
   TORCH_CHECK(x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose_act_bf16: both dims must be multiples of 64");
   TORCH_CHECK(x.size(0) < (1L << 31) && x.size(1) < (1L << 31), "transpose_act_bf16: matrix too large");
   auto xt = torch::empty({x.size(1), x.size(0)}, x.options());
@@ -596,6 +598,7 @@ std::vector<Tensor> ff_in_geglu_pt(Tensor x, Tensor w1i, c10::optional<Tensor> b
 
 Tensor permlane16_probe() {
   auto out = torch::empty({128}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA));
+  CHECK_CUDA(out);
   dalle::permlane16_probe((unsigned*)out.data_ptr<int>(), cur_stream());
   return out;
 }
@@ -1195,6 +1198,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cpol", [](int64_t c) { dalle::gemm_set_cpol((int)c); }, py::arg("cpol"),
         "cache policy of the hand-written GEMMs' output stores: 0 plain, 1 sc0, 2 nt, 16 sc1, 17 sc0 sc1");
   m.def("gemm_cpol", []() { return (int64_t)dalle::gemm_cpol(); });
+  m.def("gemm_set_lines", [](int64_t v) { dalle::gemm_set_lines((int)v); }, py::arg("lines"),
+        "1: register-epilogue GEMM stores of whole 128-B lines (default), 0: 16 rows x 64 B per store");
+  m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
   m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });

@@ -101,6 +101,29 @@ __device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
   y = r[1];
 }
 
+// DPP row_ror:8 -- lane l of every 16-lane row reads lane (l + 8) & 15 of the same row
+__device__ __forceinline__ unsigned ror8(unsigned v) { return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false); }
+
+// Whole-line re-layout of one 16-row sub-tile (round 4, profiles/r4_store_patterns.jsonl): on entry lane
+// (fr, q) holds two 16-byte chunks of ITS row fr, c0 from column pair jp = 0 and c1 from jp = 1 (the
+// layout after swap16); on exit c0 is the chunk of row (fr & 7) and c1 the chunk of row 8 + (fr & 7), both
+// at element column lines_col(lane) of the wave's 64. The lanes of row halves fr < 8 / fr >= 8 trade their
+// jp = 1 / jp = 0 chunks through one DPP row rotate per dword, so each store instruction covers 8 rows x
+// 128 B (whole lines) instead of 16 rows x 64 B: 41-51 vs 14-15 B/clk of store issue per CU.
+__device__ __forceinline__ void lines16(u32x4_vs& c0, u32x4_vs& c1, bool low) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned r = ror8(low ? c1[k] : c0[k]);
+    const unsigned a = low ? c0[k] : r, b = low ? r : c1[k];
+    c0[k] = a;
+    c1[k] = b;
+  }
+}
+__device__ __forceinline__ int lines_col(int lane) {
+  const int fr = lane & 15, q = lane >> 4;
+  return (fr >> 3) * 32 + (q & 1) * 16 + (q >> 1) * 8;
+}
+
 // epilogue output stream: a wave-uniform base, its buffer descriptor and the store cache policy
 struct Out {
   __bf16* base;
@@ -109,6 +132,9 @@ struct Out {
   __device__ __forceinline__ Out(__bf16* b, int cp) : base(b), rsrc(uniform_rsrc(b)), cpol(cp) {}
   __device__ __forceinline__ void st(__bf16* p, unsigned x0, unsigned x1, unsigned y0, unsigned y1) const {
     const u32x4_vs v = {x0, x1, y0, y1};
+    cstore16(base, rsrc, (uint32_t)((char*)p - (char*)base), v, cpol);
+  }
+  __device__ __forceinline__ void st4(__bf16* p, const u32x4_vs& v) const {
     cstore16(base, rsrc, (uint32_t)((char*)p - (char*)base), v, cpol);
   }
 };
@@ -156,7 +182,7 @@ __device__ __forceinline__ int pt_seq2st(const PtArgs& e, int p) {
 // Epilogue of one finished tile (origin r0, c0) straight from the transposed accumulators: lane l of
 // wave (wm, wn) holds, for sub-tile (i, j), row r0 + wm*128 + i*16 + (l & 15) and the 4 columns
 // c0 + wn*64 + j*16 + (l >> 4)*4 + 0..3.
-template <int EPI>
+template <int EPI, bool LINES>
 __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0, int wm, int wn, int lane, const PtArgs& e) {
   using namespace pt;
   const int fr = lane & 15, q = lane >> 4;
@@ -188,6 +214,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __bf16* rowp = e.C + (size_t)(r0 + wm * 128 + i * 16 + fr) * e.ldc + cw + (q & 2) * 4;
+      u32x4_vs ch[2];
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         const int j0 = 2 * jp, j1 = j0 + 1;
@@ -197,7 +224,14 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
         unsigned y1 = pk2(acc[i][j1][2] + bv[j1][2], acc[i][j1][3] + bv[j1][3]);
         swap16(x0, y0);
         swap16(x1, y1);
-        oc.st(rowp + ((q & 1) ? j1 : j0) * 16, x0, x1, y0, y1);
+        if constexpr (LINES) ch[jp] = u32x4_vs{x0, x1, y0, y1};
+        else oc.st(rowp + ((q & 1) ? j1 : j0) * 16, x0, x1, y0, y1);
+      }
+      if constexpr (LINES) {
+        lines16(ch[0], ch[1], fr < 8);
+        __bf16* lp = e.C + (size_t)(r0 + wm * 128 + i * 16 + (fr & 7)) * e.ldc + cw + lines_col(lane);
+        oc.st4(lp, ch[0]);
+        oc.st4(lp + (size_t)8 * e.ldc, ch[1]);
       }
     }
   } else if constexpr (EPI == 1) {
@@ -228,7 +262,16 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
         const int j0 = 2 * jp, j1 = j0 + 1;
         swap16(w[j0][0], w[j1][0]);
         swap16(w[j0][1], w[j1][1]);
-        oc.st(rowp + ((q & 1) ? j1 : j0) * 16, w[j0][0], w[j0][1], w[j1][0], w[j1][1]);
+        if constexpr (!LINES) oc.st(rowp + ((q & 1) ? j1 : j0) * 16, w[j0][0], w[j0][1], w[j1][0], w[j1][1]);
+      }
+      if constexpr (LINES) {
+        // the 16 rows of a sub-tile are 16 consecutive positions of one sample (n % 16 == 0, host-checked)
+        u32x4_vs c0v = {w[0][0], w[0][1], w[1][0], w[1][1]}, c1v = {w[2][0], w[2][1], w[3][0], w[3][1]};
+        lines16(c0v, c1v, fr < 8);
+        const int p0 = p - (fr & 8);
+        __bf16* base = dstT + (size_t)(b * e.H + hh) * e.Np * 64 + lines_col(lane);
+        oc.st4(base + (size_t)pt_seq2st(e, p0) * 64, c0v);
+        oc.st4(base + (size_t)pt_seq2st(e, p0 + 8) * 64, c1v);
       }
       __builtin_amdgcn_sched_barrier(0);  // bound the live loads to one row sub-tile
     }
@@ -239,6 +282,7 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
     // sub-tile pair (j0, j0 + 1) of one 64-row half at a time keeps the live set small.
     const int F = e.F;
     const pt::Out od(e.dh, e.cpol);
+    u32x4_vs hold[4][2];  // LINES: the jp = 0 [da | dg] chunks of the half's 4 sub-tiles, paired with jp = 1
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
@@ -291,8 +335,25 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
           }
           swap16(da[0][0], da[1][0]); swap16(da[0][1], da[1][1]);
           swap16(dg[0][0], dg[1][0]); swap16(dg[0][1], dg[1][1]);
-          od.st(e.dh + off, da[0][0], da[0][1], da[1][0], da[1][1]);
-          od.st(e.dh + off + F, dg[0][0], dg[0][1], dg[1][0], dg[1][1]);
+          if constexpr (LINES) {
+            u32x4_vs ca = {da[0][0], da[0][1], da[1][0], da[1][1]}, cg = {dg[0][0], dg[0][1], dg[1][0], dg[1][1]};
+            if (jp == 0) {
+              hold[ii][0] = ca;
+              hold[ii][1] = cg;
+            } else {
+              lines16(hold[ii][0], ca, fr < 8);
+              lines16(hold[ii][1], cg, fr < 8);
+              const size_t lrow = (size_t)(r0 + wm * 128 + i * 16 + (fr & 7));
+              __bf16* lp = e.dh + lrow * 2 * F + cw + lines_col(lane);
+              od.st4(lp, hold[ii][0]);
+              od.st4(lp + (size_t)16 * F, ca);
+              od.st4(lp + F, hold[ii][1]);
+              od.st4(lp + (size_t)16 * F + F, cg);
+            }
+          } else {
+            od.st(e.dh + off, da[0][0], da[0][1], da[1][0], da[1][1]);
+            od.st(e.dh + off + F, dg[0][0], dg[0][1], dg[1][0], dg[1][1]);
+          }
         }
         // reduce over the 16 rows held by lanes 16q .. 16q+15 (fixed xor tree: deterministic)
 #pragma unroll
@@ -365,10 +426,86 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
   }
 }
 
+// FF-in + GEGLU forward (EPI 3) with whole-line stores, one tile per workgroup: after the main loop the
+// 128 KiB of operand LDS is free, so the tile goes out through it. Pass 1 writes value and gate (bf16, 8 B
+// per lane: 4 consecutive features) into two [256 rows][128 features] images whose 16-byte chunks are
+// XOR-swizzled by row (c ^ (row & 15): the 16 lanes of a write group hit 16 distinct chunks), pass 2 the
+// products u = value * gelu(gate) (computed in registers in pass 1); each read-back instruction covers 4 whole
+// rows x 256 B, so every global store writes whole 128-B lines of a (value | gate halves) and u.
+__device__ __forceinline__ int geglu_lds_idx(int row, int feat) {
+  return row * 128 + ((((feat >> 3) ^ (row & 15)) << 3) | (feat & 7));
+}
+
+__device__ __forceinline__ void pt_epilogue_geglu_lds(pt::f4 (&acc)[8][4], __bf16* smem, int r0, int c0, int wm, int wn,
+                                                      int lane, const PtArgs& e) {
+  using namespace pt;
+  const int fr = lane & 15, q = lane >> 4;
+  const int tid = threadIdx.x;
+  const int F = e.F;
+  const int fw = c0 >> 1;  // the workgroup's first feature (128 features per tile)
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
+  if (e.bias != nullptr) {  // the interleaved bias (2F,)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint2 b = *reinterpret_cast<const uint2*>(e.bias + c0 + wn * 64 + j * 16 + q * 4);
+      bv[j][0] = lo_f(b.x); bv[j][1] = hi_f(b.x); bv[j][2] = lo_f(b.y); bv[j][3] = hi_f(b.y);
+    }
+  }
+  __bf16* V = smem;              // [256][128] value image
+  __bf16* G = smem + 256 * 128;  // [256][128] gate image, later the u image lives in V
+  asm volatile("s_barrier" ::: "memory");  // every wave is past its last operand read
+  unsigned uu[8][2][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wm * 128 + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const unsigned v0 = pk2(acc[i][j][0] + bv[j][0], acc[i][j][1] + bv[j][1]);
+      const unsigned v1 = pk2(acc[i][j][2] + bv[j][2], acc[i][j][3] + bv[j][3]);
+      const unsigned g0 = pk2(acc[i][j + 2][0] + bv[j + 2][0], acc[i][j + 2][1] + bv[j + 2][1]);
+      const unsigned g1 = pk2(acc[i][j + 2][2] + bv[j + 2][2], acc[i][j + 2][3] + bv[j + 2][3]);
+      uu[i][j][0] = pk2(lo_f(v0) * gelu_fast(lo_f(g0)), hi_f(v0) * gelu_fast(hi_f(g0)));
+      uu[i][j][1] = pk2(lo_f(v1) * gelu_fast(lo_f(g1)), hi_f(v1) * gelu_fast(hi_f(g1)));
+      const int feat = wn * 32 + j * 16 + q * 4;
+      *reinterpret_cast<uint2*>(V + geglu_lds_idx(row, feat)) = uint2{v0, v1};
+      *reinterpret_cast<uint2*>(G + geglu_lds_idx(row, feat)) = uint2{g0, g1};
+    }
+  }
+  __syncthreads();
+  const pt::Out oa(e.a, e.cpol), ou(e.u, e.cpol);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 512 + tid, row = idx >> 4, ch = idx & 15;
+    const int li = row * 128 + ((ch ^ (row & 15)) << 3);
+    const u32x4_vs vv = *reinterpret_cast<const u32x4_vs*>(V + li);
+    const u32x4_vs gg = *reinterpret_cast<const u32x4_vs*>(G + li);
+    __bf16* ap = e.a + (size_t)(r0 + row) * 2 * F + fw + ch * 8;
+    oa.st4(ap, vv);
+    oa.st4(ap + F, gg);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<uint2*>(V + geglu_lds_idx(wm * 128 + i * 16 + fr, wn * 32 + j * 16 + q * 4)) = uint2{uu[i][j][0], uu[i][j][1]};
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 512 + tid, row = idx >> 4, ch = idx & 15;
+    const u32x4_vs uv = *reinterpret_cast<const u32x4_vs*>(V + row * 128 + ((ch ^ (row & 15)) << 3));
+    ou.st4(e.u + (size_t)(r0 + row) * F + fw + ch * 8, uv);
+  }
+}
+
 // PERSIST = false: one tile per workgroup (grid = tile count), the same main loop and register-direct
 // epilogue -- a workgroup's stores then drain while the NEXT workgroup on that CU already streams its
 // first K-tiles (the epilogue ends with the store issue; nothing waits for completion)
-template <int EPI, bool PERSIST = true>
+template <int EPI, bool PERSIST = true, bool LINES = false>
 __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                  int M, int N, int K, PtArgs e) {
   using namespace pt;
@@ -525,7 +662,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
     // first K-steps are in flight; then re-zero
     if (it + 1 < my_tiles) {
       __builtin_amdgcn_sched_barrier(0);
-      pt_epilogue<EPI>(acc, cr, cc, wm, wn, lane, e);
+      pt_epilogue<EPI, LINES>(acc, cr, cc, wm, wn, lane, e);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -540,7 +677,8 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   }
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
   const unsigned long long t_epi = __builtin_amdgcn_s_memrealtime();
-  pt_epilogue<EPI>(acc, pr, pc, wm, wn, lane, e);
+  if constexpr (EPI == 3 && LINES && !PERSIST) pt_epilogue_geglu_lds(acc, smem, pr, pc, wm, wn, lane, e);
+  else pt_epilogue<EPI, LINES>(acc, pr, pc, wm, wn, lane, e);
   if (e.drain && e.stamps == nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!PERSIST && e.stamps != nullptr) {
     const unsigned long long t_issued = __builtin_amdgcn_s_memrealtime();
@@ -627,8 +765,28 @@ static int g_gemm_drain = [] {
 void gemm_set_drain(int d) { g_gemm_drain = d; }
 int gemm_drain() { return g_gemm_drain; }
 
+// DALLE_AMD_GEMM_LINES (default 1): epilogue stores of whole 128-B lines (8 rows x 128 B per store
+// instruction, lines16) instead of 16 rows x 64 B; gemm_set_lines overrides it at run time (benchmarks)
+static int g_gemm_lines = [] {
+  const char* s = getenv("DALLE_AMD_GEMM_LINES");
+  return s ? atoi(s) : 1;
+}();
+void gemm_set_lines(int v) { g_gemm_lines = v; }
+int gemm_lines() { return g_gemm_lines; }
+
+template <int EPI, bool LINES>
+static void pt_launch_k(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist, int ntiles) {
+  if (persist)
+    hipLaunchKernelGGL((gemm_pt_kernel<EPI, true, LINES>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
+                       (const __bf16*)B, M, N, K, e);
+  else
+    hipLaunchKernelGGL((gemm_pt_kernel<EPI, false, LINES>), dim3(ntiles), dim3(pt::THREADS), 0, st, (const __bf16*)A,
+                       (const __bf16*)B, M, N, K, e);
+}
+
 template <int EPI>
-static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist = -1) {
+static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist = -1,
+                      bool lines_ok = true) {
   const int ntiles = (M / pt::BM) * (N / pt::BN);
   if (persist < 0) persist = pt_persist_default();
   if (!persist && e.stagger < 0) e.stagger = gemm_stagger_ticks(ntiles, K);
@@ -637,12 +795,15 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
   // buffer-store policies address the output with a 32-bit byte offset: plain stores past 2 GiB of output
   e.cpol = (size_t)M * N * 4 < (1ull << 32) ? g_gemm_cpol : 0;
   e.drain = g_gemm_drain;
-  if (persist)
-    hipLaunchKernelGGL((gemm_pt_kernel<EPI, true>), dim3(pt_grid(ntiles)), dim3(pt::THREADS), 0, st, (const __bf16*)A,
-                       (const __bf16*)B, M, N, K, e);
-  else
-    hipLaunchKernelGGL((gemm_pt_kernel<EPI, false>), dim3(ntiles), dim3(pt::THREADS), 0, st, (const __bf16*)A,
-                       (const __bf16*)B, M, N, K, e);
+  if constexpr (EPI == 0 || EPI == 1 || EPI == 2 || EPI == 3) {
+    // EPI 3: whole lines through LDS in the one-tile-per-workgroup form only (a persistent kernel's LDS
+    // holds the next tile's operands)
+    if (g_gemm_lines && lines_ok && (EPI != 3 || !persist)) {
+      pt_launch_k<EPI, true>(A, B, M, N, K, e, st, persist, ntiles);
+      return;
+    }
+  }
+  pt_launch_k<EPI, false>(A, B, M, N, K, e, st, persist, ntiles);
 }
 
 static bool pt_shape_ok(int M, int N, int K) { return M > 0 && N > 0 && M % pt::BM == 0 && N % pt::BN == 0 && K % pt::BK == 0 && K >= 2 * pt::BK; }
@@ -703,7 +864,8 @@ bool gemm_pt_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, c
   e.col_major = col_major;
   e.qscale = qscale;
   e.group = pt_group_default();
-  pt_launch<1>(A, W, M, N, K, e, st, persist);
+  // whole-line stores pair rows 8 apart inside a 16-row sub-tile: one sample's positions when n % 16 == 0
+  pt_launch<1>(A, W, M, N, K, e, st, persist, n % 16 == 0);
   return true;
 }
 

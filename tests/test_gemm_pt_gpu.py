@@ -171,3 +171,43 @@ def test_store_policy_and_drain_bitwise(cuda, cpol, drain):
         C.gemm_set_drain(1)
     for r, g in zip(ref, got):
         assert torch.equal(r, g)
+
+
+@pytest.mark.parametrize("persist", [0, 1])
+def test_line_stores_bitwise(cuda, persist):
+    """Whole-line epilogue stores (gemm_set_lines(1): 8 rows x 128 B per store via a DPP row exchange; the
+    FF-in + GEGLU epilogue through LDS) move the same bytes as the 16 rows x 64 B form: plain product, QKV +
+    rotary, FF-out dgrad + GEGLU backward, FF-in + GEGLU forward."""
+    from dalle_amd.ops import hip_ops
+    from dalle_amd.ops.hip_ops import _rope_tables, rope_cs_table
+
+    C = hip_ops.C()
+    torch.manual_seed(11)
+    A = torch.randn(2048, 512, device=cuda).bfloat16()
+    B = torch.randn(1536, 512, device=cuda).bfloat16()
+    bias = torch.randn(1536, device=cuda).bfloat16()
+    T, S, H, D = 65, 16, 4, 256
+    geom = AttnGeometry(T, S, 5)
+    n = T + S * S - 1
+    h = torch.randn(8 * n, D, device=cuda).bfloat16()
+    w = (0.05 * torch.randn(3 * H * 64, D, device=cuda)).bfloat16()
+    cs = rope_cs_table(geom, 64, cuda)
+    dy = (torch.randn(2560, 1024, device=cuda) * 0.5).bfloat16()
+    w2t = (torch.randn(4096, 1024, device=cuda) * 0.03).bfloat16()
+    hh = torch.randn(2560, 8192, device=cuda).bfloat16()
+    perm = hip_ops.geglu_interleave_index(4096, cuda)
+    w1 = torch.randn(8192, 1024, device=cuda) * 0.03
+    b1 = torch.randn(8192, device=cuda) * 0.1
+    w1i, b1i = w1[perm].bfloat16().contiguous(), b1[perm].bfloat16().contiguous()
+    prev = C.gemm_lines()
+    outs = {}
+    try:
+        for lines in (0, 1):
+            C.gemm_set_lines(lines)
+            outs[lines] = [C.gemm_pt(A, B, bias, 10 + 10 * persist, 0), *C.qkv_rope_pt(h, w, cs, T, S, H, n, False, 0.125, persist),
+                           *C.qkv_rope_pt(h, w, cs, T, S, H, n, True, 0.125, persist), *C.ff_dgrad_geglu_pt(dy, w2t, hh, None, persist),
+                           *C.ff_in_geglu_pt(dy, w1i, b1i, persist)]
+    finally:
+        C.gemm_set_lines(prev)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
