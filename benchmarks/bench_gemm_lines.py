@@ -81,7 +81,17 @@ def main():
         dy = (0.5 * torch.randn(M, D, device=dev)).bfloat16()
         w2t = (0.03 * torch.randn(F, D, device=dev)).bfloat16()
         hh = torch.randn(M, 2 * F, device=dev).bfloat16()
+        def P(pf, fn):
+            def f():
+                C.gemm_set_prefetch(pf)
+                r = fn()
+                C.gemm_set_prefetch(0)
+                return r
+            return f
+
         t = run({"8ph": lambda: C.ff_dgrad_geglu(dy, w2t, hh),
+                 "np_l1_pf": P(1, L(1, lambda: C.ff_dgrad_geglu_pt(dy, w2t, hh, None, 0))),
+                 "ps_l1_pf": P(1, L(1, lambda: C.ff_dgrad_geglu_pt(dy, w2t, hh, None, 1))),
                  "np_l0": L(0, lambda: C.ff_dgrad_geglu_pt(dy, w2t, hh, None, 0)),
                  "np_l1": L(1, lambda: C.ff_dgrad_geglu_pt(dy, w2t, hh, None, 0)),
                  "ps_l0": L(0, lambda: C.ff_dgrad_geglu_pt(dy, w2t, hh, None, 1)),

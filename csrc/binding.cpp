@@ -80,6 +80,7 @@ bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, i
 void gemm_set_cpol(int);
 int gemm_cpol();
 void gemm_set_lines(int);
+void gemm_set_prefetch(int);
 int gemm_lines();
 void gemm_set_drain(int);
 int gemm_drain();
@@ -1201,6 +1202,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_lines", [](int64_t v) { dalle::gemm_set_lines((int)v); }, py::arg("lines"),
         "1: register-epilogue GEMM stores of whole 128-B lines (default), 0: 16 rows x 64 B per store");
   m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
+  m.def("gemm_set_prefetch", [](int64_t v) { dalle::gemm_set_prefetch((int)v); }, py::arg("prefetch"),
+        "1: the FF-out dgrad + GEGLU-backward GEMM prefetches its epilogue's pre-activation lines in the main loop");
   m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });

@@ -170,6 +170,7 @@ struct PtArgs {
   unsigned long long* stamps;
   int skip_odd;
   int drain;  // wait for the output stores before the workgroup ends (gemm_set_drain)
+  int prefetch;  // EPI 2: pull the tile's pre-activation lines toward the caches during its main loop
 };
 
 __device__ __forceinline__ int pt_seq2st(const PtArgs& e, int p) {
@@ -511,7 +512,8 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   using namespace pt;
   // [buf][A-lo | B-lo | B-hi | A-hi] half-tile images, 128 KiB in ONE array (a second __shared__
   // object can make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF];
+  // + 2 KiB: the landing area of the EPI 2 cache prefetch (8 waves x 256 B, never read)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF + 1024];
   if constexpr (!PERSIST) stagger_start(e.stagger, e.first_wave);
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -646,6 +648,21 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      if constexpr (EPI == 2) {
+        // cache prefetch of the pre-activation lines the epilogue will read (2048 x 128 B per tile: the
+        // value and gate halves of 256 rows), one 4-byte LDS-DMA piece per lane and line, at four K-steps
+        // spread over the main loop: the HBM reads move from the epilogue (when every CU's epilogue
+        // competes for them) into the MFMA-bound main loop. Issued after the counted wait, so the wait
+        // structure is unchanged (a younger piece only ever makes a later vmcnt stricter).
+        const int slot = nk >= 8 ? (kt * 4) / nk : -1;
+        if (e.prefetch && slot >= 0 && kt == (slot * nk + 3) / 4) {
+          const int L = slot * 512 + tid;  // line id in [0, 2048)
+          const int row = L >> 3, ln = L & 7;
+          const __bf16* src = e.h + (size_t)(cr + row) * 2 * e.F + (ln < 4 ? cc + ln * 64 : e.F + cc + (ln - 4) * 64);
+          __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                           (void __attribute__((address_space(3)))*)(smem + 2 * 4 * HALF + wave * 128), 4, 0, 0);
+        }
+      }
       asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -772,6 +789,13 @@ static int g_gemm_lines = [] {
   return s ? atoi(s) : 1;
 }();
 void gemm_set_lines(int v) { g_gemm_lines = v; }
+// DALLE_AMD_GEMM_PREFETCH (default 0 until measured): the FF-out dgrad + GEGLU-backward GEMM prefetches
+// its epilogue's pre-activation lines during the main loop; gemm_set_prefetch overrides it at run time
+static int g_gemm_prefetch = [] {
+  const char* s = getenv("DALLE_AMD_GEMM_PREFETCH");
+  return s ? atoi(s) : 0;
+}();
+void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
 int gemm_lines() { return g_gemm_lines; }
 
 template <int EPI, bool LINES>
@@ -795,6 +819,7 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
   // buffer-store policies address the output with a 32-bit byte offset: plain stores past 2 GiB of output
   e.cpol = (size_t)M * N * 4 < (1ull << 32) ? g_gemm_cpol : 0;
   e.drain = g_gemm_drain;
+  e.prefetch = g_gemm_prefetch;
   if constexpr (EPI == 0 || EPI == 1 || EPI == 2 || EPI == 3) {
     // EPI 3: whole lines through LDS in the one-tile-per-workgroup form only (a persistent kernel's LDS
     // holds the next tile's operands)

@@ -101,9 +101,16 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
 
 
 NT_INPUT_GRAD = os.environ.get("DALLE_AMD_NT_DGRAD", "1") != "0"
-# plain (epilogue-free) projection GEMMs on the hand-written register-epilogue kernel
-# (csrc/kernels/gemm_pt.hip, one tile per workgroup + first-wave start stagger) instead of hipBLASLt
-OWN_GEMM = int(os.environ.get("DALLE_AMD_OWN_GEMM", "0"))
+# plain (epilogue-free) projection GEMMs on the hand-written register-epilogue kernel (csrc/kernels/gemm_pt.hip,
+# one tile per workgroup, whole-line epilogue stores) instead of hipBLASLt. DALLE_AMD_OWN_GEMM: "auto" (default) =
+# the (N, K) shapes in OWN_GEMM_SHAPES, measured faster than hipBLASLt at the training token counts
+# (benchmarks/bench_gemm_lines.py); "1" = every shape that tiles; "0" = none; "N:K,N:K,..." = those shapes
+_own_env = os.environ.get("DALLE_AMD_OWN_GEMM", "auto")
+OWN_GEMM_SHAPES = set()
+OWN_GEMM = 0 if _own_env == "0" else (2 if _own_env == "1" else 1)
+if ":" in _own_env:
+    OWN_GEMM_SHAPES = {tuple(int(v) for v in t.split(":")) for t in _own_env.split(",") if t}
+OWN_GEMM_MIN_M = 16384  # below this the grid does not fill the chip's 256 CUs several times over
 
 
 def _own_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -112,9 +119,17 @@ def _own_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.shape[1] % 64 == 0 and a.shape[1] >= 128)
 
 
+def own_gemm_for(M: int, N: int, K: int) -> bool:
+    """Whether the plain product (M, K) x (N, K)^T goes to the hand-written GEMM (DALLE_AMD_OWN_GEMM policy)."""
+    if OWN_GEMM == 2:
+        return True
+    return OWN_GEMM == 1 and M >= OWN_GEMM_MIN_M and (N, K) in OWN_GEMM_SHAPES
+
+
 def mm_nt(a: torch.Tensor, b: torch.Tensor, bias=None) -> torch.Tensor:
-    """a (M, K) . b (N, K)^T (+ bias): the hand-written GEMM when OWN_GEMM and the shape tiles, else hipBLASLt."""
-    if OWN_GEMM and _own_gemm_ok(a, b):
+    """a (M, K) . b (N, K)^T (+ bias): the hand-written GEMM where the policy picks it and the shape tiles,
+    else hipBLASLt."""
+    if OWN_GEMM and _own_gemm_ok(a, b) and own_gemm_for(a.shape[0], b.shape[0], a.shape[1]):
         _count("own_gemm")
         return C().gemm_pt(a, b, bias, 10, 0)
     if bias is not None:

@@ -274,7 +274,7 @@ def test_reference_geometry_end_to_end(cuda, reversible, own, monkeypatch):
     from dalle_amd.ops import hip_ops
 
     if own:  # every projection GEMM on the hand-written kernels, FF-in with the GEGLU epilogue
-        monkeypatch.setattr(hip_ops, "OWN_GEMM", 1)
+        monkeypatch.setattr(hip_ops, "OWN_GEMM", 2)
         monkeypatch.setattr(hip_ops, "FUSED_FF_IN", 1)
     torch.manual_seed(0)
     cfg = DALLEConfig(depth=4, attn_types=reference_attn_types(4), shared_attn_ids=reference_shared_ids(4),
