@@ -81,6 +81,7 @@ void gemm_set_cpol(int);
 int gemm_cpol();
 void gemm_set_lines(int);
 void gemm_set_prefetch(int);
+void gemm_set_pt_overlap(int, int);
 int gemm_lines();
 void gemm_set_drain(int);
 int gemm_drain();
@@ -1202,6 +1203,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_lines", [](int64_t v) { dalle::gemm_set_lines((int)v); }, py::arg("lines"),
         "1: register-epilogue GEMM stores of whole 128-B lines (default), 0: 16 rows x 64 B per store");
   m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
+  m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },
+        py::arg("overlap"), py::arg("stagger_pct") = 0,
+        "persistent plain GEMM: epilogue stores beside the next tile's first K-step; start stagger in % of a tile");
   m.def("gemm_set_prefetch", [](int64_t v) { dalle::gemm_set_prefetch((int)v); }, py::arg("prefetch"),
         "1: the FF-out dgrad + GEGLU-backward GEMM prefetches its epilogue's pre-activation lines in the main loop");
   m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),

@@ -171,6 +171,7 @@ struct PtArgs {
   int skip_odd;
   int drain;  // wait for the output stores before the workgroup ends (gemm_set_drain)
   int prefetch;  // EPI 2: pull the tile's pre-activation lines toward the caches during its main loop
+  int overlap;   // persistent: a tile's epilogue stores drain beside the next tile's first K-steps (pt_overlap)
 };
 
 __device__ __forceinline__ int pt_seq2st(const PtArgs& e, int p) {
@@ -510,11 +511,14 @@ template <int EPI, bool PERSIST = true, bool LINES = false>
 __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                                  int M, int N, int K, PtArgs e) {
   using namespace pt;
+  // vector-memory instructions of one wave's overlapped epilogue (pt_epilogue, EPI 0 without bias: 8
+  // row sub-tiles x 2 16-byte stores); 0 = this epilogue cannot overlap
+  constexpr int EPI_VM = EPI == 0 ? 16 : 0;
   // [buf][A-lo | B-lo | B-hi | A-hi] half-tile images, 128 KiB in ONE array (a second __shared__
   // object can make hipcc drain vmcnt before every ds_read)
   // + 2 KiB: the landing area of the EPI 2 cache prefetch (8 waves x 256 B, never read)
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * HALF + 1024];
-  if constexpr (!PERSIST) stagger_start(e.stagger, e.first_wave);
+  stagger_start(e.stagger, e.first_wave);
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
@@ -577,6 +581,20 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
       const bool s1 = g + 1 < total, s2 = g + 2 < total;
 
       // ---- phase 1: B-lo then A-lo -> quadrant (lo, lo)
+      // overlapped epilogue (persistent, e.overlap): the previous tile's stores go out HERE, after this
+      // phase's DMA, so they are younger than every operand load the phase-4 wait must retire: that wait
+      // then leaves them in flight (vmcnt(6 + EPI_VM)) and they drain beside this K-step's MFMAs
+      const bool ovl = PERSIST && EPI_VM > 0 && e.overlap && kt == 0 && it > 0;
+      if (ovl) {
+        if (s1) stage(r1, c1, k1, buf ^ 1, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        pt_epilogue<EPI, LINES>(acc, pr, pc, wm, wn, lane, e);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -586,7 +604,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) a[i][kk] = fragA(Alo, i, kk);
-      if (s1) stage(r1, c1, k1, buf ^ 1, 3);
+      if (s1 && !ovl) stage(r1, c1, k1, buf ^ 1, 3);
       asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
       asm volatile("s_barrier" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -644,7 +662,8 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
       // ---- phase 4: registers only -> quadrant (hi, lo); retire K-step g + 1
       if (s2) {
         stage(r2, c2, k2, buf, 2);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (ovl) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + EPI_VM) : "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -677,7 +696,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
     }
     // ---- the finished tile's epilogue, straight from the accumulators (no LDS), while the next tile's
     // first K-steps are in flight; then re-zero
-    if (it + 1 < my_tiles) {
+    if (it + 1 < my_tiles && !(EPI_VM > 0 && e.overlap)) {
       __builtin_amdgcn_sched_barrier(0);
       pt_epilogue<EPI, LINES>(acc, cr, cc, wm, wn, lane, e);
 #pragma unroll
@@ -796,6 +815,21 @@ static int g_gemm_prefetch = [] {
   return s ? atoi(s) : 0;
 }();
 void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
+// DALLE_AMD_PT_OVERLAP (default 1): persistent plain GEMMs (no bias) issue a tile's stores beside the next
+// tile's first K-step (see gemm_pt_kernel phase 1); DALLE_AMD_PT_STAGGER=<percent of one tile>: start the
+// persistent workgroups at four phases so their epilogues do not all hit HBM at once
+static int g_pt_overlap = [] {
+  const char* s = getenv("DALLE_AMD_PT_OVERLAP");
+  return s ? atoi(s) : 1;
+}();
+static int g_pt_stagger = [] {
+  const char* s = getenv("DALLE_AMD_PT_STAGGER");
+  return s ? atoi(s) : 0;
+}();
+void gemm_set_pt_overlap(int v, int stagger_pct) {
+  g_pt_overlap = v;
+  g_pt_stagger = stagger_pct;
+}
 int gemm_lines() { return g_gemm_lines; }
 
 template <int EPI, bool LINES>
@@ -820,6 +854,12 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
   e.cpol = (size_t)M * N * 4 < (1ull << 32) ? g_gemm_cpol : 0;
   e.drain = g_gemm_drain;
   e.prefetch = g_gemm_prefetch;
+  e.overlap = g_pt_overlap && (EPI != 0 || e.bias == nullptr);
+  if (persist && g_pt_stagger > 0 && ntiles > 2 * pt_cus()) {
+    // a quarter-phase offset per group of 8 workgroups: (b >> 3) & 3 quarters of stagger_pct % of one tile
+    const double tile_s = 2.0 * 256.0 * 256.0 * K / (1.3e15 / pt_cus());
+    e.stagger = (int)(tile_s * g_pt_stagger / 100.0 * 1e8);
+  }
   if constexpr (EPI == 0 || EPI == 1 || EPI == 2 || EPI == 3) {
     // EPI 3: whole lines through LDS in the one-tile-per-workgroup form only (a persistent kernel's LDS
     // holds the next tile's operands)
