@@ -82,6 +82,9 @@ int gemm_cpol();
 void gemm_set_lines(int);
 void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
+void attn_set_pf(int, int);
+void gemm_set_geglu_bwd_2wg(int);
+bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
 int gemm_lines();
 void gemm_set_drain(int);
 int gemm_drain();
@@ -1203,6 +1206,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_lines", [](int64_t v) { dalle::gemm_set_lines((int)v); }, py::arg("lines"),
         "1: register-epilogue GEMM stores of whole 128-B lines (default), 0: 16 rows x 64 B per store");
   m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
+  m.def("gemm_set_geglu_bwd_2wg", [](int64_t v) { dalle::gemm_set_geglu_bwd_2wg((int)v); }, py::arg("v"),
+        "1: FF-out dgrad + GEGLU backward on the two-workgroups-per-CU kernel");
+  m.def("gemm_2wg", [](Tensor A, Tensor B) {
+    CHECK_IN(A, torch::kBFloat16); CHECK_IN(B, torch::kBFloat16);
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_2wg: A (M, K), B (N, K)");
+    auto C = torch::empty({A.size(0), B.size(0)}, A.options());
+    TORCH_CHECK(dalle::gemm_2wg(A.data_ptr(), B.data_ptr(), C.data_ptr(), nullptr, (int)A.size(0), (int)B.size(0), (int)A.size(1),
+                                cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
+    return C;
+  });
+  m.def("attn_set_pf", [](int64_t f, int64_t q) { dalle::attn_set_pf((int)f, (int)q); }, py::arg("fwd"), py::arg("dq"),
+        "attention forward / dQ: load the first local key tile before the text phase (1) or after it (0)");
   m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },
         py::arg("overlap"), py::arg("stagger_pct") = 0,
         "persistent plain GEMM: epilogue stores beside the next tile's first K-step; start stagger in % of a tile");

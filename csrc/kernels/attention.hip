@@ -364,7 +364,7 @@ __device__ __forceinline__ void fwd_tiles(SoftmaxState& st, const __bf16* const 
 //   (double-buffered 2 x {Ka, Kb, Va, Vb}, register-staged loads issued before compute, T14).
 // Phase B (wave-private): each image query block streams ITS OWN local key tiles through a private
 //   LDS slot (reusing phase A's buffers) -- no workgroup barrier, no wave idling on other blocks' tiles.
-template <int MINB>
+template <int MINB, bool PREFETCH_LOCAL = true>
 __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                           const __bf16* __restrict__ V, __bf16* __restrict__ out,
                                                           float* __restrict__ lse, AttnGeom g) {
@@ -388,6 +388,21 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   // step 0: 4 coalesced 1 KiB pieces instead of per-lane row reads that touch 32 lines per instruction
   dma_tile_wave(Q + base + (size_t)(active ? qb : 0) * 32 * 64, smem + 4 * TILE + wave * TILE, lane);
   SoftmaxState st;
+  // phase B's first local (image) key tile, loaded NOW into registers: its HBM latency then hides under
+  // phase A instead of being exposed after the last text pair (each local tile is read by one query tile)
+  const bool has_local = active && qb >= ntext && !(g.diag & 4);
+  const int lo = has_local ? local_lo_tile(g, qb) : 0;
+  s16x8 kr[4], vr[4];
+  auto load_loc = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
+      kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
+      vr[j] = *reinterpret_cast<const s16x8*>(V + off);
+    }
+  };
+  if (has_local && PREFETCH_LOCAL) load_loc(lo);
 
   // ---- phase A: shared text tiles, two per step ----
   const int npairs = (n_text + 1) >> 1;
@@ -429,20 +444,9 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
-  if (active && qb >= ntext && !(g.diag & 4)) {
+  if (has_local) {
     __bf16* P = smem + wave * (2 * TILE);
-    const int lo = local_lo_tile(g, qb);
-    s16x8 kr[4], vr[4];
-    auto load_loc = [&](int t) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-        const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
-        kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
-        vr[j] = *reinterpret_cast<const s16x8*>(V + off);
-      }
-    };
-    load_loc(lo);
+    if (!PREFETCH_LOCAL) load_loc(lo);
     for (int t = lo; t <= qb; ++t) {
       // the previous tile's LDS reads were consumed by its MFMAs (in program order before these stores)
 #pragma unroll
@@ -553,7 +557,7 @@ __device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* 
 // query tile -- its own row's (column's) -- so that tile's dK / dV are produced right here, by the wave
 // that owns the query tile, from the K / V it already staged and the Q / dO it already holds: the
 // separate image-key dK/dV kernel (a launch that re-read Q, dO, K and V of every local tile) disappears.
-template <int MINB, bool FUSE_LOCAL>
+template <int MINB, bool FUSE_LOCAL, bool PREFETCH_LOCAL = false>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                              const __bf16* __restrict__ out, const float* __restrict__ lse,
@@ -608,6 +612,20 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   }
   const float lq = lse[(size_t)bh * g.Np + qrow];
   f32x16 dq0 = {}, dq1 = {};
+  // PREFETCH_LOCAL: phase B's first local key tile loaded before phase A (see attn_fwd_kernel)
+  const bool has_local = active && qb >= ntext && !(g.diag & 4);
+  const int lo = has_local ? local_lo_tile(g, qb) : 0;
+  s16x8 kr[4], vr[4];
+  auto load_loc = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
+      kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
+      vr[j] = *reinterpret_cast<const s16x8*>(V + off);
+    }
+  };
+  if (has_local && PREFETCH_LOCAL) load_loc(lo);
 
   // ---- phase A: shared text tiles, two per step ----
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
@@ -643,20 +661,9 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
-  if (active && qb >= ntext && !(g.diag & 4)) {
+  if (has_local) {
     __bf16* P = smem + wave * (2 * TILE);
-    const int lo = local_lo_tile(g, qb);
-    s16x8 kr[4], vr[4];
-    auto load_loc = [&](int t) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-        const size_t off = base + (size_t)(t * 32 + row) * 64 + col;
-        kr[j] = *reinterpret_cast<const s16x8*>(Kt + off);
-        vr[j] = *reinterpret_cast<const s16x8*>(V + off);
-      }
-    };
-    load_loc(lo);
+    if (!PREFETCH_LOCAL) load_loc(lo);
     for (int t = lo; t <= qb; ++t) {
       // the previous tile's LDS reads were consumed by its MFMAs (in program order before these stores)
 #pragma unroll
@@ -1076,9 +1083,34 @@ static int attn_occ(int which) {
     else hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, st, __VA_ARGS__);                      \
   } while (0)
 
+// DALLE_AMD_ATTN_PF=<fwd>,<dq> (default 1,0): load phase B's first local key tile before phase A;
+// attn_set_pf overrides it at run time (benchmarks)
+static int g_attn_pf[2] = {-1, -1};
+static int attn_pf(int which) {
+  if (g_attn_pf[0] < 0) {
+    int v[2] = {1, 0};
+    if (const char* e = getenv("DALLE_AMD_ATTN_PF")) sscanf(e, "%d,%d", &v[0], &v[1]);
+    g_attn_pf[0] = v[0];
+    g_attn_pf[1] = v[1];
+  }
+  return g_attn_pf[which];
+}
+void attn_set_pf(int fwd, int dq) {
+  g_attn_pf[0] = fwd;
+  g_attn_pf[1] = dq;
+}
+
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
   dim3 grid((g.Np / 32 + 3) / 4, BH);
-  ATTN_LAUNCH(attn_fwd_kernel, 0, grid, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (__bf16*)out, lse, g);
+  const bool pf = attn_pf(0) != 0;
+  const __bf16 *qq = (const __bf16*)q, *kk = (const __bf16*)k, *vv = (const __bf16*)v;
+  if (attn_occ(0) == 3) {
+    if (pf) hipLaunchKernelGGL((attn_fwd_kernel<3, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+    else hipLaunchKernelGGL((attn_fwd_kernel<3, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+  } else {
+    if (pf) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+    else hipLaunchKernelGGL((attn_fwd_kernel<2, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+  }
 }
 
 void attn_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
@@ -1123,13 +1155,23 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   };
   if (conc) launch_dkdv(kst);
   const int dr = conc ? 1 : 0;
+  const bool pfq = attn_pf(1) != 0;
   if (fuse_local) {
-    if (attn_occ(1) == 3)
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                         (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+    if (attn_occ(1) == 3) {
+      if (pfq)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+    } else {
+      if (pfq)
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+    }
   } else if (attn_occ(1) == 3) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
                        (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);

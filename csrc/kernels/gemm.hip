@@ -301,11 +301,11 @@ __device__ __forceinline__ bf16x8 frag_mn(const __bf16* img, int c_img, int kk, 
 // Shared epilogue of the phased kernels: stage each wave's 128 x 64 accumulator tile (bf16) through
 // LDS, then EPI 0 = 16-byte row stores (+bias), EPI 1 = rotary + scatter into the attention storage.
 // All LDS operand reads and DMA must be retired by the caller (the whole 128 KiB is reused).
+// (wm, wn) = the wave's 128 x 64 block of the tile; ep = its private 16 KB of LDS
 template <int EPI>
-__device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16* smem, __bf16* __restrict__ C,
-                                                    const __bf16* __restrict__ bias, int N, int row0, int col0, int wave,
-                                                    int lane, const RopeEpi& rope) {
-  const int wm = wave >> 2, wn = wave & 3;
+__device__ __forceinline__ void gemm_store_epilogue_w(f32x4_t (&acc)[8][4], __bf16* ep, __bf16* __restrict__ C,
+                                                      const __bf16* __restrict__ bias, int N, int row0, int col0, int wm,
+                                                      int wn, int lane, const RopeEpi& rope) {
   const int fr = lane & 15, fq = lane >> 4;
   if constexpr (EPI == 5) {  // measurement only: main loop without the epilogue (results kept live)
     float t = 0.f;
@@ -318,7 +318,6 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
     if (N < 0) C[lane] = (__bf16)t;
     return;
   }
-  __bf16* ep = smem + wave * (128 * 64);
   // EPI 2: all 32 [value | gate] pre-activation loads of a lane (16 rows x 2 halves) are issued before
   // any math instead of the 8 a partially unrolled loop keeps in flight (the epilogue does not overlap
   // this workgroup's MFMA work, so its HBM latency is exposed once per tile)
@@ -454,6 +453,13 @@ __device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16
       else epi_store16(reinterpret_cast<s16x8*>(dstT + o), pack8(x), rope.nt);
     }
   }
+}
+
+template <int EPI>
+__device__ __forceinline__ void gemm_store_epilogue(f32x4_t (&acc)[8][4], __bf16* smem, __bf16* __restrict__ C,
+                                                    const __bf16* __restrict__ bias, int N, int row0, int col0, int wave,
+                                                    int lane, const RopeEpi& rope) {
+  gemm_store_epilogue_w<EPI>(acc, smem + wave * (128 * 64), C, bias, N, row0, col0, wave >> 2, wave & 3, lane, rope);
 }
 
 template <int EPI, int OPT>
@@ -834,6 +840,125 @@ bool gemm_nt(const void* A, const void* B, void* C, const void* bias, int M, int
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Two co-resident workgroups per CU (round 4; first built and measured in round 2 for plain stores,
+// profiles/r2_gemm_2wg_variant.hip.txt). A workgroup is 4 waves (2 x 2, each the 8-phase kernel's 128 x 64
+// output block) on a 256 x 128 tile, K-step 32, operands through a 3-slot LDS ring (24 KB per slot, 72 KB
+// per workgroup), so two workgroups fit on a CU (<= 256 VGPRs at 2 waves per SIMD, 144 KB of LDS) and one's
+// epilogue runs beside the other's MFMAs. Its simple main loop is ~25 % slower than the 8-phase one on plain
+// products (hence rejected there), but the GEGLU-backward epilogue (512 KB of HBM traffic per 256 x 256 of
+// output, serialised after the main loop in the one-workgroup-per-CU kernels) is what this structure hides.
+// LDS image: rows of 32 bf16 (64 B, 4 chunks of 16 B); physical chunk = logical ^ g((row >> 2) & 3),
+// g = {0, 2, 3, 1}: conflict-free for the ds_read_b128 lane groups of a 16-row fragment read.
+// ------------------------------------------------------------------------------------------------
+constexpr int W2_BM = 256, W2_BN = 128, W2_BK = 32;
+constexpr int W2_SLOT = (W2_BM + W2_BN) * W2_BK;  // elements per ring slot (A rows, then B rows)
+
+__device__ __forceinline__ int w2_swz(int r) {
+  const int q = (r >> 2) & 3;
+  return (0x1320 >> (4 * q)) & 3;  // g = {0, 2, 3, 1}
+}
+
+// one K-step of A (256 rows) and B (128 rows) into a ring slot: 24 pieces of 16 rows x 64 B, 6 per wave
+__device__ __forceinline__ void w2_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ B, int K, int row0,
+                                         int col0, int k0, __bf16* slot, int wave, int lane) {
+  const int pr = lane >> 2, pc = lane & 3;  // row within the piece, physical chunk
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int piece = wave * 6 + i;  // 0..15: A rows 16 piece.., 16..23: B rows 16 (piece - 16)..
+    const int r = piece * 16 + pr;   // image row (A rows 0-255, then B rows 256-383)
+    const int lc = pc ^ w2_swz(r);
+    const __bf16* g = piece < 16 ? A + (size_t)(row0 + r) * K + k0 + lc * 8
+                                 : B + (size_t)(col0 + r - W2_BM) * K + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                     (void __attribute__((address_space(3)))*)(slot + piece * 512), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 w2_frag(const __bf16* slot, int r, int fq) {
+  return *reinterpret_cast<const bf16x8*>(slot + r * W2_BK + ((fq ^ w2_swz(r)) << 3));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_2wg_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                             __bf16* __restrict__ C, const __bf16* __restrict__ bias, int M,
+                                                             int N, int K, RopeEpi rope, int group) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[3 * W2_SLOT];  // 72 KB, one array (see the 8-phase kernel)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  gemm_tile_of(tm, tn, M / W2_BM, N / W2_BN, group);
+  const int row0 = tm * W2_BM, col0 = tn * W2_BN;
+  const int fq = lane >> 4, fr = lane & 15;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / W2_BK;
+  w2_stage(A, B, K, row0, col0, 0, smem, wave, lane);
+  if (nk > 1) w2_stage(A, B, K, row0, col0, W2_BK, smem + W2_SLOT, wave, lane);
+  int slot = 0;  // ring slot of K-step t
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (t + 2 < nk) {
+      const int s2 = slot == 0 ? 2 : slot - 1;  // (t + 2) % 3 = the slot read at t - 1
+      w2_stage(A, B, K, row0, col0, (t + 2) * W2_BK, smem + s2 * W2_SLOT, wave, lane);
+    }
+    const __bf16* S = smem + slot * W2_SLOT;
+    bf16x8 a[8], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = w2_frag(S, W2_BM + wn * 64 + j * 16 + fr, fq);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = w2_frag(S, wm * 128 + i * 16 + fr, fq);
+    // first half of the MFMAs as soon as B and the first four A fragments are in (the other four
+    // A reads land under them)
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  gemm_store_epilogue_w<EPI>(acc, smem + wave * (128 * 64), C, bias, N, row0, col0, wm, wn, lane, rope);
+  if (rope.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// DALLE_AMD_GEGLU_BWD_2WG=1: the FF-out dgrad + GEGLU backward on the two-workgroup kernel (gemm_set_geglu_bwd_2wg)
+static int g_geglu_bwd_2wg = [] {
+  const char* s = getenv("DALLE_AMD_GEGLU_BWD_2WG");
+  return s ? atoi(s) : 0;
+}();
+void gemm_set_geglu_bwd_2wg(int v) { g_geglu_bwd_2wg = v; }
+
+// plain C = A B^T on the two-workgroup kernel (tests / benchmarks)
+bool gemm_2wg(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, hipStream_t st) {
+  if (M % W2_BM || N % W2_BN || K % W2_BK || K < 2 * W2_BK) return false;
+  RopeEpi e{};
+  const int nwg = (M / W2_BM) * (N / W2_BN);
+  hipLaunchKernelGGL((gemm_nt_2wg_kernel<0>), dim3(nwg), dim3(256), 0, st, (const __bf16*)A, (const __bf16*)B, (__bf16*)C,
+                     (const __bf16*)bias, M, N, K, e, 4);
+  return true;
+}
+
 // FF-out dgrad with the GEGLU backward in the epilogue: du = dy (M, K) . W2^T where w2t = W2^T (F, K)
 // bf16, then dh (M, 2F) = GEGLU'(h, du) and part ((M / 128), 2F) = partial FF-in bias grads. The
 // (M, F) du intermediate never exists.
@@ -853,6 +978,12 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   e.F = F;
   e.cpol = (size_t)M * F * 4 < (1ull << 32) ? gemm_cpol() : 0;  // buffer stores: 32-bit byte offsets
   e.drain = gemm_drain();
+  if (g_geglu_bwd_2wg && F % W2_BN == 0 && K % W2_BK == 0 && K >= 2 * W2_BK) {
+    const int nwg2 = (M / W2_BM) * (F / W2_BN);
+    hipLaunchKernelGGL((gemm_nt_2wg_kernel<2>), dim3(nwg2), dim3(256), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
+                       (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);
+    return true;
+  }
   const int nwg = (M / GBM) * (F / GBN);
   hipLaunchKernelGGL((gemm_nt_8ph_kernel<2, 0>), dim3(nwg), dim3(G_THREADS), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
                      (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);

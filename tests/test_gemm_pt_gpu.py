@@ -215,3 +215,27 @@ def test_line_stores_bitwise(cuda, persist):
     for a, b in zip(outs[0][1:], outs[1][1:]):
         assert a.shape == b.shape
         assert ((a.float() - b.float()).abs() <= 2 ** -7 * b.float().abs() + 1e-6).all()
+
+
+@pytest.mark.parametrize("M,F,K", [(512, 1024, 256), (2560, 4096, 1024)])
+def test_ff_dgrad_geglu_two_workgroup_bitwise(cuda, M, F, K):
+    """The two-workgroups-per-CU FF-out dgrad + GEGLU backward (gemm_set_geglu_bwd_2wg) walks K in the same
+    32-deep chunks as the 8-phase kernel and shares its epilogue: bitwise equal dh and bias partials. The
+    plain two-workgroup product against an fp32 reference."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(13)
+    dy = (torch.randn(M, K, device=cuda) * 0.5).bfloat16()
+    w2t = (torch.randn(F, K, device=cuda) * 0.03).bfloat16()
+    h = torch.randn(M, 2 * F, device=cuda).bfloat16()
+    try:
+        C.gemm_set_geglu_bwd_2wg(0)
+        dh0, db0 = C.ff_dgrad_geglu(dy, w2t, h)
+        C.gemm_set_geglu_bwd_2wg(1)
+        dh1, db1 = C.ff_dgrad_geglu(dy, w2t, h)
+    finally:
+        C.gemm_set_geglu_bwd_2wg(0)
+    assert torch.equal(dh0, dh1) and torch.equal(db0, db1)
+    got = C.gemm_2wg(dy, w2t)
+    assert _rel(got, dy.float() @ w2t.float().t()) < 5e-3
