@@ -1083,12 +1083,12 @@ static int attn_occ(int which) {
     else hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, st, __VA_ARGS__);                      \
   } while (0)
 
-// DALLE_AMD_ATTN_PF=<fwd>,<dq> (default 1,0): load phase B's first local key tile before phase A;
+// DALLE_AMD_ATTN_PF=<fwd>,<dq> (default 0,0; measured slower at occupancy 3: more spills): load phase B's first local key tile before phase A;
 // attn_set_pf overrides it at run time (benchmarks)
 static int g_attn_pf[2] = {-1, -1};
 static int attn_pf(int which) {
   if (g_attn_pf[0] < 0) {
-    int v[2] = {1, 0};
+    int v[2] = {0, 0};
     if (const char* e = getenv("DALLE_AMD_ATTN_PF")) sscanf(e, "%d,%d", &v[0], &v[1]);
     g_attn_pf[0] = v[0];
     g_attn_pf[1] = v[1];

@@ -815,12 +815,12 @@ static int g_gemm_prefetch = [] {
   return s ? atoi(s) : 0;
 }();
 void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
-// DALLE_AMD_PT_OVERLAP (default 1): persistent plain GEMMs (no bias) issue a tile's stores beside the next
+// DALLE_AMD_PT_OVERLAP (default 0; measured slower at every B128 shape): persistent plain GEMMs (no bias) issue a tile's stores beside the next
 // tile's first K-step (see gemm_pt_kernel phase 1); DALLE_AMD_PT_STAGGER=<percent of one tile>: start the
 // persistent workgroups at four phases so their epilogues do not all hit HBM at once
 static int g_pt_overlap = [] {
   const char* s = getenv("DALLE_AMD_PT_OVERLAP");
-  return s ? atoi(s) : 1;
+  return s ? atoi(s) : 0;
 }();
 static int g_pt_stagger = [] {
   const char* s = getenv("DALLE_AMD_PT_STAGGER");
