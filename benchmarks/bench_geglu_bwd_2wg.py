@@ -50,6 +50,12 @@ def main():
     t = run({"8ph": G(0), "2wg": G(1), "plain_hipblaslt": lambda: torch.mm(dy, w2t.t()), "plain_2wg": lambda: C.gemm_2wg(dy, w2t),
              "plain_8ph": lambda: C.gemm_nt(dy, w2t, None, 300)})
     print(json.dumps({"M": M, "F": F, "K": K, "us": t}), flush=True)
+    # start stagger of the co-resident workgroups (10 ns ticks; fw < 0: second slot delayed, > 0: 4-phase)
+    for ticks, fw in [(1500, -256), (2800, -256), (4000, -256), (1400, 512), (700, 512), (2800, -128)]:
+        C.gemm_set_2wg_stagger(ticks, fw)
+        t = run({"2wg": G(1), "plain_2wg": lambda: C.gemm_2wg(dy, w2t)}, rounds=5)
+        print(json.dumps({"stagger": ticks, "first_wave": fw, "us": t}), flush=True)
+    C.gemm_set_2wg_stagger(0, -256)
 
 
 if __name__ == "__main__":

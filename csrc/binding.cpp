@@ -84,6 +84,7 @@ void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
 void attn_set_pf(int, int);
 void gemm_set_geglu_bwd_2wg(int);
+void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
 int gemm_lines();
 void gemm_set_drain(int);
@@ -1208,6 +1209,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
   m.def("gemm_set_geglu_bwd_2wg", [](int64_t v) { dalle::gemm_set_geglu_bwd_2wg((int)v); }, py::arg("v"),
         "1: FF-out dgrad + GEGLU backward on the two-workgroups-per-CU kernel");
+  m.def("gemm_set_2wg_stagger", [](int64_t ticks, int64_t first_wave) { dalle::gemm_set_2wg_stagger((int)ticks, (int)first_wave); },
+        py::arg("ticks"), py::arg("first_wave") = -256,
+        "two-workgroup GEMM start stagger: 10 ns ticks; first_wave < 0 delays workgroups [-fw, -2 fw), > 0 is 4-phase");
   m.def("gemm_2wg", [](Tensor A, Tensor B) {
     CHECK_IN(A, torch::kBFloat16); CHECK_IN(B, torch::kBFloat16);
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_2wg: A (M, K), B (N, K)");

@@ -885,6 +885,20 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2wg_kernel(const __bf16* __res
                                                              __bf16* __restrict__ C, const __bf16* __restrict__ bias, int M,
                                                              int N, int K, RopeEpi rope, int group) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[3 * W2_SLOT];  // 72 KB, one array (see the 8-phase kernel)
+  // the two co-resident workgroups of a CU start in phase and would stay there (equal tiles), so their
+  // epilogues would coincide: first_wave < 0 delays the second slot's first workgroups ([-fw, -2 fw)) by
+  // `stagger` ticks; first_wave > 0 is the 4-phase start of stagger_start
+  if (rope.stagger > 0) {
+    if (rope.first_wave < 0) {
+      const int w0 = -rope.first_wave;
+      if ((int)blockIdx.x >= w0 && (int)blockIdx.x < 2 * w0) {
+        const unsigned long long until = __builtin_amdgcn_s_memrealtime() + (unsigned long long)rope.stagger;
+        while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
+      }
+    } else {
+      stagger_start(rope.stagger, rope.first_wave);
+    }
+  }
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   int tm, tn;
@@ -948,11 +962,27 @@ static int g_geglu_bwd_2wg = [] {
   return s ? atoi(s) : 0;
 }();
 void gemm_set_geglu_bwd_2wg(int v) { g_geglu_bwd_2wg = v; }
+// DALLE_AMD_2WG_STAGGER=<ticks>[,<first_wave>] (10 ns ticks; first_wave < 0: delay the second slot's first
+// workgroups, > 0: the 4-phase stagger_start over the first first_wave workgroups)
+static int g_2wg_stagger[2] = {-1, -256};
+static void w2_stagger(RopeEpi& e) {
+  if (g_2wg_stagger[0] < 0) {
+    g_2wg_stagger[0] = 0;
+    if (const char* s = getenv("DALLE_AMD_2WG_STAGGER")) sscanf(s, "%d,%d", &g_2wg_stagger[0], &g_2wg_stagger[1]);
+  }
+  e.stagger = g_2wg_stagger[0];
+  e.first_wave = g_2wg_stagger[1];
+}
+void gemm_set_2wg_stagger(int ticks, int first_wave) {
+  g_2wg_stagger[0] = ticks;
+  g_2wg_stagger[1] = first_wave;
+}
 
 // plain C = A B^T on the two-workgroup kernel (tests / benchmarks)
 bool gemm_2wg(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, hipStream_t st) {
   if (M % W2_BM || N % W2_BN || K % W2_BK || K < 2 * W2_BK) return false;
   RopeEpi e{};
+  w2_stagger(e);
   const int nwg = (M / W2_BM) * (N / W2_BN);
   hipLaunchKernelGGL((gemm_nt_2wg_kernel<0>), dim3(nwg), dim3(256), 0, st, (const __bf16*)A, (const __bf16*)B, (__bf16*)C,
                      (const __bf16*)bias, M, N, K, e, 4);
@@ -980,6 +1010,7 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   e.drain = gemm_drain();
   if (g_geglu_bwd_2wg && F % W2_BN == 0 && K % W2_BK == 0 && K >= 2 * W2_BK) {
     const int nwg2 = (M / W2_BM) * (F / W2_BN);
+    w2_stagger(e);
     hipLaunchKernelGGL((gemm_nt_2wg_kernel<2>), dim3(nwg2), dim3(256), 0, st, (const __bf16*)dy, (const __bf16*)w2t,
                        (__bf16*)nullptr, (const __bf16*)nullptr, M, F, K, e, 4);
     return true;
