@@ -137,6 +137,7 @@ static dalle::AttnGeom make_attn_geom(int T, int S, int n, int K, int H, int pat
   g.H = H;
   g.pattern = pattern;
   if (const char* e = getenv("DALLE_AMD_ATTN_DIAG")) g.diag = atoi(e);
+  if (const char* e = getenv("DALLE_AMD_ATTN_STAGGER")) g.stagger = atoi(e);
   TORCH_CHECK(g.I % 32 == 0, "image grid must be a multiple of 32 tokens");
   TORCH_CHECK(n == T + g.I - 1, "sequence length must be text_len + image_seq_len - 1");
   return g;

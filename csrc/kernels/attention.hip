@@ -156,6 +156,17 @@ __device__ __forceinline__ void xcd_remap(int& grp, int& bh) {
   grp = j - (j / ng) * ng;
 }
 
+// measurement (AttnGeom::stagger): equal-length workgroups launched together stay in lockstep, so the 3
+// co-resident workgroups of a CU would wait on memory at the same moments; delay the first 768 (slot
+// s = L >> 8 of the breadth-first dispatch) by s x ticks
+__device__ __forceinline__ void attn_stagger(const AttnGeom& g) {
+  if (g.stagger <= 0) return;
+  const int L = blockIdx.x + blockIdx.y * gridDim.x;
+  if (L >= 768) return;
+  const unsigned long long until = __builtin_amdgcn_s_memrealtime() + (unsigned long long)((L >> 8) * g.stagger);
+  while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
+}
+
 // first local (image) key tile needed by image query block qb
 __device__ __forceinline__ int local_lo_tile(const AttnGeom& g, int qb) {
   const int kq0 = qb * 32 - g.Tp;
@@ -371,6 +382,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
   int grp, bh;
   xcd_remap(grp, bh);
+  attn_stagger(g);
   const int b = bh / g.H, h = bh - b * g.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
@@ -567,6 +579,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   int grp, bh;
   xcd_remap(grp, bh);
+  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int qb0 = grp * 4;
@@ -785,6 +798,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
   __shared__ float stats[4][2][32];                                   // per wave {lse, delta}
   int grp, bh;
   xcd_remap(grp, bh);
+  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nkb = g.Np >> 5, ntext = g.Tp >> 5;
   const int kb = ntext + grp * 4 + wave;
@@ -907,6 +921,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
   __shared__ float stats[2][2][2][32];  // [stage][parity][lse | delta][row]
   int grp, bh;
   xcd_remap(grp, bh);
+  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int kb0 = grp * 2;

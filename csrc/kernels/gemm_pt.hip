@@ -504,6 +504,86 @@ __device__ __forceinline__ void pt_epilogue_geglu_lds(pt::f4 (&acc)[8][4], __bf1
   }
 }
 
+// FF-out dgrad + GEGLU backward (EPI 2) through LDS, one tile per workgroup (the LDS-staged epilogue of the
+// 8-phase kernel on this kernel's faster main loop): each wave parks its 128 x 64 du block (bf16, as the
+// unfused path rounds it) in its own 16 KB of the free operand LDS -- 8-byte writes of 4 consecutive columns,
+// 16-byte chunks XOR-swizzled by row -- then every lane owns one 8-column chunk of 16 rows: its 32
+// pre-activation loads ([value | gate] halves) are issued together, da = du * gelu(gate) and
+// dg = du * value * gelu'(gate) leave as whole 128-B lines (8 rows x 128 B per store instruction), and the
+// column sums of the bf16 results over each 64-row half are reduced over the 8 lanes sharing a chunk
+// (fixed xor tree) into part (M / 64, 2F).
+__device__ __forceinline__ void pt_epilogue_geglu_bwd_lds(pt::f4 (&acc)[8][4], __bf16* smem, int r0, int c0, int wm, int wn,
+                                                          int lane, const PtArgs& e) {
+  using namespace pt;
+  const int fr = lane & 15, q = lane >> 4;
+  const int F = e.F;
+  __bf16* ep = smem + (threadIdx.x >> 6) * (128 * 64);
+  asm volatile("s_barrier" ::: "memory");  // every wave is past its last operand read
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i * 16 + fr, c = j * 16 + q * 4;
+      *reinterpret_cast<uint2*>(ep + row * 64 + ((((c >> 3) ^ (row & 7)) << 3) | (c & 7))) =
+          uint2{pk2(acc[i][j][0], acc[i][j][1]), pk2(acc[i][j][2], acc[i][j][3])};
+    }
+  const int ch = lane & 7;
+  const int gcol = c0 + wn * 64 + ch * 8;
+  const size_t rw = (size_t)(r0 + wm * 128);
+  s16x8 hv[16], hg[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const size_t r = rw + it * 8 + (lane >> 3);
+    hv[it] = *reinterpret_cast<const s16x8*>(e.h + r * 2 * F + gcol);
+    hg[it] = *reinterpret_cast<const s16x8*>(e.h + r * 2 * F + F + gcol);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's image is complete
+  const pt::Out od(e.dh, e.cpol);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    float sv[8] = {}, sg[8] = {};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int it = half * 8 + k;
+      const int row = it * 8 + (lane >> 3);
+      const size_t r = rw + row;
+      float d[8], a[8], gg[8], da[8], dg[8];
+      unpack8(*reinterpret_cast<const s16x8*>(ep + row * 64 + ((ch ^ (row & 7)) << 3)), d);
+      unpack8(hv[it], a);
+      unpack8(hg[it], gg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float ge, gr;
+        gelu_and_grad(gg[i], ge, gr);
+        da[i] = d[i] * ge;
+        dg[i] = d[i] * a[i] * gr;
+      }
+      const s16x8 pa = pack8(da), pg = pack8(dg);
+      od.st4(e.dh + r * 2 * F + gcol, __builtin_bit_cast(u32x4_vs, pa));
+      od.st4(e.dh + r * 2 * F + F + gcol, __builtin_bit_cast(u32x4_vs, pg));
+      unpack8(pa, da);
+      unpack8(pg, dg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sv[i] += da[i]; sg[i] += dg[i]; }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sv[i] += __shfl_xor(sv[i], o, 64);
+        sg[i] += __shfl_xor(sg[i], o, 64);
+      }
+    if (lane < 8) {
+      float* pr = e.part + ((rw + half * 64) >> 6) * 2 * F + gcol;
+      *reinterpret_cast<f4*>(pr) = f4{sv[0], sv[1], sv[2], sv[3]};
+      *reinterpret_cast<f4*>(pr + 4) = f4{sv[4], sv[5], sv[6], sv[7]};
+      *reinterpret_cast<f4*>(pr + F) = f4{sg[0], sg[1], sg[2], sg[3]};
+      *reinterpret_cast<f4*>(pr + F + 4) = f4{sg[4], sg[5], sg[6], sg[7]};
+    }
+  }
+}
+
 // PERSIST = false: one tile per workgroup (grid = tile count), the same main loop and register-direct
 // epilogue -- a workgroup's stores then drain while the NEXT workgroup on that CU already streams its
 // first K-tiles (the epilogue ends with the store issue; nothing waits for completion)
@@ -714,6 +794,7 @@ __global__ __launch_bounds__(pt::THREADS, 1) void gemm_pt_kernel(const __bf16* _
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
   const unsigned long long t_epi = __builtin_amdgcn_s_memrealtime();
   if constexpr (EPI == 3 && LINES && !PERSIST) pt_epilogue_geglu_lds(acc, smem, pr, pc, wm, wn, lane, e);
+  else if constexpr (EPI == 2 && LINES && !PERSIST) pt_epilogue_geglu_bwd_lds(acc, smem, pr, pc, wm, wn, lane, e);
   else pt_epilogue<EPI, LINES>(acc, pr, pc, wm, wn, lane, e);
   if (e.drain && e.stamps == nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!PERSIST && e.stamps != nullptr) {

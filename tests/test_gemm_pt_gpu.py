@@ -100,6 +100,11 @@ def test_ff_dgrad_geglu_pt(cuda, M, F, K, persist):
     dh, db = C.ff_dgrad_geglu_pt(dy, w2t, h, None, persist)
     dh_old, db_old = C.ff_dgrad_geglu(dy, w2t, h)
     assert _rel(dh, dh_old) < 1e-2 and _rel(db, db_old) < 1e-2
+    if persist == 0:
+        # one tile per workgroup: the 8-phase kernel's LDS-staged epilogue on the same bf16 du -- equal up to
+        # the compiler's contraction of the GELU multiply-adds (one bf16 ulp); bias sums in another order
+        assert ((dh.float() - dh_old.float()).abs() <= 2 ** -7 * dh_old.float().abs() + 1e-6).all()
+        assert _rel(db, db_old) < 1e-5
     hf = h.float().requires_grad_(True)
     out = hf[:, :F] * torch.nn.functional.gelu(hf[:, F:])
     out.backward(dy.float() @ w2.to(torch.bfloat16).float())
