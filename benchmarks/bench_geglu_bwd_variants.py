@@ -43,6 +43,15 @@ def main():
              "pt_persist": lambda: C.ff_dgrad_geglu_pt(dy, w2t, h, None, 1),
              "plain_hipblaslt": lambda: torch.mm(dy, w2t.t()), "pt_mainloop": lambda: C.gemm_pt(dy, w2t, None, 35, 0)})
     print(json.dumps({"M": M, "F": F, "K": K, "us": t}), flush=True)
+    del dy, w2t, h
+    # FF-in + GEGLU forward: hipBLASLt addmm + the GEGLU pass (default) vs the register-epilogue kernel one
+    # tile per workgroup (GEGLU through LDS) and persistent
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w1i = (0.03 * torch.randn(2 * F, K, device=dev)).bfloat16()
+    b1i = (0.1 * torch.randn(2 * F, device=dev)).bfloat16()
+    t = run({"hipblaslt_geglu": lambda: C.geglu_fwd(torch.addmm(b1i, x, w1i.t())),
+             "pt_tile_lds": lambda: C.ff_in_geglu_pt(x, w1i, b1i, 0), "pt_persist": lambda: C.ff_in_geglu_pt(x, w1i, b1i, 1)})
+    print(json.dumps({"op": "ff_in_geglu", "M": M, "F": F, "K": K, "us": t}), flush=True)
 
 
 if __name__ == "__main__":

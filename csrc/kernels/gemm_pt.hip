@@ -431,9 +431,10 @@ __device__ __forceinline__ void pt_epilogue(pt::f4 (&acc)[8][4], int r0, int c0,
 // FF-in + GEGLU forward (EPI 3) with whole-line stores, one tile per workgroup: after the main loop the
 // 128 KiB of operand LDS is free, so the tile goes out through it. Pass 1 writes value and gate (bf16, 8 B
 // per lane: 4 consecutive features) into two [256 rows][128 features] images whose 16-byte chunks are
-// XOR-swizzled by row (c ^ (row & 15): the 16 lanes of a write group hit 16 distinct chunks), pass 2 the
-// products u = value * gelu(gate) (computed in registers in pass 1); each read-back instruction covers 4 whole
-// rows x 256 B, so every global store writes whole 128-B lines of a (value | gate halves) and u.
+// XOR-swizzled by row (c ^ (row & 15): the 16 lanes of a write group hit 16 distinct chunks); pass 2 reads
+// them back (each instruction covers 4 whole rows x 256 B) and stores whole 128-B lines of a (value | gate
+// halves) and of u = value * gelu(gate), computed there from the same bf16 values (one barrier in all;
+// round 3 held u in registers through pass 1 and needed a third LDS pass).
 __device__ __forceinline__ int geglu_lds_idx(int row, int feat) {
   return row * 128 + ((((feat >> 3) ^ (row & 15)) << 3) | (feat & 7));
 }
@@ -458,9 +459,8 @@ __device__ __forceinline__ void pt_epilogue_geglu_lds(pt::f4 (&acc)[8][4], __bf1
     }
   }
   __bf16* V = smem;              // [256][128] value image
-  __bf16* G = smem + 256 * 128;  // [256][128] gate image, later the u image lives in V
+  __bf16* G = smem + 256 * 128;  // [256][128] gate image
   asm volatile("s_barrier" ::: "memory");  // every wave is past its last operand read
-  unsigned uu[8][2][2];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = wm * 128 + i * 16 + fr;
@@ -470,14 +470,14 @@ __device__ __forceinline__ void pt_epilogue_geglu_lds(pt::f4 (&acc)[8][4], __bf1
       const unsigned v1 = pk2(acc[i][j][2] + bv[j][2], acc[i][j][3] + bv[j][3]);
       const unsigned g0 = pk2(acc[i][j + 2][0] + bv[j + 2][0], acc[i][j + 2][1] + bv[j + 2][1]);
       const unsigned g1 = pk2(acc[i][j + 2][2] + bv[j + 2][2], acc[i][j + 2][3] + bv[j + 2][3]);
-      uu[i][j][0] = pk2(lo_f(v0) * gelu_fast(lo_f(g0)), hi_f(v0) * gelu_fast(hi_f(g0)));
-      uu[i][j][1] = pk2(lo_f(v1) * gelu_fast(lo_f(g1)), hi_f(v1) * gelu_fast(hi_f(g1)));
       const int feat = wn * 32 + j * 16 + q * 4;
       *reinterpret_cast<uint2*>(V + geglu_lds_idx(row, feat)) = uint2{v0, v1};
       *reinterpret_cast<uint2*>(G + geglu_lds_idx(row, feat)) = uint2{g0, g1};
     }
   }
   __syncthreads();
+  // one pass: each thread takes an 8-feature chunk of one row, stores its value and gate lines and the
+  // product u = value * gelu(gate) of the same (bf16) values
   const pt::Out oa(e.a, e.cpol), ou(e.u, e.cpol);
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
@@ -488,18 +488,10 @@ __device__ __forceinline__ void pt_epilogue_geglu_lds(pt::f4 (&acc)[8][4], __bf1
     __bf16* ap = e.a + (size_t)(r0 + row) * 2 * F + fw + ch * 8;
     oa.st4(ap, vv);
     oa.st4(ap + F, gg);
-  }
-  __syncthreads();
+    u32x4_vs uv;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      *reinterpret_cast<uint2*>(V + geglu_lds_idx(wm * 128 + i * 16 + fr, wn * 32 + j * 16 + q * 4)) = uint2{uu[i][j][0], uu[i][j][1]};
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int idx = it * 512 + tid, row = idx >> 4, ch = idx & 15;
-    const u32x4_vs uv = *reinterpret_cast<const u32x4_vs*>(V + row * 128 + ((ch ^ (row & 15)) << 3));
+    for (int k = 0; k < 4; ++k)
+      uv[k] = pk2(lo_f(vv[k]) * gelu_fast(lo_f(gg[k])), hi_f(vv[k]) * gelu_fast(hi_f(gg[k])));
     ou.st4(e.u + (size_t)(r0 + row) * F + fw + ch * 8, uv);
   }
 }

@@ -248,6 +248,9 @@ FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "2"))
 FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
 # GEGLU backward fused into the FF-out dgrad GEMM epilogue (csrc/kernels/gemm.hip EPI 2)
 FUSED_GEGLU_DGRAD = int(os.environ.get("DALLE_AMD_FUSED_GEGLU_DGRAD", "1"))
+# which kernel runs it: "8ph" (gemm.hip, LDS-staged epilogue) or "pt" (gemm_pt.hip main loop, one tile per
+# workgroup, the same LDS-staged epilogue: pt_epilogue_geglu_bwd_lds)
+GEGLU_DGRAD_KERNEL = os.environ.get("DALLE_AMD_GEGLU_DGRAD_KERNEL", "8ph")
 
 
 # weight-grad inputs kept token-contiguous: the LN outputs feeding the QKV and FF-in GEMMs are saved as
@@ -750,7 +753,10 @@ def _ff_core_bwd(saved, params, dy, sk):
     M, F = dy.shape[0], w2b.shape[1]
     if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
-        da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
+        if GEGLU_DGRAD_KERNEL == "pt" and dy.shape[1] >= 128:
+            da, db1 = C().ff_dgrad_geglu_pt(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None, 0)
+        else:
+            da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
         _count("ff_dgrad_geglu")
         dw2 = _wgrad(w2, saved_gemm_input(dy, WGRAD_GT), u)
     else:
