@@ -100,8 +100,10 @@ __global__ __launch_bounds__(256) void ln_shift_fwd_kernel(const float* __restri
 // sublayer's LayerScale residual, so the same pass emits its dy_prev = bf16(scale_prev * dx) and the
 // column partials [sum dx * y_prev | sum dx] (-> dscale_prev, dbias_prev) into part2 -- no separate
 // scale_residual_bwd re-reading dx.
+// D <= 1024: held to 256 VGPRs (2 waves per SIMD; the SR form compiled to 258 = 1 wave per SIMD without the
+// bound, half the rows in flight of the bandwidth-bound pass)
 template <int D, bool SR = false>
-__global__ __launch_bounds__(256) void ln_shift_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256, D <= 1024 ? 2 : 1) void ln_shift_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const __bf16* __restrict__ dy, const float* __restrict__ mean_in,
                                                            const float* __restrict__ rstd_in, const float* __restrict__ resid,
                                                            float* __restrict__ dx, float* __restrict__ dw, ShiftGeom g,
