@@ -83,6 +83,7 @@ void gemm_set_lines(int);
 void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
 void attn_set_pf(int, int);
+void attn_set_dkdv_qt(int);
 void gemm_set_geglu_bwd_2wg(int);
 void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
@@ -1221,6 +1222,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
     return C;
   });
+  m.def("attn_set_dkdv_qt", [](int64_t qt) { dalle::attn_set_dkdv_qt((int)qt); }, py::arg("qt"),
+        "query tiles per barrier step of the text dK/dV kernel: 2 (default) or 4");
   m.def("attn_set_pf", [](int64_t f, int64_t q) { dalle::attn_set_pf((int)f, (int)q); }, py::arg("fwd"), py::arg("dq"),
         "attention forward / dQ: load the first local key tile before the text phase (1) or after it (0)");
   m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },

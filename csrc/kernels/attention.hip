@@ -910,15 +910,17 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
 // workgroup) while the critical path stays at half the query tiles. The two parity partials of each
 // key block are summed through LDS at the end (fixed order, deterministic).
 // ------------------------------------------------------------------------------------------------
-template <int MINB>
+template <int MINB, int QT = 2>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                                     const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                                     __bf16* __restrict__ dK, __bf16* __restrict__ dV, AttnGeom g,
                                                                     RopeOut ro) {
-  // 2 stages x 2 parities x {Q, dO} tile images (32 KB) + the per-query stats
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 2 * TILE];
-  __shared__ float stats[2][2][2][32];  // [stage][parity][lse | delta][row]
+  // QT query tiles per step (2: one per parity; 4: two per parity, half the steps and barriers):
+  // 2 stages x QT x {Q, dO} tile images + the per-query stats
+  static_assert(QT == 2 || QT == 4, "QT");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * QT * 2 * TILE];
+  __shared__ float stats[2][QT][2][32];  // [stage][tile][lse | delta][row]
   int grp, bh;
   xcd_remap(grp, bh);
   attn_stagger(g);
@@ -938,38 +940,38 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
 #pragma unroll
     for (int s = 0; s < 4; ++s) { kf[s] = ld16(kp + 16 * s); vf[s] = ld16(vp + 16 * s); }
   }
-  // query tiles kb0 .. nqb-1, two per step (parity 0: kb0 + 2i, parity 1: kb0 + 2i + 1)
-  const int nsteps = (nqb - kb0 + 1) >> 1;
-  // staging: thread tid moves chunk (row, col) of Q and dO of both parity tiles
+  // query tiles kb0 .. nqb-1, QT per step: tile t of step i is kb0 + QT i + t, handled by the waves of
+  // parity t & 1
+  const int nsteps = (nqb - kb0 + QT - 1) / QT;
+  // staging: thread tid moves chunk (row, col) of Q and dO of every tile of the step
   const int st_row = (tid & 255) >> 3, st_col = (tid & 7) * 8;
   const int st_off = lds_idx(st_row, st_col);
-  s16x8 sreg[4];  // Q0, dO0, Q1, dO1
-  float sl = 0.f, sd = 0.f;
+  s16x8 sreg[2 * QT];  // Q0, dO0, Q1, dO1, ...
+  float sl = 0.f;
   auto load_step = [&](int i) {
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const int qt = min(kb0 + 2 * i + pp, nqb - 1);
+    for (int pp = 0; pp < QT; ++pp) {
+      const int qt = min(kb0 + QT * i + pp, nqb - 1);
       const size_t off = base + (size_t)(qt * 32 + st_row) * 64 + st_col;
       sreg[2 * pp] = *reinterpret_cast<const s16x8*>(Q + off);
       sreg[2 * pp + 1] = ld_tok(dob, tok_row(g, qt * 32 + st_row), st_col);
     }
-    if (tid < 128) {  // lse / delta rows of both tiles: 2 parities x 2 stats x 32
+    if (tid < QT * 64) {  // lse / delta rows of every tile: QT x 2 stats x 32
       const int pp = tid >> 6, which = (tid >> 5) & 1, r = tid & 31;
-      const int qt = min(kb0 + 2 * i + pp, nqb - 1);
+      const int qt = min(kb0 + QT * i + pp, nqb - 1);
       const float* src = which ? delta : lse;
       sl = src[(size_t)bh * g.Np + qt * 32 + r];
     }
   };
   auto store_step = [&](int buf) {
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      __bf16* T0 = smem + (buf * 2 + pp) * (2 * TILE);
+    for (int pp = 0; pp < QT; ++pp) {
+      __bf16* T0 = smem + (buf * QT + pp) * (2 * TILE);
       *reinterpret_cast<s16x8*>(T0 + st_off) = sreg[2 * pp];
       *reinterpret_cast<s16x8*>(T0 + TILE + st_off) = sreg[2 * pp + 1];
     }
-    if (tid < 128) stats[buf][tid >> 6][(tid >> 5) & 1][tid & 31] = sl;
+    if (tid < QT * 64) stats[buf][tid >> 6][(tid >> 5) & 1][tid & 31] = sl;
   };
-  (void)sd;
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   if (nsteps > 0) {
     load_step(0);
@@ -980,43 +982,47 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
     const bool more = i + 1 < nsteps && !(g.diag & 8);
     if (more) load_step(i + 1);
     const int buf = i & 1;
-    const int qt = kb0 + 2 * i + par;
-    if (active && qt < nqb && qt >= kb) {
-      const __bf16* Qs = smem + (buf * 2 + par) * (2 * TILE);
-      const __bf16* Ds = Qs + TILE;
-      f32x16 sc = {}, dp = {};
 #pragma unroll
-      for (int ss = 0; ss < 4; ++ss) {
-        sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
-        dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
-      }
-      f32x16 ds;
+    for (int u = 0; u < QT / 2; ++u) {
+      const int tt = par + 2 * u;
+      const int qt = kb0 + QT * i + tt;
+      if (active && qt < nqb && qt >= kb) {
+        const __bf16* Qs = smem + (buf * QT + tt) * (2 * TILE);
+        const __bf16* Ds = Qs + TILE;
+        f32x16 sc = {}, dp = {};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = acc_row(r, hl);
-        const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[buf][par][0][ql]));
-        sc[r] = pr;
-        ds[r] = pr * (dp[r] - stats[buf][par][1][ql]);
-      }
-      if (!tile_full(g, qt, kb)) {
-        const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+        for (int ss = 0; ss < 4; ++ss) {
+          sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
+          dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
+        }
+        f32x16 ds;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const bool on = mask_bit(mh, r);
-          sc[r] = on ? sc[r] : 0.f;
-          ds[r] = on ? ds[r] : 0.f;
+          const int ql = acc_row(r, hl);
+          const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[buf][tt][0][ql]));
+          sc[r] = pr;
+          ds[r] = pr * (dp[r] - stats[buf][tt][1][ql]);
         }
+        if (!tile_full(g, qt, kb)) {
+          const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const bool on = mask_bit(mh, r);
+            sc[r] = on ? sc[r] : 0.f;
+            ds[r] = on ? ds[r] : 0.f;
+          }
+        }
+        const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
+        const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
+        dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
+        dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
+        dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
+        dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
+        dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
+        dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
+        dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
+        dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
       }
-      const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
-      const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
-      dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
-      dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
-      dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
-      dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
-      dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
-      dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
-      dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
-      dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
     }
     if (more) store_step((i + 1) & 1);
     if (!(g.diag & 16)) __syncthreads();
@@ -1110,6 +1116,17 @@ static int attn_pf(int which) {
   }
   return g_attn_pf[which];
 }
+// DALLE_AMD_DKDV_QT=2|4: query tiles staged per barrier step of the text dK/dV kernel (attn_set_dkdv_qt
+// overrides it at run time)
+static int g_dkdv_qt = -1;
+static int attn_dkdv_qt() {
+  if (g_dkdv_qt < 0) {
+    const char* e = getenv("DALLE_AMD_DKDV_QT");
+    g_dkdv_qt = (e && atoi(e) == 4) ? 4 : 2;
+  }
+  return g_dkdv_qt;
+}
+void attn_set_dkdv_qt(int qt) { g_dkdv_qt = qt == 4 ? 4 : 2; }
 void attn_set_pf(int fwd, int dq) {
   g_attn_pf[0] = fwd;
   g_attn_pf[1] = dq;
@@ -1162,8 +1179,12 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   auto launch_dkdv = [&](hipStream_t s2) {
     // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
     hipStream_t st = s2;
-    ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
-                (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+    if (attn_dkdv_qt() == 4 && attn_occ(2) == 2)
+      hipLaunchKernelGGL((attn_bwd_dkdv_text_kernel<2, 4>), dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q,
+                         (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+    else
+      ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
+                  (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
     // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
     if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                 (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);

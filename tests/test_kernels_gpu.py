@@ -449,3 +449,30 @@ def test_weight_grad_token_contiguous_input(cuda, M, N, K, fused, form):
     r2 = hip_ops.weight_grad(w, g, x)
     got2 = w.grad if fused else r2
     assert _rel(got, got2) < 1e-5
+
+
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like"])
+def test_text_dkdv_four_tiles_per_step_bitwise(cuda, attn_type):
+    """The text dK/dV kernel staging four query tiles per barrier step (attn_set_dkdv_qt(4)) walks each
+    wave's query tiles in the same order as the two-tile form: bitwise-identical gradients."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(9)
+    T, S, B, H = 257, 32, 2, 3
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
+    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
+    grads = []
+    try:
+        for qt in (2, 4):
+            C.attn_set_dkdv_qt(qt)
+            x = qkv.clone().requires_grad_(True)
+            hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+            torch.cuda.synchronize()
+            grads.append(x.grad.clone())
+    finally:
+        C.attn_set_dkdv_qt(2)
+    assert torch.isfinite(grads[0].float()).all()
+    assert torch.equal(grads[0], grads[1]), attn_type
