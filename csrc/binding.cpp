@@ -84,6 +84,7 @@ void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
 void attn_set_pf(int, int);
 void attn_set_dkdv_qt(int);
+void attn_set_fwd_tps(int);
 void gemm_set_geglu_bwd_2wg(int);
 void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
@@ -1222,6 +1223,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
     return C;
   });
+  m.def("attn_set_fwd_tps", [](int64_t t) { dalle::attn_set_fwd_tps((int)t); }, py::arg("tps"),
+        "text tiles per barrier step of the attention forward: 2 (default) or 3");
   m.def("attn_set_dkdv_qt", [](int64_t qt) { dalle::attn_set_dkdv_qt((int)qt); }, py::arg("qt"),
         "query tiles per barrier step of the text dK/dV kernel: 2 (default) or 4");
   m.def("attn_set_pf", [](int64_t f, int64_t q) { dalle::attn_set_pf((int)f, (int)q); }, py::arg("fwd"), py::arg("dq"),

@@ -375,11 +375,13 @@ __device__ __forceinline__ void fwd_tiles(SoftmaxState& st, const __bf16* const 
 //   (double-buffered 2 x {Ka, Kb, Va, Vb}, register-staged loads issued before compute, T14).
 // Phase B (wave-private): each image query block streams ITS OWN local key tiles through a private
 //   LDS slot (reusing phase A's buffers) -- no workgroup barrier, no wave idling on other blocks' tiles.
-template <int MINB, bool PREFETCH_LOCAL = true>
+// TPS: text tiles staged per barrier step (2: 32 KB of LDS; 3: 48 KB, 3 steps instead of 5 for 9 text tiles)
+template <int MINB, bool PREFETCH_LOCAL = true, int TPS = 2>
 __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                           const __bf16* __restrict__ V, __bf16* __restrict__ out,
                                                           float* __restrict__ lse, AttnGeom g) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
+  static_assert(TPS == 2 || TPS == 3, "TPS");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TPS * TILE];  // 32 / 48 KB
   int grp, bh;
   xcd_remap(grp, bh);
   attn_stagger(g);
@@ -398,7 +400,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   bf16x8 qf[4];
   // this wave's Q tile (32 contiguous rows) by LDS-DMA into buffer 1, which the loop first refills at
   // step 0: 4 coalesced 1 KiB pieces instead of per-lane row reads that touch 32 lines per instruction
-  dma_tile_wave(Q + base + (size_t)(active ? qb : 0) * 32 * 64, smem + 4 * TILE + wave * TILE, lane);
+  dma_tile_wave(Q + base + (size_t)(active ? qb : 0) * 32 * 64, smem + 2 * TPS * TILE + wave * TILE, lane);
   SoftmaxState st;
   // phase B's first local (image) key tile, loaded NOW into registers: its HBM latency then hides under
   // phase A instead of being exposed after the last text pair (each local tile is read by one query tile)
@@ -416,42 +418,49 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   };
   if (has_local && PREFETCH_LOCAL) load_loc(lo);
 
-  // ---- phase A: shared text tiles, two per step ----
-  const int npairs = (n_text + 1) >> 1;
-  // {Ka, Kb, Va, Vb} of a pair step by LDS-DMA straight into buffer `buf` (dma_tile)
-  auto dma_pair = [&](int pi, int buf) {
-    const int ta = 2 * pi, tb = min(2 * pi + 1, n_text - 1);
-    __bf16* S0 = smem + buf * (4 * TILE);
-    dma_tile(Kt + base + (size_t)ta * 32 * 64, S0, wave, lane);
-    dma_tile(Kt + base + (size_t)tb * 32 * 64, S0 + TILE, wave, lane);
-    dma_tile(V + base + (size_t)ta * 32 * 64, S0 + 2 * TILE, wave, lane);
-    dma_tile(V + base + (size_t)tb * 32 * 64, S0 + 3 * TILE, wave, lane);
+  // ---- phase A: shared text tiles, TPS per step ----
+  const int nsteps = (n_text + TPS - 1) / TPS;
+  // K tiles then V tiles of a step by LDS-DMA straight into buffer `buf` (dma_tile)
+  auto dma_step = [&](int si, int buf) {
+    __bf16* S0 = smem + buf * (2 * TPS * TILE);
+#pragma unroll
+    for (int t = 0; t < TPS; ++t) {
+      const int tt = min(TPS * si + t, n_text - 1);
+      dma_tile(Kt + base + (size_t)tt * 32 * 64, S0 + t * TILE, wave, lane);
+      dma_tile(V + base + (size_t)tt * 32 * 64, S0 + (TPS + t) * TILE, wave, lane);
+    }
   };
-  dma_pair(0, 0);
+  dma_step(0, 0);
   __builtin_amdgcn_s_waitcnt(WAIT_VM0);
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = row_operand(smem + 4 * TILE + wave * TILE, s, c32, hl);
+  for (int s = 0; s < 4; ++s) qf[s] = row_operand(smem + 2 * TPS * TILE + wave * TILE, s, c32, hl);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Q is in registers before step 0 refills buffer 1
   __syncthreads();
-  for (int pi = 0; pi < npairs; ++pi) {
-    const bool more = pi + 1 < npairs && !(g.diag & 1);
-    if (more) dma_pair(pi + 1, (pi + 1) & 1);  // that buffer was released by the previous step's barrier
-    const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
-    const int ta = 2 * pi, tb = 2 * pi + 1;
+  for (int si = 0; si < nsteps; ++si) {
+    const bool more = si + 1 < nsteps && !(g.diag & 1);
+    if (more) dma_step(si + 1, (si + 1) & 1);  // that buffer was released by the previous step's barrier
+    const __bf16* S0 = smem + (si & 1) * (2 * TPS * TILE);
+    const int ta = TPS * si, tb = ta + 1;
     if (g.diag & 32) {
     } else if (tb < my_text_end) {
       const __bf16* const Ks[2] = {S0, S0 + TILE};
-      const __bf16* const Vs[2] = {S0 + 2 * TILE, S0 + 3 * TILE};
+      const __bf16* const Vs[2] = {S0 + TPS * TILE, S0 + (TPS + 1) * TILE};
       const int kt[2] = {ta, tb};
       fwd_tiles<2>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     } else if (ta < my_text_end) {
       const __bf16* const Ks[1] = {S0};
-      const __bf16* const Vs[1] = {S0 + 2 * TILE};
+      const __bf16* const Vs[1] = {S0 + TPS * TILE};
       const int kt[1] = {ta};
       fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
-    __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next pair landed (this wave's pieces) before the barrier
+    if (TPS == 3 && !(g.diag & 32) && ta + 2 < my_text_end) {
+      const __bf16* const Ks[1] = {S0 + 2 * TILE};
+      const __bf16* const Vs[1] = {S0 + (TPS + 2) * TILE};
+      const int kt[1] = {ta + 2};
+      fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
+    }
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next step's tiles landed (this wave's pieces) before the barrier
     if (!(g.diag & 2)) __syncthreads();
   }
 
@@ -1116,6 +1125,16 @@ static int attn_pf(int which) {
   }
   return g_attn_pf[which];
 }
+// DALLE_AMD_ATTN_FWD_TPS=2|3: text tiles staged per barrier step of the forward (attn_set_fwd_tps overrides)
+static int g_fwd_tps = -1;
+static int attn_fwd_tps() {
+  if (g_fwd_tps < 0) {
+    const char* e = getenv("DALLE_AMD_ATTN_FWD_TPS");
+    g_fwd_tps = (e && atoi(e) == 3) ? 3 : 2;
+  }
+  return g_fwd_tps;
+}
+void attn_set_fwd_tps(int t) { g_fwd_tps = t == 3 ? 3 : 2; }
 // DALLE_AMD_DKDV_QT=2|4: query tiles staged per barrier step of the text dK/dV kernel (attn_set_dkdv_qt
 // overrides it at run time)
 static int g_dkdv_qt = -1;
@@ -1135,12 +1154,15 @@ void attn_set_pf(int fwd, int dq) {
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
   dim3 grid((g.Np / 32 + 3) / 4, BH);
   const bool pf = attn_pf(0) != 0;
+  const bool t3 = !pf && attn_fwd_tps() == 3;
   const __bf16 *qq = (const __bf16*)q, *kk = (const __bf16*)k, *vv = (const __bf16*)v;
   if (attn_occ(0) == 3) {
     if (pf) hipLaunchKernelGGL((attn_fwd_kernel<3, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+    else if (t3) hipLaunchKernelGGL((attn_fwd_kernel<3, false, 3>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
     else hipLaunchKernelGGL((attn_fwd_kernel<3, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
   } else {
     if (pf) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
+    else if (t3) hipLaunchKernelGGL((attn_fwd_kernel<2, false, 3>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
     else hipLaunchKernelGGL((attn_fwd_kernel<2, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
   }
 }

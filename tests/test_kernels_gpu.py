@@ -476,3 +476,27 @@ def test_text_dkdv_four_tiles_per_step_bitwise(cuda, attn_type):
         C.attn_set_dkdv_qt(2)
     assert torch.isfinite(grads[0].float()).all()
     assert torch.equal(grads[0], grads[1]), attn_type
+
+
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
+def test_attention_forward_three_tiles_per_step(cuda, attn_type):
+    """The forward staging three text tiles per barrier step (attn_set_fwd_tps(3)) regroups the online-softmax
+    updates only: same output and log-sum-exp up to fp32 rounding of the rescaled accumulators."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(10)
+    T, S, B, H = 257, 32, 2, 3
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
+    outs = []
+    try:
+        for tps in (2, 3):
+            C.attn_set_fwd_tps(tps)
+            outs.append(hip_ops.attention_core(qkv, H, geom, attn_type).float())
+            torch.cuda.synchronize()
+    finally:
+        C.attn_set_fwd_tps(2)
+    assert torch.isfinite(outs[1]).all()
+    assert _rel(outs[0], outs[1]) < 2e-3, attn_type
