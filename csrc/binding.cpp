@@ -85,6 +85,7 @@ void gemm_set_pt_overlap(int, int);
 void attn_set_pf(int, int);
 void attn_set_dkdv_qt(int);
 void attn_set_fwd_tps(int);
+void attn_set_dq_stage(int);
 void gemm_set_geglu_bwd_2wg(int);
 void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
@@ -1223,6 +1224,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
     return C;
   });
+  m.def("attn_set_dq_stage", [](int64_t v) { dalle::attn_set_dq_stage((int)v); }, py::arg("stage"),
+        "dQ kernel text staging: 0 register pairs (default), 2 / 3 LDS-DMA tiles per barrier step");
   m.def("attn_set_fwd_tps", [](int64_t t) { dalle::attn_set_fwd_tps((int)t); }, py::arg("tps"),
         "text tiles per barrier step of the attention forward: 2 (default) or 3");
   m.def("attn_set_dkdv_qt", [](int64_t qt) { dalle::attn_set_dkdv_qt((int)qt); }, py::arg("qt"),

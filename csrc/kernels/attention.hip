@@ -578,13 +578,17 @@ __device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* 
 // query tile -- its own row's (column's) -- so that tile's dK / dV are produced right here, by the wave
 // that owns the query tile, from the K / V it already staged and the Q / dO it already holds: the
 // separate image-key dK/dV kernel (a launch that re-read Q, dO, K and V of every local tile) disappears.
-template <int MINB, bool FUSE_LOCAL, bool PREFETCH_LOCAL = false>
+// STAGE: 0 = text tiles register-staged two per barrier step (round 1-3 form); 2 / 3 = LDS-DMA'd (no
+// staging VGPRs, no ds_write) two / three per step (the forward's scheme)
+template <int MINB, bool FUSE_LOCAL, bool PREFETCH_LOCAL = false, int STAGE = 0>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                              const __bf16* __restrict__ out, const float* __restrict__ lse,
                                                              float* __restrict__ delta, __bf16* __restrict__ dQ, AttnGeom g,
                                                              RopeOut ro, int delta_ready) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 4 * TILE];  // 32 KB
+  static_assert(STAGE == 0 || STAGE == 2 || STAGE == 3, "STAGE");
+  constexpr int TPS = STAGE == 3 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TPS * TILE];  // 32 / 48 KB
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   int grp, bh;
   xcd_remap(grp, bh);
@@ -649,7 +653,35 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   };
   if (has_local && PREFETCH_LOCAL) load_loc(lo);
 
-  // ---- phase A: shared text tiles, two per step ----
+  // ---- phase A: shared text tiles, two (three) per step ----
+  if constexpr (STAGE != 0) {
+    const int nsteps = (n_text + TPS - 1) / TPS;
+    auto dma_step = [&](int si, int buf) {
+      __bf16* S0 = smem + buf * (2 * TPS * TILE);
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        const int tt = min(TPS * si + t, n_text - 1);
+        dma_tile(Kt + base + (size_t)tt * 32 * 64, S0 + t * TILE, wave, lane);
+        dma_tile(V + base + (size_t)tt * 32 * 64, S0 + (TPS + t) * TILE, wave, lane);
+      }
+    };
+    dma_step(0, 0);
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);
+    __syncthreads();
+    for (int si = 0; si < nsteps; ++si) {
+      const bool more = si + 1 < nsteps && !(g.diag & 1);
+      if (more) dma_step(si + 1, (si + 1) & 1);  // that buffer was released by the previous step's barrier
+      const __bf16* S0 = smem + (si & 1) * (2 * TPS * TILE);
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        const int tile = TPS * si + t;
+        if (tile < my_text_end && !(g.diag & 32))
+          dq_tile(dq0, dq1, S0 + t * TILE, S0 + (TPS + t) * TILE, tile, qf, dof, lq, dl, g, qb, qs, lane);
+      }
+      __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next step's tiles landed (this wave's pieces) before the barrier
+      if (!(g.diag & 2)) __syncthreads();
+    }
+  } else {
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
   const int st_off = lds_idx(st_row, st_col);
   const int npairs = (n_text + 1) >> 1;
@@ -680,6 +712,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
     if (tb < my_text_end && !(g.diag & 32)) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
     if (more) store_pair((pi + 1) & 1);
     if (!(g.diag & 2)) __syncthreads();
+  }
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
@@ -1135,6 +1168,18 @@ static int attn_fwd_tps() {
   return g_fwd_tps;
 }
 void attn_set_fwd_tps(int t) { g_fwd_tps = t == 3 ? 3 : 2; }
+// DALLE_AMD_ATTN_DQ_STAGE=0|2|3: the dQ kernel's text-tile staging (0 register-staged pairs; 2 / 3 LDS-DMA, two /
+// three tiles per barrier step); attn_set_dq_stage overrides it at run time
+static int g_dq_stage = -1;
+static int attn_dq_stage() {
+  if (g_dq_stage < 0) {
+    const char* e = getenv("DALLE_AMD_ATTN_DQ_STAGE");
+    const int v = e ? atoi(e) : 0;
+    g_dq_stage = (v == 2 || v == 3) ? v : 0;
+  }
+  return g_dq_stage;
+}
+void attn_set_dq_stage(int v) { g_dq_stage = (v == 2 || v == 3) ? v : 0; }
 // DALLE_AMD_DKDV_QT=2|4: query tiles staged per barrier step of the text dK/dV kernel (attn_set_dkdv_qt
 // overrides it at run time)
 static int g_dkdv_qt = -1;
@@ -1214,29 +1259,31 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   if (conc) launch_dkdv(kst);
   const int dr = conc ? 1 : 0;
   const bool pfq = attn_pf(1) != 0;
+  const int stage = pfq ? 0 : attn_dq_stage();
+#define DQ_LAUNCH(MB, FL, PF, STG)                                                                                    \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<MB, FL, PF, STG>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,  \
+                     (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr)
+#define DQ_STAGES(MB, FL)                   \
+  do {                                      \
+    if (stage == 2) DQ_LAUNCH(MB, FL, false, 2); \
+    else if (stage == 3) DQ_LAUNCH(MB, FL, false, 3); \
+    else DQ_LAUNCH(MB, FL, false, 0);       \
+  } while (0)
   if (fuse_local) {
     if (attn_occ(1) == 3) {
-      if (pfq)
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
-      else
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+      if (pfq) DQ_LAUNCH(3, true, true, 0);
+      else DQ_STAGES(3, true);
     } else {
-      if (pfq)
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
-      else
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<2, true>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                           (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+      if (pfq) DQ_LAUNCH(2, true, true, 0);
+      else DQ_STAGES(2, true);
     }
   } else if (attn_occ(1) == 3) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+    DQ_STAGES(3, false);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<2, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr);
+    DQ_STAGES(2, false);
   }
+#undef DQ_STAGES
+#undef DQ_LAUNCH
   if (conc) {
     // the caller's stream resumes only after the side-stream kernels: every later use of the outputs,
     // and every reuse of the inputs' memory by the caching allocator, is ordered after them

@@ -6,7 +6,7 @@ TAG=${1:-r4ab}
 mkdir -p gpurun_out
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log | cut -c1-200
-{ timeout -k 10 300 python3 -u -m pytest tests/test_gemm_pt_gpu.py -x -q --timeout 120 --timeout-method thread -k "dgrad or line_stores or ff_in" && timeout -k 10 300 python3 -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "four_tiles or three_tiles or sparse_attention"; } > gpurun_out/${TAG}_pt_tests.log 2>&1 || { echo "pt tests failed"; tail -30 gpurun_out/${TAG}_pt_tests.log; exit 1; }
+{ timeout -k 10 300 python3 -u -m pytest tests/test_gemm_pt_gpu.py -x -q --timeout 120 --timeout-method thread -k "dgrad or line_stores or ff_in" && timeout -k 10 300 python3 -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "four_tiles or three_tiles or dma_staging or sparse_attention"; } > gpurun_out/${TAG}_pt_tests.log 2>&1 || { echo "pt tests failed"; tail -30 gpurun_out/${TAG}_pt_tests.log; exit 1; }
 grep -E 'passed|failed' gpurun_out/${TAG}_pt_tests.log
 timeout -k 10 300 python3 -u benchmarks/bench_geglu_bwd_variants.py > gpurun_out/${TAG}_geglu_variants.jsonl 2>&1 || { echo "geglu bench failed"; tail -5 gpurun_out/${TAG}_geglu_variants.jsonl; exit 1; }
 cat gpurun_out/${TAG}_geglu_variants.jsonl
@@ -20,5 +20,6 @@ step geglu_pt DALLE_AMD_GEGLU_DGRAD_KERNEL=pt
 step ffin_pt DALLE_AMD_FUSED_FF_IN=1
 step dkdv_qt4 DALLE_AMD_DKDV_QT=4
 step fwd_tps3 DALLE_AMD_ATTN_FWD_TPS=3
+step dq_stage3 DALLE_AMD_ATTN_DQ_STAGE=3
 step default2 X=1
 bash scripts/gpu_attn_stagger.sh

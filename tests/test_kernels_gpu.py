@@ -500,3 +500,30 @@ def test_attention_forward_three_tiles_per_step(cuda, attn_type):
         C.attn_set_fwd_tps(2)
     assert torch.isfinite(outs[1]).all()
     assert _rel(outs[0], outs[1]) < 2e-3, attn_type
+
+
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
+def test_dq_dma_staging_bitwise(cuda, attn_type):
+    """The dQ kernel with its text tiles LDS-DMA'd two or three per barrier step (attn_set_dq_stage(2 | 3))
+    accumulates the same tiles in the same order as the register-staged form: bitwise-identical gradients."""
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(12)
+    T, S, B, H = 257, 32, 2, 3
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
+    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
+    grads = []
+    try:
+        for stage in (0, 2, 3):
+            C.attn_set_dq_stage(stage)
+            x = qkv.clone().requires_grad_(True)
+            hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+            torch.cuda.synchronize()
+            grads.append(x.grad.clone())
+    finally:
+        C.attn_set_dq_stage(0)
+    assert torch.isfinite(grads[0].float()).all()
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2]), attn_type
