@@ -1229,7 +1229,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_fwd_tps", [](int64_t t) { dalle::attn_set_fwd_tps((int)t); }, py::arg("tps"),
         "text tiles per barrier step of the attention forward: 2 (default) or 3");
   m.def("attn_set_dkdv_qt", [](int64_t qt) { dalle::attn_set_dkdv_qt((int)qt); }, py::arg("qt"),
-        "query tiles per barrier step of the text dK/dV kernel: 2 (default) or 4");
+        "query tiles per barrier step of the text dK/dV kernel: 4 (default) or 2");
   m.def("attn_set_pf", [](int64_t f, int64_t q) { dalle::attn_set_pf((int)f, (int)q); }, py::arg("fwd"), py::arg("dq"),
         "attention forward / dQ: load the first local key tile before the text phase (1) or after it (0)");
   m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },

@@ -1180,17 +1180,18 @@ static int attn_dq_stage() {
   return g_dq_stage;
 }
 void attn_set_dq_stage(int v) { g_dq_stage = (v == 2 || v == 3) ? v : 0; }
-// DALLE_AMD_DKDV_QT=2|4: query tiles staged per barrier step of the text dK/dV kernel (attn_set_dkdv_qt
+// DALLE_AMD_DKDV_QT=4|2: query tiles staged per barrier step of the text dK/dV kernel (default 4: half the
+// barrier steps, bitwise-identical results, -0.9 ms of attention per bench24 B128 step; attn_set_dkdv_qt
 // overrides it at run time)
 static int g_dkdv_qt = -1;
 static int attn_dkdv_qt() {
   if (g_dkdv_qt < 0) {
     const char* e = getenv("DALLE_AMD_DKDV_QT");
-    g_dkdv_qt = (e && atoi(e) == 4) ? 4 : 2;
+    g_dkdv_qt = (e && atoi(e) == 2) ? 2 : 4;
   }
   return g_dkdv_qt;
 }
-void attn_set_dkdv_qt(int qt) { g_dkdv_qt = qt == 4 ? 4 : 2; }
+void attn_set_dkdv_qt(int qt) { g_dkdv_qt = qt == 2 ? 2 : 4; }
 void attn_set_pf(int fwd, int dq) {
   g_attn_pf[0] = fwd;
   g_attn_pf[1] = dq;

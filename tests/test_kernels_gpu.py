@@ -473,7 +473,7 @@ def test_text_dkdv_four_tiles_per_step_bitwise(cuda, attn_type):
             torch.cuda.synchronize()
             grads.append(x.grad.clone())
     finally:
-        C.attn_set_dkdv_qt(2)
+        C.attn_set_dkdv_qt(4)
     assert torch.isfinite(grads[0].float()).all()
     assert torch.equal(grads[0], grads[1]), attn_type
 
