@@ -9,6 +9,7 @@ run() {  # name, timeout, args...
 }
 run step64 240 --steps 15 --warmup 3 --batch 64
 run step128 300 --steps 10 --warmup 3
+run step160 300 --steps 8 --warmup 2 --batch 160
 run collab 300 --steps 10 --warmup 3 --engine collab
 run psgd8 300 --steps 5 --warmup 2 --compression powersgd --optim-bits 8
 run ref48_auto 400 --model reference --batch 48 --steps 3 --warmup 1 --recompute auto
