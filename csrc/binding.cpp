@@ -5,8 +5,10 @@
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
 
 #include "kernels/geom.h"
+#include "blaslt/lt_tuned.h"
 
 namespace dalle {
 
@@ -119,6 +121,125 @@ static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream()
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " has wrong dtype")
 #define CHECK_IN(x, dt) CHECK_CUDA(x); CHECK_CONTIG(x); CHECK_DT(x, dt)
+
+// ---------------------------------------------------------------------------------------------
+// hipBLASLt strided-batched bf16 -> fp32 product with a measured solution (csrc/blaslt/lt_tuned.cpp):
+// out (s, N, K) = a (s, N, ms) . b (s, ms, K) for the split-K weight-gradient views (each operand with a
+// unit stride in one of its two matrix dims). tune: on the first call for this problem, time every
+// supported solution (one warm-up, `reps` timed runs, a run-to-run bitwise check) and keep the fastest
+// reproducible one. Returns the chosen solution index (0 = hipBLASLt's heuristic pick).
+static dalle::LtProblem lt_problem_of(const Tensor& a, const Tensor& b, const Tensor& out) {
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && out.dim() == 3, "lt_bmm: 3-D operands");
+  const long s = a.size(0), N = a.size(1), ms = a.size(2), K = b.size(2);
+  TORCH_CHECK(b.size(0) == s && b.size(1) == ms && out.size(0) == s && out.size(1) == N && out.size(2) == K, "lt_bmm: shapes");
+  dalle::LtProblem p;
+  p.m = K;
+  p.n = N;
+  p.k = ms;
+  p.batch = s;
+  p.ldc = K;
+  p.sc = N * K;
+  if (b.stride(2) == 1) {  // X1 = B^T stored column-major (K x ms)
+    p.opA = HIPBLAS_OP_N;
+    p.lda = b.stride(1);
+    TORCH_CHECK(p.lda >= K, "lt_bmm: b leading dim");
+  } else {
+    TORCH_CHECK(b.stride(1) == 1, "lt_bmm: b needs a unit stride");
+    p.opA = HIPBLAS_OP_T;  // stored column-major (ms x K)
+    p.lda = b.stride(2);
+    TORCH_CHECK(p.lda >= ms, "lt_bmm: b leading dim");
+  }
+  if (a.stride(2) == 1) {  // X2 = A^T stored column-major (ms x N)
+    p.opB = HIPBLAS_OP_N;
+    p.ldb = a.stride(1);
+    TORCH_CHECK(p.ldb >= ms, "lt_bmm: a leading dim");
+  } else {
+    TORCH_CHECK(a.stride(1) == 1, "lt_bmm: a needs a unit stride");
+    p.opB = HIPBLAS_OP_T;  // stored column-major (N x ms)
+    p.ldb = a.stride(2);
+    TORCH_CHECK(p.ldb >= N, "lt_bmm: a leading dim");
+  }
+  p.sa = b.stride(0);
+  p.sb = a.stride(0);
+  return p;
+}
+
+static Tensor lt_ws(const Tensor& like, size_t bytes) {
+  return torch::empty({(long)std::max<size_t>(bytes, 1)}, like.options().dtype(torch::kUInt8));
+}
+
+int64_t lt_bmm_(Tensor a, Tensor b, Tensor out, bool tune, int64_t reps) {
+  CHECK_CUDA(out);
+  CHECK_CONTIG(out);
+  CHECK_DT(out, torch::kFloat32);
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
+              "lt_bmm: bf16 GPU operands");
+  const dalle::LtProblem p = lt_problem_of(a, b, out);
+  hipStream_t st = cur_stream();
+  const void* X1 = b.data_ptr();
+  const void* X2 = a.data_ptr();
+  float* C = out.data_ptr<float>();
+  if (tune && !dalle::lt_tuned(p)) {
+    const int n = dalle::lt_count(p);
+    size_t wsmax = 1;
+    for (int i = 0; i < n; ++i) wsmax = std::max(wsmax, dalle::lt_ws_bytes(p, i));
+    auto ws = lt_ws(out, wsmax);
+    auto ref = torch::empty_like(out);
+    hipEvent_t e0, e1;
+    TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "lt_bmm: events");
+    int best = 0;
+    double best_us = 1e30;
+    for (int i = 0; i < n; ++i) {
+      dalle::lt_run_idx(p, i, X1, X2, C, ws.data_ptr(), st);
+      ref.copy_(out);
+      TORCH_CHECK(hipEventRecord(e0, st) == hipSuccess, "lt_bmm: event");
+      for (int r = 0; r < reps; ++r) dalle::lt_run_idx(p, i, X1, X2, C, ws.data_ptr(), st);
+      TORCH_CHECK(hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess, "lt_bmm: event");
+      float ms = 0.f;
+      TORCH_CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess, "lt_bmm: event time");
+      const double us = 1000.0 * ms / std::max<int64_t>(reps, 1);
+      if (us < best_us && torch::equal(ref, out)) {
+        best_us = us;
+        best = i;
+      }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    dalle::lt_choose(p, best);
+  }
+  auto ws = lt_ws(out, dalle::lt_ws_bytes(p, dalle::lt_chosen(p)));
+  dalle::lt_run_idx(p, -1, X1, X2, C, ws.data_ptr(), st);
+  return dalle::lt_chosen(p);
+}
+
+// the same search, reported: [(solution, microseconds, reproducible, kernel name)] for this problem (does not
+// change the chosen solution)
+std::vector<std::tuple<int64_t, double, bool, std::string>> lt_bmm_survey(Tensor a, Tensor b, Tensor out, int64_t reps) {
+  CHECK_CUDA(out);
+  const dalle::LtProblem p = lt_problem_of(a, b, out);
+  hipStream_t st = cur_stream();
+  const int n = dalle::lt_count(p);
+  size_t wsmax = 1;
+  for (int i = 0; i < n; ++i) wsmax = std::max(wsmax, dalle::lt_ws_bytes(p, i));
+  auto ws = lt_ws(out, wsmax);
+  auto ref = torch::empty_like(out);
+  hipEvent_t e0, e1;
+  TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "lt_bmm_survey: events");
+  std::vector<std::tuple<int64_t, double, bool, std::string>> res;
+  for (int i = 0; i < n; ++i) {
+    dalle::lt_run_idx(p, i, b.data_ptr(), a.data_ptr(), out.data_ptr<float>(), ws.data_ptr(), st);
+    ref.copy_(out);
+    TORCH_CHECK(hipEventRecord(e0, st) == hipSuccess, "event");
+    for (int r = 0; r < reps; ++r) dalle::lt_run_idx(p, i, b.data_ptr(), a.data_ptr(), out.data_ptr<float>(), ws.data_ptr(), st);
+    TORCH_CHECK(hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess, "event");
+    float ms = 0.f;
+    TORCH_CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess, "event time");
+    res.emplace_back(i, 1000.0 * ms / std::max<int64_t>(reps, 1), torch::equal(ref, out), dalle::lt_solution_name(p, i));
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return res;
+}
 
 static int ilog2(int v) {
   int l = 0;
@@ -1224,6 +1345,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
     return C;
   });
+  m.def("lt_bmm_", &lt_bmm_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("tune") = true, py::arg("reps") = 3,
+        "out (s, N, K) fp32 = a (s, N, ms) . b (s, ms, K) bf16 on hipBLASLt with a measured solution per problem");
+  m.def("lt_bmm_survey", &lt_bmm_survey, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("reps") = 3);
   m.def("attn_set_dq_stage", [](int64_t v) { dalle::attn_set_dq_stage((int)v); }, py::arg("stage"),
         "dQ kernel text staging: 0 register pairs (default), 2 / 3 LDS-DMA tiles per barrier step");
   m.def("attn_set_fwd_tps", [](int64_t t) { dalle::attn_set_fwd_tps((int)t); }, py::arg("tps"),

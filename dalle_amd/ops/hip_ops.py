@@ -308,6 +308,12 @@ def wgrad_t_splits(M: int, N: int, K: int, form: str) -> int:
     return s
 
 
+# split-K weight grads on hipBLASLt with a measured solution per problem (csrc/blaslt/lt_tuned.cpp: every
+# supported solution timed once on first use, fastest bitwise-reproducible kept) instead of torch.bmm's
+# heuristic pick
+WGRAD_LT = int(os.environ.get("DALLE_AMD_WGRAD_LT", "0"))
+
+
 def _weight_grad_t(gw, fused: bool, g2, x2):
     """dW = g^T x with G and/or X given token-contiguous (XT): split-K batched hipBLASLt GEMM whose
     operands are strided views of the transposed copies (no gather), fp32 partials + the fold kernel."""
@@ -322,7 +328,12 @@ def _weight_grad_t(gw, fused: bool, g2, x2):
     b = xt.view(K, s, ms).transpose(0, 1).transpose(1, 2) if xt is not None else x2.view(s, ms, K)
     if s > 1:
         out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=a.device)
-        part = torch.bmm(a, b, out_dtype=torch.float32)
+        if WGRAD_LT:
+            part = torch.empty(s, N, K, dtype=torch.float32, device=a.device)
+            C().lt_bmm_(a, b, part, True, 3)
+            _count("wgrad_lt")
+        else:
+            part = torch.bmm(a, b, out_dtype=torch.float32)
         C().splitk_accum_(out, part, fused)
         return None if fused else out
     if fused:

@@ -31,6 +31,7 @@ hip_sources = [
     "csrc/kernels/embed.hip",
     "csrc/kernels/conv.hip",
     "csrc/optim/lamb.hip",
+    "csrc/blaslt/lt_tuned.cpp",
 ]
 
 # Plain setuptools Extension (not CUDAExtension): CUDAExtension would run hipify over the sources.
@@ -41,7 +42,7 @@ ext_modules = [
         hip_sources,
         include_dirs=[os.path.join(ROOT, "csrc")] + include_paths(device_type="cuda"),
         library_dirs=library_paths(device_type="cuda"),
-        libraries=["c10", "torch", "torch_cpu", "torch_python", "amdhip64", "c10_hip", "torch_hip"],
+        libraries=["c10", "torch", "torch_cpu", "torch_python", "amdhip64", "c10_hip", "torch_hip", "hipblaslt"],
         language="c++",
         extra_compile_args={
             "cxx": ["-O3", "-std=c++17"],
