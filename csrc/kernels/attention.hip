@@ -254,30 +254,43 @@ __device__ __forceinline__ int stage_swz(int row) { return ((row >> 2) & 1) | ((
 __device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const AttnGeom& g, int bh, int s0, int t, int dt,
                                                     const f32x16& acc, float scale, float* stage, int lane) {
   const int hl = lane >> 5, c32 = lane & 31;
+  const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
+  const int q4 = lane & 3;
+  const int d0 = 32 * dt + 8 * q4;
+  // the (cos, sin) rows of this lane's two tokens first: they depend only on the positions, so their load
+  // latency runs under the LDS staging below instead of after it (round 4; the epilogues' table loads were
+  // a serial latency chain per store call)
+  int pp[2];
+  f32x4 c0[2], c1[2], n0[2], n1[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int tok = it * 16 + (lane >> 2);
+    const int p = st2seq(g, s0 + tok);
+    pp[it] = p;
+    const int pc = p < 0 ? 0 : p;
+    const float* cp = ro.cosT + (size_t)pc * 64 + d0;
+    const float* sp = ro.sinT + (size_t)pc * 64 + d0;
+    c0[it] = *reinterpret_cast<const f32x4*>(cp);
+    c1[it] = *reinterpret_cast<const f32x4*>(cp + 4);
+    n0[it] = *reinterpret_cast<const f32x4*>(sp);
+    n1[it] = *reinterpret_cast<const f32x4*>(sp + 4);
+  }
 #pragma unroll
   for (int gq = 0; gq < 4; ++gq) {
     const int ch = (2 * gq + hl) ^ stage_swz(c32);
     *reinterpret_cast<f32x4*>(stage + c32 * 32 + 4 * ch) = f32x4{acc[4 * gq], acc[4 * gq + 1], acc[4 * gq + 2], acc[4 * gq + 3]};
   }
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); the table loads stay in flight
   __builtin_amdgcn_wave_barrier();
-  const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
-  const int q4 = lane & 3;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int tok = it * 16 + (lane >> 2);
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4) ^ stage_swz(tok)));
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4 + 1) ^ stage_swz(tok)));
-    const int p = st2seq(g, s0 + tok);
-    if (p < 0) continue;
-    const int d0 = 32 * dt + 8 * q4;
-    const float* cp = ro.cosT + (size_t)p * 64 + d0;
-    const float* sp = ro.sinT + (size_t)p * 64 + d0;
-    const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
-    const f32x4 n0 = *reinterpret_cast<const f32x4*>(sp), n1 = *reinterpret_cast<const f32x4*>(sp + 4);
+    const int p = pp[it];
     const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const float c[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-    const float sn[8] = {n0[0], n0[1], n0[2], n0[3], n1[0], n1[1], n1[2], n1[3]};
+    const float c[8] = {c0[it][0], c0[it][1], c0[it][2], c0[it][3], c1[it][0], c1[it][1], c1[it][2], c1[it][3]};
+    const float sn[8] = {n0[it][0], n0[it][1], n0[it][2], n0[it][3], n1[it][0], n1[it][1], n1[it][2], n1[it][3]};
     float y[8];
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {  // transposed rotation of the pair (i, i + 1)
@@ -285,7 +298,7 @@ __device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const Att
       y[i] = a0 * c[i] + a1 * sn[i + 1];
       y[i + 1] = a1 * c[i + 1] + a0 * sn[i];
     }
-    *reinterpret_cast<s16x8*>(ro.dqkv + ((size_t)b * g.n + p) * (3 * HD) + t * HD + h * 64 + d0) = pack8(y);
+    if (p >= 0) *reinterpret_cast<s16x8*>(ro.dqkv + ((size_t)b * g.n + p) * (3 * HD) + t * HD + h * 64 + d0) = pack8(y);
   }
   __builtin_amdgcn_wave_barrier();  // every lane has read the slot before it is rewritten
 }

@@ -1,8 +1,7 @@
-# attention forward / dQ with the compute skipped (prologue + epilogue cost) and other phase skips
+# dQ-kernel skeleton split: everything skipped but the prologue (Q / dO / O loads, delta) and the epilogue
 set -o pipefail
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-for d in 7 39 35; do
-  DALLE_AMD_ATTN_DIAG=$d timeout -k 10 120 python3 benchmarks/attn_fwd_diag.py || exit 1
+for d in 39 36 0; do
+  DALLE_AMD_ATTN_DIAG=$d timeout -k 10 120 python3 -u benchmarks/bench_attn_parts.py 128 > gpurun_out/attn_diag2_$d.log 2>&1 || { echo "diag $d failed"; tail -5 gpurun_out/attn_diag2_$d.log; exit 1; }
+  echo "diag=$d"; grep '^{' gpurun_out/attn_diag2_$d.log
 done
-DIAGS="7 39" bash scripts/gpu_attn_bwd_diag.sh
