@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
       __builtin_amdgcn_wave_barrier();
     }
   }
-  if (FUSE_LOCAL && active && qb >= ntext && ro.dqkv) {
+  if (FUSE_LOCAL && active && qb >= ntext && ro.dqkv && !(g.diag & 64)) {
     // key-centric pass over the diagonal tile: K / V rows of the tile's keys (lane = key) from the slot,
     // then the slot is refilled with this wave's Q / dO tile (lane = query row) and the row stats
     __bf16* P = smem + wave * (2 * TILE);
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   // the epilogue's per-wave staging slot (4 KB at wave * 4 KB) overlaps other waves' phase-B slots
   __syncthreads();
 
-  if (!active) return;
+  if (!active || (g.diag & 128)) return;
   if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 4 KB
     float* stage = reinterpret_cast<float*>(smem) + wave * 1024;
     rope_bwd_store_half(ro, g, bh, qb * 32, 0, 0, dq0, ro.qscale, stage, lane);
