@@ -241,56 +241,55 @@ struct RopeOut {
   float qscale;
 };
 
-// One dim-half (dims 32 dt .. 32 dt + 31) of a wave's 32-token gradient tile, held in the MFMA
-// accumulator layout (lane c32 + 32 hl owns dims 32 dt + 8 gq + 4 hl + i from acc[4 gq + i]), is staged
-// through the wave's 4 KB LDS slot (fp32, 16-byte chunks XOR-swizzled by row) and re-read so that 4
-// lanes own one token's 32 contiguous dims: coalesced cos/sin row reads and 64-byte contiguous stores
-// per token into dqkv. The caller guarantees no other wave touches `stage` (4 KB, 16-byte aligned).
-// 16-byte chunk swizzle of the staging slot (rows of 128 B): a bijection on row & 7 (so the ds_write_b128
-// groups of 8 consecutive rows hit 8 distinct chunk slots) whose parity is bit 2 of the row (so each
-// ds_read_b128 lane group -- 4 rows x 4 lanes, two rows of each parity -- covers all 16 slots of 256 B).
-__device__ __forceinline__ int stage_swz(int row) { return ((row >> 2) & 1) | ((row & 3) << 1); }
-
-__device__ __forceinline__ void rope_bwd_store_half(const RopeOut& ro, const AttnGeom& g, int bh, int s0, int t, int dt,
-                                                    const f32x16& acc, float scale, float* stage, int lane) {
+// Both dim-halves of a wave's 32-token gradient tile (acc0: dims 0-31, acc1: dims 32-63, MFMA accumulator
+// layout) staged once through 8 KB of the wave's LDS ([32 tokens][64 dims] fp32, 16-byte chunk c of row r at
+// c ^ (r & 15)) and stored as whole 128-B token rows (8 lanes x 16 B per token, 8 tokens per instruction)
+// with the rotary inverse applied (round 4: the half form wrote 64-B half rows, two store calls per tile).
+__device__ __forceinline__ void rope_bwd_store_full(const RopeOut& ro, const AttnGeom& g, int bh, int s0, int t,
+                                                    const f32x16& acc0, const f32x16& acc1, float scale, float* stage,
+                                                    int lane) {
   const int hl = lane >> 5, c32 = lane & 31;
   const int b = bh / g.H, h = bh - b * g.H, HD = g.H * 64;
-  const int q4 = lane & 3;
-  const int d0 = 32 * dt + 8 * q4;
-  // the (cos, sin) rows of this lane's two tokens first: they depend only on the positions, so their load
-  // latency runs under the LDS staging below instead of after it (round 4; the epilogues' table loads were
-  // a serial latency chain per store call)
-  int pp[2];
+  const int q8 = lane & 7, d0 = 8 * q8;
+  // the (cos, sin) rows of the lane's tokens, two passes ahead (the first two before the staging, so their
+  // latency runs under it; each later pair right after the pass that frees its registers)
+  int pp[4];
   f32x4 c0[2], c1[2], n0[2], n1[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int tok = it * 16 + (lane >> 2);
+  auto load_tab = [&](int it) {
+    const int tok = it * 8 + (lane >> 3);
     const int p = st2seq(g, s0 + tok);
     pp[it] = p;
     const int pc = p < 0 ? 0 : p;
     const float* cp = ro.cosT + (size_t)pc * 64 + d0;
     const float* sp = ro.sinT + (size_t)pc * 64 + d0;
-    c0[it] = *reinterpret_cast<const f32x4*>(cp);
-    c1[it] = *reinterpret_cast<const f32x4*>(cp + 4);
-    n0[it] = *reinterpret_cast<const f32x4*>(sp);
-    n1[it] = *reinterpret_cast<const f32x4*>(sp + 4);
-  }
+    c0[it & 1] = *reinterpret_cast<const f32x4*>(cp);
+    c1[it & 1] = *reinterpret_cast<const f32x4*>(cp + 4);
+    n0[it & 1] = *reinterpret_cast<const f32x4*>(sp);
+    n1[it & 1] = *reinterpret_cast<const f32x4*>(sp + 4);
+  };
+  load_tab(0);
+  load_tab(1);
 #pragma unroll
-  for (int gq = 0; gq < 4; ++gq) {
-    const int ch = (2 * gq + hl) ^ stage_swz(c32);
-    *reinterpret_cast<f32x4*>(stage + c32 * 32 + 4 * ch) = f32x4{acc[4 * gq], acc[4 * gq + 1], acc[4 * gq + 2], acc[4 * gq + 3]};
+  for (int dt = 0; dt < 2; ++dt) {
+    const f32x16& acc = dt ? acc1 : acc0;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int ch = (8 * dt + 2 * gq + hl) ^ (c32 & 15);
+      *reinterpret_cast<f32x4*>(stage + c32 * 64 + 4 * ch) = f32x4{acc[4 * gq], acc[4 * gq + 1], acc[4 * gq + 2], acc[4 * gq + 3]};
+    }
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); the table loads stay in flight
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int tok = it * 16 + (lane >> 2);
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4) ^ stage_swz(tok)));
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 32 + 4 * ((2 * q4 + 1) ^ stage_swz(tok)));
-    const int p = pp[it];
+  for (int it = 0; it < 4; ++it) {
+    const int tok = it * 8 + (lane >> 3), sl = it & 1;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + tok * 64 + 4 * ((2 * q8) ^ (tok & 15)));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + tok * 64 + 4 * ((2 * q8 + 1) ^ (tok & 15)));
     const float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const float c[8] = {c0[it][0], c0[it][1], c0[it][2], c0[it][3], c1[it][0], c1[it][1], c1[it][2], c1[it][3]};
-    const float sn[8] = {n0[it][0], n0[it][1], n0[it][2], n0[it][3], n1[it][0], n1[it][1], n1[it][2], n1[it][3]};
+    const float c[8] = {c0[sl][0], c0[sl][1], c0[sl][2], c0[sl][3], c1[sl][0], c1[sl][1], c1[sl][2], c1[sl][3]};
+    const float sn[8] = {n0[sl][0], n0[sl][1], n0[sl][2], n0[sl][3], n1[sl][0], n1[sl][1], n1[sl][2], n1[sl][3]};
+    const int p = pp[it];
+    if (it + 2 < 4) load_tab(it + 2);
     float y[8];
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {  // transposed rotation of the pair (i, i + 1)
@@ -603,6 +602,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   constexpr int TPS = STAGE == 3 ? 3 : 2;
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TPS * TILE];  // 32 / 48 KB
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
+  __shared__ float dsh[4][32];                                          // prologue: per wave row deltas
   int grp, bh;
   xcd_remap(grp, bh);
   attn_stagger(g);
@@ -625,7 +625,56 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   // dK/dV kernels that run next on the stream
   bf16x8 qf[4], dof[4];
   float dl = 0.f;
-  {
+  if (!(g.diag & 256)) {
+    // Q (4 KB of contiguous storage rows) and dO (32 gathered 128-B token rows) of this wave through its 8 KB
+    // LDS slot (phase A's buffers are not in use yet), 8 lanes per row: every load instruction covers 8 whole
+    // 128-B lines, where the per-lane operand-layout loads touched 32 lines per instruction (round 4). delta
+    // = rowsum(dO * O) from the same registers, reduced over each row's 8 lanes (fixed xor tree).
+    __bf16* Ps = smem + wave * (2 * TILE);
+    float dpart[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+      const int srow = (active ? qb * 32 : 0) + row;
+      const int toff = tok_row(g, srow);
+      const s16x8 qv = *reinterpret_cast<const s16x8*>(Q + base + (size_t)srow * 64 + col);
+      const s16x8 dv = ld_tok(dob, toff, col);
+      *reinterpret_cast<s16x8*>(Ps + lds_idx(row, col)) = qv;
+      *reinterpret_cast<s16x8*>(Ps + TILE + lds_idx(row, col)) = dv;
+      dpart[j] = 0.f;
+      if (!delta_ready) {
+        const s16x8 ov = ld_tok(outb, toff, col);
+        float fd[8], fo[8];
+        unpack8(dv, fd);
+        unpack8(ov, fo);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dpart[j] = fmaf(fd[i], fo[i], dpart[j]);
+      }
+    }
+    if (!delta_ready) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dpart[j] += __shfl_xor(dpart[j], 1, 64);
+        dpart[j] += __shfl_xor(dpart[j], 2, 64);
+        dpart[j] += __shfl_xor(dpart[j], 4, 64);
+        const int row = 8 * j + (lane >> 3);
+        if ((lane & 7) == 0) {
+          dsh[wave][row] = dpart[j];
+          if (active) delta[(size_t)bh * g.Np + qb * 32 + row] = dpart[j];
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot and the row deltas are written
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      qf[s2] = row_operand(Ps, s2, lane & 31, hl);
+      dof[s2] = row_operand(Ps + TILE, s2, lane & 31, hl);
+    }
+    dl = delta_ready ? delta[(size_t)bh * g.Np + qrow] : dsh[wave][lane & 31];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __syncthreads();  // every wave has its operands in registers before phase A refills the buffers
+  } else {
     const int qoff = tok_row(g, qrow);
     const __bf16* qp = Q + base + (size_t)qrow * 64 + 8 * hl;
 #pragma unroll
@@ -807,19 +856,16 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
     dk1 = MFMA32(tr_operand(P, 1, 1, lane), e1, dk1);
     // the MFMAs consumed the slot's operands: it now stages this wave's dK / dV stores
     float* stage = reinterpret_cast<float*>(P);
-    rope_bwd_store_half(ro, g, bh, qb * 32, 1, 0, dk0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, qb * 32, 1, 1, dk1, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, qb * 32, 2, 0, dv0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, qb * 32, 2, 1, dv1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, qb * 32, 1, dk0, dk1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, qb * 32, 2, dv0, dv1, 1.0f, stage, lane);
   }
   // the epilogue's per-wave staging slot (4 KB at wave * 4 KB) overlaps other waves' phase-B slots
   __syncthreads();
 
   if (!active || (g.diag & 128)) return;
-  if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 4 KB
-    float* stage = reinterpret_cast<float*>(smem) + wave * 1024;
-    rope_bwd_store_half(ro, g, bh, qb * 32, 0, 0, dq0, ro.qscale, stage, lane);
-    rope_bwd_store_half(ro, g, bh, qb * 32, 0, 1, dq1, ro.qscale, stage, lane);
+  if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 8 KB
+    float* stage = reinterpret_cast<float*>(smem) + wave * 2048;
+    rope_bwd_store_full(ro, g, bh, qb * 32, 0, dq0, dq1, ro.qscale, stage, lane);
     return;
   }
   __bf16* qp = dQ + base + (size_t)qs * 64;
@@ -934,10 +980,8 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
   }
   if (ro.dqkv) {  // this wave's private {Q, dO} slot is free after its last tile
     float* stage = reinterpret_cast<float*>(Qs);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 0, dk0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 1, dk1, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 0, dv0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 1, dv1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, kb * 32, 1, dk0, dk1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, kb * 32, 2, dv0, dv1, 1.0f, stage, lane);
     return;
   }
   __bf16* kp = dK + base + (size_t)ks * 64;
@@ -1108,10 +1152,8 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this key block's 16 KB of partials are consumed: stage through them
     __builtin_amdgcn_wave_barrier();
     float* stage = red + (wave & 1) * 64 * 64;
-    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 0, sk0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 1, 1, sk1, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 0, sv0, 1.0f, stage, lane);
-    rope_bwd_store_half(ro, g, bh, kb * 32, 2, 1, sv1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, kb * 32, 1, sk0, sk1, 1.0f, stage, lane);
+    rope_bwd_store_full(ro, g, bh, kb * 32, 2, sv0, sv1, 1.0f, stage, lane);
   } else if (par == 0 && active) {
     __bf16* kp = dK + base + (size_t)ks * 64;
     __bf16* vp = dV + base + (size_t)ks * 64;
