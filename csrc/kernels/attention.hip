@@ -1026,7 +1026,10 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int kb0 = grp * 2;
-  const int kb = kb0 + (wave & 1), par = wave >> 1;
+  // odd last key block (QT 4): all four waves work on it, wave w taking the query tile t = w of each
+  // step, instead of two waves idling on the absent partner block
+  const bool tail = QT == 4 && kb0 + 1 >= ntext && !(g.diag & 512);
+  const int kb = tail ? kb0 : kb0 + (wave & 1), par = tail ? wave : wave >> 1;
   const bool active = kb < ntext;
   const size_t base = (size_t)bh * g.Np * 64;
   const __bf16* dob = tok_base(dout, g, bh);
@@ -1076,102 +1079,124 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
     load_step(0);
     store_step(0);
   }
+  // retire the K / V fragment loads here: with them possibly in flight at the loop entry (the
+  // conditional prologue above), the compiler guards each MFMA of the loop with a vmcnt wait that
+  // in fact drains the NEXT step's prefetch loads, exposing their latency every step
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
+  // one query tile: scores S^T / dP^T (key rows x query lanes), probabilities and dS, then the
+  // dV += P^T dO / dK += dS^T Q products
+  auto scores = [&](const __bf16* Qs, const __bf16* Ds, f32x16& sc, f32x16& dp) {
+    sc = f32x16{};
+    dp = f32x16{};
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) {
+      sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
+      dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
+    }
+  };
+  auto probs = [&](int buf, int tt, int qt, f32x16& sc, f32x16& dp) {  // sc <- P, dp <- dS
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = acc_row(r, hl);
+      const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[buf][tt][0][ql]));
+      sc[r] = pr;
+      dp[r] = pr * (dp[r] - stats[buf][tt][1][ql]);
+    }
+    if (!tile_full(g, qt, kb)) {
+      const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool on = mask_bit(mh, r);
+        sc[r] = on ? sc[r] : 0.f;
+        dp[r] = on ? dp[r] : 0.f;
+      }
+    }
+  };
+  auto accum = [&](const __bf16* Qs, const __bf16* Ds, const f32x16& sc, const f32x16& ds) {
+    const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
+    const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
+    dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
+    dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
+    dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
+    dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
+    dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
+    dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
+    dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
+    dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
+  };
+  // (measured: issuing the second tile's score products ahead of the first tile's softmax -- a
+  // two-tile software pipeline -- made this kernel slower at B128: 677-690 us against 642 us)
   for (int i = 0; i < nsteps; ++i) {
     const bool more = i + 1 < nsteps && !(g.diag & 8);
     if (more) load_step(i + 1);
     const int buf = i & 1;
 #pragma unroll
     for (int u = 0; u < QT / 2; ++u) {
-      const int tt = par + 2 * u;
+      const int tt = tail ? par : par + 2 * u;
       const int qt = kb0 + QT * i + tt;
-      if (active && qt < nqb && qt >= kb) {
+      if (active && qt < nqb && qt >= kb && !(tail && u > 0)) {
         const __bf16* Qs = smem + (buf * QT + tt) * (2 * TILE);
-        const __bf16* Ds = Qs + TILE;
-        f32x16 sc = {}, dp = {};
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss) {
-          sc = MFMA32(row_operand(Qs, ss, c32, hl), kf[ss], sc);
-          dp = MFMA32(row_operand(Ds, ss, c32, hl), vf[ss], dp);
-        }
-        f32x16 ds;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = acc_row(r, hl);
-          const float pr = fast_exp2(fmaf(sc[r], LOG2E, -stats[buf][tt][0][ql]));
-          sc[r] = pr;
-          ds[r] = pr * (dp[r] - stats[buf][tt][1][ql]);
-        }
-        if (!tile_full(g, qt, kb)) {
-          const uint32_t mh = query_mask(g, ks, qt) >> (4 * hl);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const bool on = mask_bit(mh, r);
-            sc[r] = on ? sc[r] : 0.f;
-            ds[r] = on ? ds[r] : 0.f;
-          }
-        }
-        const bf16x8 p0 = cvt8(sc, 0), p1 = cvt8(sc, 8);
-        const bf16x8 d0 = cvt8(ds, 0), d1 = cvt8(ds, 8);
-        dv0 = MFMA32(tr_operand(Ds, 0, 0, lane), p0, dv0);
-        dv0 = MFMA32(tr_operand(Ds, 1, 0, lane), p1, dv0);
-        dv1 = MFMA32(tr_operand(Ds, 0, 1, lane), p0, dv1);
-        dv1 = MFMA32(tr_operand(Ds, 1, 1, lane), p1, dv1);
-        dk0 = MFMA32(tr_operand(Qs, 0, 0, lane), d0, dk0);
-        dk0 = MFMA32(tr_operand(Qs, 1, 0, lane), d1, dk0);
-        dk1 = MFMA32(tr_operand(Qs, 0, 1, lane), d0, dk1);
-        dk1 = MFMA32(tr_operand(Qs, 1, 1, lane), d1, dk1);
+        f32x16 sc, dp;
+        scores(Qs, Qs + TILE, sc, dp);
+        probs(buf, tt, qt, sc, dp);
+        accum(Qs, Qs + TILE, sc, dp);
       }
     }
     if (more) store_step((i + 1) & 1);
     if (!(g.diag & 16)) __syncthreads();
   }
-  // parity 1 waves hand their partials to the parity 0 wave of the same key block through LDS
-  // (value-major layout: consecutive lanes on consecutive banks), which sums and stores
-  float* red = reinterpret_cast<float*>(smem);  // 2 key blocks x 64 values x 64 lanes floats = 32 KB
-  if (par == 1) {
+  // the other parity's waves hand their partials to the parity 0 wave of the same key block through
+  // LDS (value-major layout: consecutive lanes on consecutive banks), which sums (fixed order) and
+  // stores; a tail workgroup sums three partials (waves 1..3) into wave 0
+  float* red = reinterpret_cast<float*>(smem);  // up to 3 slots x 64 values x 64 lanes floats = 48 KB
+  if (par != 0) {
+    const int slot = tail ? wave - 1 : (wave & 1);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      red[((wave & 1) * 64 + r) * 64 + lane] = dk0[r];
-      red[((wave & 1) * 64 + 16 + r) * 64 + lane] = dk1[r];
-      red[((wave & 1) * 64 + 32 + r) * 64 + lane] = dv0[r];
-      red[((wave & 1) * 64 + 48 + r) * 64 + lane] = dv1[r];
+      red[(slot * 64 + r) * 64 + lane] = dk0[r];
+      red[(slot * 64 + 16 + r) * 64 + lane] = dk1[r];
+      red[(slot * 64 + 32 + r) * 64 + lane] = dv0[r];
+      red[(slot * 64 + 48 + r) * 64 + lane] = dv1[r];
     }
   }
   __syncthreads();
-  if (par == 0 && active && ro.dqkv) {
-    const float* mine = red + (wave & 1) * 64 * 64;
-    f32x16 sk0, sk1, sv0, sv1;
+  if (par == 0 && active) {
+    const int s0 = tail ? 0 : (wave & 1), s1 = tail ? 3 : s0 + 1;
+    for (int sl2 = s0; sl2 < s1; ++sl2) {
+      const float* mine = red + sl2 * 64 * 64;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sk0[r] = dk0[r] + mine[r * 64 + lane];
-      sk1[r] = dk1[r] + mine[(16 + r) * 64 + lane];
-      sv0[r] = dv0[r] + mine[(32 + r) * 64 + lane];
-      sv1[r] = dv1[r] + mine[(48 + r) * 64 + lane];
+      for (int r = 0; r < 16; ++r) {
+        dk0[r] += mine[r * 64 + lane];
+        dk1[r] += mine[(16 + r) * 64 + lane];
+        dv0[r] += mine[(32 + r) * 64 + lane];
+        dv1[r] += mine[(48 + r) * 64 + lane];
+      }
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // this key block's 16 KB of partials are consumed: stage through them
-    __builtin_amdgcn_wave_barrier();
-    float* stage = red + (wave & 1) * 64 * 64;
-    rope_bwd_store_full(ro, g, bh, kb * 32, 1, sk0, sk1, 1.0f, stage, lane);
-    rope_bwd_store_full(ro, g, bh, kb * 32, 2, sv0, sv1, 1.0f, stage, lane);
-  } else if (par == 0 && active) {
-    __bf16* kp = dK + base + (size_t)ks * 64;
-    __bf16* vp = dV + base + (size_t)ks * 64;
+    if (ro.dqkv) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // this key block's partials are consumed: stage through them
+      __builtin_amdgcn_wave_barrier();
+      float* stage = red + (wave & 1) * 64 * 64;
+      rope_bwd_store_full(ro, g, bh, kb * 32, 1, dk0, dk1, 1.0f, stage, lane);
+      rope_bwd_store_full(ro, g, bh, kb * 32, 2, dv0, dv1, 1.0f, stage, lane);
+    } else {
+      __bf16* kp = dK + base + (size_t)ks * 64;
+      __bf16* vp = dV + base + (size_t)ks * 64;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      const f32x16& a = dt ? dk1 : dk0;
-      const f32x16& c = dt ? dv1 : dv0;
+      for (int dt = 0; dt < 2; ++dt) {
+        const f32x16& a = dt ? dk1 : dk0;
+        const f32x16& c = dt ? dv1 : dv0;
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        float fa[4], fc[4];
+        for (int gq = 0; gq < 4; ++gq) {
+          float fa[4], fc[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * gq + i;
-          fa[i] = a[r] + red[((wave & 1) * 64 + dt * 16 + r) * 64 + lane];
-          fc[i] = c[r] + red[((wave & 1) * 64 + 32 + dt * 16 + r) * 64 + lane];
+          for (int i = 0; i < 4; ++i) {
+            fa[i] = a[4 * gq + i];
+            fc[i] = c[4 * gq + i];
+          }
+          *reinterpret_cast<s16x4*>(kp + 32 * dt + 8 * gq + 4 * hl) = pack4(fa);
+          *reinterpret_cast<s16x4*>(vp + 32 * dt + 8 * gq + 4 * hl) = pack4(fc);
         }
-        *reinterpret_cast<s16x4*>(kp + 32 * dt + 8 * gq + 4 * hl) = pack4(fa);
-        *reinterpret_cast<s16x4*>(vp + 32 * dt + 8 * gq + 4 * hl) = pack4(fc);
       }
     }
   }
