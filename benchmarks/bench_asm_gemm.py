@@ -1,0 +1,139 @@
+"""Standalone check + A/B of the generated assembly GEMM (csrc/asm/gen_gemm.py) against hipBLASLt.
+
+Loads the code object through the HIP module API (ctypes), so it needs no extension build:
+
+    python benchmarks/bench_asm_gemm.py [--hsaco path] [--check-only] [--shapes M:N:K,...]
+
+Prints one JSON line per shape: microseconds and TF/s of hipBLASLt (torch.matmul) and of each kernel,
+interleaved in one process on the same random operands (rule: A/B in one process).
+"""
+import argparse
+import ctypes
+import json
+import os
+import struct
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class Module:
+    def __init__(self, path):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        data = open(path, "rb").read()
+        self._buf = ctypes.create_string_buffer(data, len(data))
+        self.mod = ctypes.c_void_p()
+        err = self.hip.hipModuleLoadData(ctypes.byref(self.mod), self._buf)
+        assert err == 0, f"hipModuleLoadData: {err}"
+        self.funcs = {}
+
+    def func(self, name):
+        if name not in self.funcs:
+            f = ctypes.c_void_p()
+            err = self.hip.hipModuleGetFunction(ctypes.byref(f), self.mod, name.encode())
+            assert err == 0, f"hipModuleGetFunction({name}): {err}"
+            self.funcs[name] = f
+        return self.funcs[name]
+
+    def launch(self, name, grid, args: bytes, stream=None):
+        f = self.func(name)
+        buf = ctypes.create_string_buffer(args, len(args))
+        size = ctypes.c_size_t(len(args))
+        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(buf, ctypes.c_void_p), 2,
+                                      ctypes.cast(ctypes.byref(size), ctypes.c_void_p), 3)
+        st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream().cuda_stream)
+        err = self.hip.hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, st, None, extra)
+        assert err == 0, f"hipModuleLaunchKernel: {err}"
+
+
+def gemm_args(A, B, C, aux0=None, grid=256):
+    M, K = A.shape
+    N = B.shape[0]
+    assert M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and K >= 256
+    assert A.stride(1) == 1 and B.stride(1) == 1 and C.stride(1) == 1
+    tiles_n = N // 256
+    nt = (M // 256) * tiles_n
+    ptrs = [A.data_ptr(), B.data_ptr(), C.data_ptr(), aux0.data_ptr() if aux0 is not None else 0, 0, 0]
+    ints = [M, N, K, A.stride(0), B.stride(0), C.stride(0), tiles_n, nt, grid, 0, 0, 0]
+    return struct.pack("<6Q12i", *ptrs, *ints)
+
+
+def run(mod, name, A, B, C, aux0=None, grid=None):
+    M, N = A.shape[0], B.shape[0]
+    nt = (M // 256) * (N // 256)
+    if grid is None:
+        grid = min(256, (nt + 7) // 8 * 8)
+    mod.launch(name, grid, gemm_args(A, B, C, aux0, grid))
+
+
+def check(mod, shapes):
+    ok = True
+    for (M, N, K) in shapes:
+        torch.manual_seed(M + N + K)
+        A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        bias = torch.randn(N, device="cuda")
+        ref = A.float() @ B.float().t()
+        for name, aux in (("dalle_gemm_nt_plain", None), ("dalle_gemm_nt_bias", bias)):
+            C = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+            run(mod, name, A, B, C, aux)
+            torch.cuda.synchronize()
+            r = ref + (bias if aux is not None else 0)
+            err = ((C.float() - r).abs().max() / r.abs().max()).item()
+            nan = torch.isnan(C.float()).sum().item()
+            good = err < 1e-2 and nan == 0
+            ok &= good
+            print(json.dumps({"check": name, "M": M, "N": N, "K": K, "max_rel_err": err, "nan": nan, "ok": good}),
+                  flush=True)
+    return ok
+
+
+def bench(mod, shapes, iters=20):
+    for (M, N, K) in shapes:
+        A = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+        B = torch.rand(N, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        fns = {
+            "hipblaslt": lambda: torch.mm(A, B.t(), out=C),
+            "asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", A, B, C),
+        }
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        times = {k: [] for k in fns}
+        for _ in range(5):   # interleaved rounds
+            for k, f in fns.items():
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(iters):
+                    f()
+                e.record()
+                e.synchronize()
+                times[k].append(s.elapsed_time(e) * 1000 / iters)
+        flop = 2.0 * M * N * K
+        us = {k: round(sorted(v)[len(v) // 2], 1) for k, v in times.items()}
+        print(json.dumps({"shape": f"M{M}_N{N}_K{K}", "us": us,
+                          "TF": {k: round(flop / v / 1e6) for k, v in us.items()}}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hsaco", default=os.path.join(HERE, "..", "dalle_amd", "gemm_gfx950.hsaco"))
+    ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
+                                        "163840:1024:4096,163840:1024:8192,163840:1024:3072")
+    a = ap.parse_args()
+    mod = Module(a.hsaco)
+    ok = check(mod, [(256, 256, 256), (512, 768, 320), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096)])
+    if not ok:
+        sys.exit(1)
+    if a.check_only:
+        return
+    shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]
+    bench(mod, shapes)
+
+
+if __name__ == "__main__":
+    main()

@@ -82,9 +82,11 @@ class CollaborativeGradScaler:
     # -- called by CollaborativeOptimizer at the global step ------------------------------------------
     @torch.no_grad()
     def unscale_and_check(self, grads: Iterable[torch.Tensor] = (), flat_grad: Optional[torch.Tensor] = None,
-                          group=None) -> bool:
+                          group=None, local_only: bool = False) -> bool:
         """Unscale the accumulated grads in place and return True if they are finite on EVERY rank of
-        ``group`` (one tiny all-reduce), False otherwise (the caller then skips the update)."""
+        ``group`` (one tiny all-reduce), False otherwise (the caller then skips the update).
+        ``local_only``: check this rank's grads only, with no collective -- for a round whose
+        communicator just failed (a collective queued behind the broken one would hang the peer)."""
         inv = 1.0 / self._scale
         bufs = [flat_grad] if flat_grad is not None else [g for g in grads if g is not None]
         bad = None
@@ -95,7 +97,7 @@ class CollaborativeGradScaler:
         flag = torch.zeros((), dtype=torch.float32, device=bufs[0].device if bufs else "cpu")
         if bad is not None:
             flag = bad.float()
-        if dist.is_available() and dist.is_initialized():
+        if not local_only and dist.is_available() and dist.is_initialized():
             world = dist.get_world_size(group) if group is not None else dist.get_world_size()
             if world > 1:
                 flag = flag.reshape(1)

@@ -787,7 +787,11 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
                 # averaged grads (unscaling is linear; an overflow on any peer is non-finite in the sum)
                 averaged = self.grad_averager.step(total_samples=total, epoch=self.local_epoch, batch_size=self._last_bs)
             flat = self.arena.grad if (self.arena is not None and self.grad_averager.reuse_grad_buffers) else None
-            if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group):
+            # after a failed overlapped round (dead / slow peer, deadline hit) the group's communicator is
+            # broken: check the local fallback grads without a collective instead of queueing one behind it
+            local_only = averaged is False or self._comm_failed()
+            if not grad_scaler.unscale_and_check(self.grad_averager._grads(), flat_grad=flat, group=self.group,
+                                                 local_only=local_only):
                 logger.warning(f"{self.run_id}: non-finite scaled gradients at epoch {self.local_epoch}; skipping update")
                 self.grad_averager.abandon_overlap()
                 self.grad_averager.reset_accumulated_grads_()

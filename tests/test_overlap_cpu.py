@@ -118,3 +118,47 @@ def test_trainer_declares_its_accumulation():
 
     src = inspect.getsource(CollaborativeHFTrainer.train)
     assert "set_backwards_per_step" in src
+
+
+def _failed_round_worker(rank, world, port, q):
+    """An armed, scaled round whose overlapped all-reduce failed (dead / slow peer): the overflow check must
+    run locally -- a group all-reduce queued behind the broken collective would hang instead of falling back."""
+    try:
+        _init(rank, world, port)
+        w, b, opt = _make(True, rank)
+        scaler = CollaborativeGradScaler(init_scale=2.0 ** 10)
+        seen = []
+        real_check = scaler.unscale_and_check
+
+        def check(*a, **kw):
+            seen.append(kw.get("local_only", False))
+            return real_check(*a, **kw)
+
+        scaler.unscale_and_check = check
+        ga = opt.grad_averager
+
+        def failed_round(epoch, batch_size):
+            ga.abandon_overlap()          # the in-flight round died: no collective completes
+            ga.comm_failed = True
+            return False
+
+        ga._step_overlapped = failed_round
+        w.grad, b.grad = torch.zeros_like(w), torch.zeros_like(b)
+        armed = []
+        for step in range(4):
+            armed.append(ga._armed)
+            _backward(w, b, rank, step, scaler.get_scale())
+            scaler.step(opt)
+            scaler.update()
+        q.put(pickle.dumps((rank, seen, armed, bool(torch.isfinite(w).all()))))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put(pickle.dumps(("error", rank, traceback.format_exc())))
+
+
+def test_failed_armed_scaled_round_checks_overflow_locally():
+    for rank, seen, armed, finite in _run(_failed_round_worker, 2):
+        assert any(armed), armed          # the round that failed was an overlapped one
+        assert seen and seen[0] is True, seen
+        assert finite
