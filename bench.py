@@ -71,9 +71,13 @@ def parse():
     ap.add_argument("--optim-bits", type=int, default=None, choices=[8, 32],
                     help="LAMB moment storage (default: 32 for --engine step, 8 = the reference's CPULAMB8Bit for collab)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--allreduce-algo", default=os.environ.get("DALLE_AMD_ALLREDUCE_ALGO", "rccl"), choices=["rccl", "rs_ag"],
-                    help="gradient all-reduce: one RCCL all_reduce per 64 MB bucket, or reduce-scatter + all-gather "
-                         "per bucket (the explicit direct-mesh form, average fused into the reduce-scatter)")
+    ap.add_argument("--allreduce-algo", default=os.environ.get("DALLE_AMD_ALLREDUCE_ALGO", "auto"),
+                    choices=["auto", "rccl", "rs_ag"],
+                    help="gradient all-reduce: one RCCL all_reduce per bucket, or reduce-scatter + all-gather per bucket "
+                         "(the explicit direct-mesh form, average fused into the reduce-scatter); auto (default): time "
+                         "both at every --bucket-mb candidate on the real communicator at start-up and keep the fastest")
+    ap.add_argument("--bucket-mb", default=os.environ.get("DALLE_AMD_BUCKET_MB", "auto"),
+                    help="gradient bucket size in MB, or auto: 16/32/64/128 MB timed at start-up (with --allreduce-algo)")
     ap.add_argument("--compression", default="none", choices=["none", "powersgd", "uniform8bit"],
                     help="gradient averaging: plain bucketed all-reduce, PowerSGD rank-4 with error feedback "
                          "(BASELINE config 3) or the hivemind size-adaptive fp16 / uniform-8-bit butterfly")
@@ -240,7 +244,24 @@ def run_rank(args) -> None:
         zero = None  # the collaborative optimizer resets the accumulated grads after each global step
     else:
         opt = _lamb(groups, bits, arena=arena)
-        sync_grads = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype, algo=args.allreduce_algo)
+        ar_tuning = None
+        algo = args.allreduce_algo
+        bucket_bytes = None if args.bucket_mb == "auto" else int(float(args.bucket_mb) * 2 ** 20)
+        if world > 1 and args.compression == "none" and (algo == "auto" or bucket_bytes is None):
+            # pick the all-reduce form for THIS mesh (xGMI point-to-point links, or gloo in the CPU rehearsal):
+            # every candidate timed over the real arena, max over ranks, so every rank selects the same one
+            from dalle_amd.parallel.dp import tune_grad_sync
+            algos = ("rccl", "rs_ag") if algo == "auto" else (algo,)
+            mbs = (16, 32, 64, 128) if bucket_bytes is None else (bucket_bytes / 2 ** 20,)
+            algo, bucket_bytes, ar_tuning = tune_grad_sync(arena, world, grad_dtype=args.grad_dtype, algos=algos,
+                                                        bucket_mb=mbs)
+        if algo == "auto":
+            algo = "rccl"
+        if bucket_bytes is None:
+            from dalle_amd.parallel.dp import DEFAULT_BUCKET_BYTES
+            bucket_bytes = DEFAULT_BUCKET_BYTES
+        args.allreduce_algo = algo
+        sync_grads = GradSync(arena, world_size=world, grad_dtype=args.grad_dtype, algo=algo, bucket_bytes=bucket_bytes)
         if args.compression == "powersgd":
             # compression work runs at every world size (the all-reduces are skipped only when world == 1)
             from dalle_amd.parallel.powersgd import PowerSGD
@@ -337,6 +358,9 @@ def run_rank(args) -> None:
         dist.all_gather_object(t_all, t_ar)
         t_ar = max(t_all)
         comm_stats = {"algo": args.allreduce_algo, "buckets": comm.bucket_busbw(),
+                      "selected": {"algo": args.allreduce_algo, "bucket_mb": round(comm.bucket_elems * 4 / 2 ** 20, 1),
+                                   "tuned": ar_tuning is not None},
+                      "tuning": ar_tuning,
                       "bytes_per_step": int(step_bytes), "standalone_ms": round(t_ar * 1e3, 3),
                       "busbw_GBps": round(2 * (world - 1) / world * step_bytes / t_ar / 1e9, 1),
                       "exposed_ms_per_step": None if exposed is None else round(exposed, 3),

@@ -24,7 +24,13 @@ where it applies) followed by an ``all_gather_into_tensor`` of the reduced shard
 the SAME bits for every element (each shard is reduced once, by one rank).
 
 ``grad_dtype='bf16'`` halves the bytes on the wire (RCCL then reduces in bf16, so the averaged gradient
-carries bf16 rounding -- use for large worlds only).
+carries bf16 rounding -- use for large worlds only). It overlaps with backward too: ``notify`` casts each
+final range into the preallocated bf16 wire buffer and launches its collective there; ``all_reduce()``
+copies the reduced ranges back.
+
+Neither the bucket size nor the algorithm is a guess for a given mesh: ``tune_grad_sync`` times the full
+arena all-reduce for every (algorithm, bucket size) candidate on the real communicator (max over ranks,
+so every rank picks the same one) and bench.py uses the fastest (``--allreduce-algo auto``).
 """
 from __future__ import annotations
 
@@ -64,11 +70,13 @@ class GradSync:
         self._pending_ag = []      # rs_ag without a fused average: (work, slice, shard) awaiting scale + gather
         self._keep = []            # rs_ag on RCCL: shards alive until their gathers complete
         self._fallback_ranges = []  # rs_ag: buckets that went through a plain all_reduce (length % world)
+        self._shards = None        # rs_ag on RCCL: one preallocated shard buffer, bucket b -> [b // N, ...)
+        self._lp_sent = []         # bf16 wire: ranges whose reduced values still have to be copied back
 
     # -------------------------------------------------------------------- overlap with backward
     def attach(self):
         """Let the fused backward hand over final grads as soon as they exist (see module doc)."""
-        if self.world_size > 1 and self.grad_dtype == "fp32":
+        if self.world_size > 1:
             from ..ops import hip_ops
 
             hip_ops.set_grad_ready_hook(self.notify)
@@ -82,31 +90,50 @@ class GradSync:
             hip_ops.set_grad_ready_hook(None)
             self._attached = False
 
-    def _launch(self, s: int, e: int):
+    def _wire(self):
+        """the tensor the collectives run on: the arena grads (fp32) or the bf16 wire copy"""
         g = self.arena.grad
+        if self.grad_dtype != "bf16":
+            return g
+        if self._lowp is None:
+            self._lowp = torch.empty(g.numel(), dtype=torch.bfloat16, device=g.device)
+        return self._lowp
+
+    def _launch(self, s: int, e: int):
+        g = self._wire()
+        if self.grad_dtype == "bf16":
+            g[s:e].copy_(self.arena.grad[s:e])   # cast the final range onto the wire (compute stream)
+            self._lp_sent.append((s, e))
         for b in range(s, e, self.bucket_elems):
             sl = g[b:min(e, b + self.bucket_elems)]
             if self.algo == "rs_ag" and sl.numel() % self.world_size == 0:
-                self._launch_rs_ag(sl)
+                self._launch_rs_ag(sl, b)
             else:
                 if self.algo == "rs_ag":
                     self._fallback_ranges.append((b, b + sl.numel()))
                 self._works.append(dist.all_reduce(sl, group=self.group, async_op=True))
         self._sent.append((s, e))
 
-    def _launch_rs_ag(self, sl: torch.Tensor):
+    def _launch_rs_ag(self, sl: torch.Tensor, b: int = 0):
         """Reduce-scatter the bucket into this rank's shard, then all-gather the reduced shards back into
         the bucket. On RCCL both are queued at once (one communicator stream orders them) and the 1/N
-        average rides in the reduce-scatter (ReduceOp.AVG); elsewhere the gather waits for the reduction."""
+        average rides in the reduce-scatter (ReduceOp.AVG); elsewhere the gather waits for the reduction.
+        Shards come from one preallocated buffer: the bucket starting at arena element ``b`` (length a
+        multiple of N) owns ``[b // N, b // N + len / N)``, disjoint from every other bucket's."""
         n = sl.numel() // self.world_size
-        shard = torch.empty(n, dtype=sl.dtype, device=sl.device)
-        avg = self.average and sl.is_cuda and dist.get_backend(self.group) == "nccl"
+        nccl = sl.is_cuda and dist.get_backend(self.group) == "nccl"
+        if nccl:
+            if self._shards is None or self._shards.dtype != sl.dtype:
+                self._shards = torch.empty(self.arena.numel // self.world_size + 1, dtype=sl.dtype, device=sl.device)
+            shard = self._shards[b // self.world_size:b // self.world_size + n]
+        else:
+            shard = torch.empty(n, dtype=sl.dtype, device=sl.device)
+        avg = self.average and nccl
         w = dist.reduce_scatter_tensor(shard, sl, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=self.group,
                                        async_op=True)
-        if sl.is_cuda and dist.get_backend(self.group) == "nccl":
+        if nccl:
             self._works.append(w)
             self._works.append(dist.all_gather_into_tensor(sl, shard, group=self.group, async_op=True))
-            self._keep.append(shard)
         else:
             self._pending_ag.append((w, sl, shard))
 
@@ -137,7 +164,7 @@ class GradSync:
                 self._finish_rs_ag()
                 for w in self._works:
                     w.wait()
-                self._works, self._sent, self._keep, self._fallback_ranges = [], [], [], []
+                self._works, self._sent, self._keep, self._fallback_ranges, self._lp_sent = [], [], [], [], []
             sync()
             t = (time.perf_counter() - t0) / reps
             ts = [None] * self.world_size
@@ -205,29 +232,24 @@ class GradSync:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         self.bytes_reduced += g.numel() * (2 if self.grad_dtype == "bf16" else 4)
+        for s, e in self._remaining():
+            self._launch(s, e)
+        self._finish_rs_ag()
+        for w in self._works:
+            w.wait()
+        self._works, self._sent, self._keep = [], [], []
         if self.grad_dtype == "bf16":
-            if self._lowp is None:
-                self._lowp = torch.empty(g.numel(), dtype=torch.bfloat16, device=g.device)
             lp = self._lowp
-            lp.copy_(g)
-            works = [dist.all_reduce(lp[s:e], group=self.group, async_op=True) for s, e in self.buckets]
-            for w in works:
-                w.wait()
-            g.copy_(lp)
-        else:
-            for s, e in self._remaining():
-                self._launch(s, e)
-            self._finish_rs_ag()
-            for w in self._works:
-                w.wait()
-            self._works, self._sent, self._keep = [], [], []
-            self.last_early_elems, self.early_elems = self.early_elems, 0
+            for s, e in self._lp_sent:
+                g[s:e].copy_(lp[s:e])
+            self._lp_sent = []
+        self.last_early_elems, self.early_elems = self.early_elems, 0
         if ev0 is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self._exposed.append((ev0, ev1))
         if self.average:
-            if self.algo == "rs_ag" and self.grad_dtype == "fp32":
+            if self.algo == "rs_ag":
                 # buckets that went through rs_ag are averaged already; all_reduce fallbacks (a bucket whose
                 # length is not a multiple of the world) still need the scale
                 self._scale_fallbacks(g)
@@ -238,3 +260,42 @@ class GradSync:
         for b0, b1 in self._fallback_ranges:
             g[b0:b1].mul_(1.0 / self.world_size)
         self._fallback_ranges = []
+
+
+@torch.no_grad()
+def tune_grad_sync(arena: FlatArena, world_size: int, group=None, grad_dtype: str = "fp32",
+                   algos=("rccl", "rs_ag"), bucket_mb=(16, 32, 64, 128), reps: int = 3):
+    """Time the full-arena gradient all-reduce for every (algorithm, bucket size) candidate on the real
+    communicator and return ``(algo, bucket_bytes, table)`` of the fastest. Times are the max over ranks
+    (``all_gather_object``), so every rank sees the same table and selects the same candidate. The arena
+    grads are restored afterwards. With one rank there is nothing to tune: the defaults come back."""
+    import time
+
+    if world_size <= 1:
+        return "rccl", DEFAULT_BUCKET_BYTES, []
+    g = arena.grad
+    saved = g.clone()
+    sync = torch.cuda.synchronize if g.is_cuda else (lambda: None)
+    table = []
+    for algo in algos:
+        for mb in bucket_mb:
+            gs = GradSync(arena, world_size=world_size, group=group, grad_dtype=grad_dtype,
+                          bucket_bytes=mb * 2 ** 20, algo=algo)
+            gs.all_reduce()          # warm-up: communicator paths, shard / wire buffers
+            sync()
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                gs.all_reduce()
+            sync()
+            t = (time.perf_counter() - t0) / reps
+            ts = [None] * world_size
+            dist.all_gather_object(ts, t, group=group)
+            t = max(ts)
+            nbytes = g.numel() * (2 if grad_dtype == "bf16" else 4)
+            table.append({"algo": algo, "bucket_mb": mb, "ms": round(t * 1e3, 3),
+                          "busbw_GBps": round(2 * (world_size - 1) / world_size * nbytes / t / 1e9, 1)})
+            g.copy_(saved)
+    best = min(table, key=lambda r: (r["ms"], r["algo"], r["bucket_mb"]))
+    del saved
+    return best["algo"], best["bucket_mb"] * 2 ** 20, table

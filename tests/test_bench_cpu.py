@@ -36,6 +36,12 @@ def test_bench_spawns_n_ranks(tmp_path, engine):
         ar = res["grad_allreduce"]
         assert ar["bytes_per_step"] > 0 and ar["busbw_GBps"] > 0 and ar["standalone_ms"] > 0
         assert 0.0 <= ar["overlapped_frac"] <= 1.0
+        # --allreduce-algo / --bucket-mb auto: every (algorithm, bucket) candidate timed on the real communicator
+        # at start-up, the fastest selected -- the same on every rank (the params below stay bitwise identical)
+        sel, table = ar["selected"], ar["tuning"]
+        assert sel["tuned"] and len(table) == 8 and {r["algo"] for r in table} == {"rccl", "rs_ag"}
+        best = min(table, key=lambda r: (r["ms"], r["algo"], r["bucket_mb"]))
+        assert (sel["algo"], sel["bucket_mb"]) == (best["algo"], best["bucket_mb"]) == (ar["algo"], sel["bucket_mb"])
     assert torch.equal(p0, p1)  # replicas stay bitwise identical
     if engine == "collab":
         assert res["config"]["engine"] == "CollaborativeOptimizer.step"
@@ -103,3 +109,13 @@ def test_bench_under_torchrun(tmp_path, n):
     assert res["config"]["parallelism"] == f"dp{n}" and res["config"]["global_batch"] == 2 * n
     ps = [torch.load(tmp_path / f"params.rank{r}.pt", weights_only=True) for r in range(n)]
     assert all(torch.equal(ps[0], p) for p in ps[1:])
+
+
+def test_bench_bf16_wire(tmp_path):
+    """--grad-dtype bf16 with a fixed bucket and algorithm (no tuning): ranks stay bitwise identical (the
+    hand-over from inside backward is covered by tests/test_dp_cpu.py)."""
+    res, p0, p1 = _run(tmp_path, "--grad-dtype", "bf16", "--allreduce-algo", "rs_ag", "--bucket-mb", "1")
+    ar = res["grad_allreduce"]
+    assert res["config"]["grad_allreduce_dtype"] == "bf16" and ar["selected"]["bucket_mb"] == 1.0
+    assert not ar["selected"]["tuned"] and ar["tuning"] is None
+    assert torch.equal(p0, p1)
