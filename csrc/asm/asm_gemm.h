@@ -1,0 +1,13 @@
+// Hand-scheduled assembly GEMMs (csrc/asm/gen_gemm.py): C[M, N] = A[M, K] . B[N, K]^T, bf16 operands,
+// fp32 accumulation. M, N multiples of 256, K a multiple of 64 and >= 256; rows of A / B / C are lda / ldb /
+// ldc elements apart. Returns false (launches nothing) for unsupported shapes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dalle {
+
+bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, const void* aux0, const void* aux1,
+                 const void* aux2, int M, int N, int K, int lda, int ldb, int ldc, int ld_aux, int flags, hipStream_t st);
+int asm_gemm_grid(int num_tiles);
+
+}  // namespace dalle

@@ -9,6 +9,7 @@
 
 #include "kernels/geom.h"
 #include "blaslt/lt_tuned.h"
+#include "asm/asm_gemm.h"
 
 namespace dalle {
 
@@ -635,6 +636,35 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
   }
   auto C = torch::empty({M, N}, A.options());
   TORCH_CHECK(dalle::gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, M, N, K, (int)variant, cur_stream()));
+  return C;
+}
+
+// ---- hand-scheduled assembly GEMMs (csrc/asm/gen_gemm.py): C = A . B^T (+ fp32 bias) ----
+// A (M, K), B (N, K) bf16 (row strides free, K-contiguous); M, N multiples of 256, K of 64, K >= 256
+Tensor asm_gemm(Tensor A, Tensor B, c10::optional<Tensor> bias, c10::optional<Tensor> out) {
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "asm_gemm: bf16 cuda");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "asm_gemm: A (M, K) and B (N, K)");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "asm_gemm: K-contiguous operands");
+  const int M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 256, "asm_gemm: M, N multiples of 256, K of 64 (>= 256)");
+  TORCH_CHECK((int64_t)M * A.stride(0) * 2 < (1ll << 40) && A.stride(0) < (1 << 20) && B.stride(0) < (1 << 20), "asm_gemm: strides");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN((*bias), torch::kFloat32);
+    TORCH_CHECK(bias->numel() == N, "asm_gemm: bias (N,) fp32");
+    bp = bias->data_ptr();
+  }
+  Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == torch::kBFloat16 && C.dim() == 2 && C.size(0) == M && C.size(1) == N && C.stride(1) == 1,
+                "asm_gemm: out (M, N) bf16");
+  } else {
+    C = torch::empty({M, N}, A.options());
+  }
+  TORCH_CHECK(dalle::asm_gemm_nt(bp ? "dalle_gemm_nt_bias" : "dalle_gemm_nt_plain", A.data_ptr(), B.data_ptr(), C.data_ptr(), bp,
+                                 nullptr, nullptr, M, N, K, (int)A.stride(0), (int)B.stride(0), (int)C.stride(0), 0, 0, cur_stream()),
+              "asm_gemm: launch failed");
   return C;
 }
 
@@ -1364,6 +1394,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
+  m.def("asm_gemm", &asm_gemm, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out") = py::none());
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
   m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),
         py::arg("n"), py::arg("col_major"), py::arg("qscale"), py::arg("persist") = -1);

@@ -32,7 +32,13 @@ hip_sources = [
     "csrc/kernels/conv.hip",
     "csrc/optim/lamb.hip",
     "csrc/blaslt/lt_tuned.cpp",
+    "csrc/asm/asm_gemm.cpp",
 ]
+
+# the hand-scheduled assembly kernels: generate + assemble + embed (csrc/asm/gemm_hsaco.inc) before compiling
+import subprocess, sys  # noqa: E401,E402
+
+subprocess.run([sys.executable, os.path.join(ROOT, "csrc/asm/build_asm.py")], check=True)
 
 # Plain setuptools Extension (not CUDAExtension): CUDAExtension would run hipify over the sources.
 # These kernels are written for CDNA4 directly; BuildExtension compiles the .hip files with hipcc.
