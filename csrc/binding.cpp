@@ -8,7 +8,6 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include "kernels/geom.h"
-#include "blaslt/lt_tuned.h"
 #include "asm/asm_gemm.h"
 
 namespace dalle {
@@ -31,7 +30,6 @@ void scale_residual_bwd(const float*, const void*, const float*, void*, float*, 
 void nonfinite(const float*, long, int*, hipStream_t);
 void zero_if_flag(float*, long, const int*, hipStream_t);
 bool gemm_nt(const void*, const void*, void*, const void*, int, int, int, int, hipStream_t);
-bool gemm_wgrad(const void*, const void*, float*, float*, int, int, int, int, int, hipStream_t);
 void uq8_compress(const float*, long, uint8_t*, float*, void*, hipStream_t);
 size_t uq8_workspace_bytes();
 void uq8_dequant(const uint8_t*, const float*, float*, long, float, int, hipStream_t);
@@ -44,7 +42,6 @@ std::vector<int> skinny_shape_info(int, int, int, int);
 bool gemm_qkv_rope(const void*, const void*, void*, void*, void*, const float*, const float*, int, int, int, int, int, int, int,
                    float, hipStream_t);
 void splitk_accum(const float*, float*, long, int, int, hipStream_t);
-void splitk_accum_t(const float*, float*, int, int, int, int, hipStream_t);
 void psgd_orthonormalize(float*, const long*, const int*, int, int, float, hipStream_t);
 bool psgd_reconstruct(float*, float*, const float*, const float*, long, int, int, hipStream_t);
 void xent_fwd_bwd(void*, const int64_t*, float*, long, int, float, hipStream_t);
@@ -61,7 +58,6 @@ bool conv_out(const void*, const void*, const float*, const float*, const float*
               int, int, hipStream_t);
 void softmax_rows(const float*, void*, long, int, float, hipStream_t);
 long xent_colsum_blocks(long, int);
-void xent_set_reg(int);
 void embed_bwd(const float*, const int*, const int*, const int*, float*, float*, int, int, hipStream_t);
 void decode_ln_shift(float*, const float*, const float*, void*, void*, const int*, const DecodeGeom&, int, int, int, hipStream_t,
                      const float*, const void*, const float*, int);
@@ -85,10 +81,6 @@ int gemm_cpol();
 void gemm_set_lines(int);
 void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
-void attn_set_pf(int, int);
-void attn_set_dkdv_qt(int);
-void attn_set_fwd_tps(int);
-void attn_set_dq_stage(int);
 void gemm_set_geglu_bwd_2wg(int);
 void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
@@ -124,124 +116,6 @@ static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream()
 #define CHECK_IN(x, dt) CHECK_CUDA(x); CHECK_CONTIG(x); CHECK_DT(x, dt)
 
 // ---------------------------------------------------------------------------------------------
-// hipBLASLt strided-batched bf16 -> fp32 product with a measured solution (csrc/blaslt/lt_tuned.cpp):
-// out (s, N, K) = a (s, N, ms) . b (s, ms, K) for the split-K weight-gradient views (each operand with a
-// unit stride in one of its two matrix dims). tune: on the first call for this problem, time every
-// supported solution (one warm-up, `reps` timed runs, a run-to-run bitwise check) and keep the fastest
-// reproducible one. Returns the chosen solution index (0 = hipBLASLt's heuristic pick).
-static dalle::LtProblem lt_problem_of(const Tensor& a, const Tensor& b, const Tensor& out) {
-  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && out.dim() == 3, "lt_bmm: 3-D operands");
-  const long s = a.size(0), N = a.size(1), ms = a.size(2), K = b.size(2);
-  TORCH_CHECK(b.size(0) == s && b.size(1) == ms && out.size(0) == s && out.size(1) == N && out.size(2) == K, "lt_bmm: shapes");
-  dalle::LtProblem p;
-  p.m = K;
-  p.n = N;
-  p.k = ms;
-  p.batch = s;
-  p.ldc = K;
-  p.sc = N * K;
-  if (b.stride(2) == 1) {  // X1 = B^T stored column-major (K x ms)
-    p.opA = HIPBLAS_OP_N;
-    p.lda = b.stride(1);
-    TORCH_CHECK(p.lda >= K, "lt_bmm: b leading dim");
-  } else {
-    TORCH_CHECK(b.stride(1) == 1, "lt_bmm: b needs a unit stride");
-    p.opA = HIPBLAS_OP_T;  // stored column-major (ms x K)
-    p.lda = b.stride(2);
-    TORCH_CHECK(p.lda >= ms, "lt_bmm: b leading dim");
-  }
-  if (a.stride(2) == 1) {  // X2 = A^T stored column-major (ms x N)
-    p.opB = HIPBLAS_OP_N;
-    p.ldb = a.stride(1);
-    TORCH_CHECK(p.ldb >= ms, "lt_bmm: a leading dim");
-  } else {
-    TORCH_CHECK(a.stride(1) == 1, "lt_bmm: a needs a unit stride");
-    p.opB = HIPBLAS_OP_T;  // stored column-major (N x ms)
-    p.ldb = a.stride(2);
-    TORCH_CHECK(p.ldb >= N, "lt_bmm: a leading dim");
-  }
-  p.sa = b.stride(0);
-  p.sb = a.stride(0);
-  return p;
-}
-
-static Tensor lt_ws(const Tensor& like, size_t bytes) {
-  return torch::empty({(long)std::max<size_t>(bytes, 1)}, like.options().dtype(torch::kUInt8));
-}
-
-int64_t lt_bmm_(Tensor a, Tensor b, Tensor out, bool tune, int64_t reps) {
-  CHECK_CUDA(out);
-  CHECK_CONTIG(out);
-  CHECK_DT(out, torch::kFloat32);
-  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
-              "lt_bmm: bf16 GPU operands");
-  const dalle::LtProblem p = lt_problem_of(a, b, out);
-  hipStream_t st = cur_stream();
-  const void* X1 = b.data_ptr();
-  const void* X2 = a.data_ptr();
-  float* C = out.data_ptr<float>();
-  if (tune && !dalle::lt_tuned(p)) {
-    const int n = dalle::lt_count(p);
-    size_t wsmax = 1;
-    for (int i = 0; i < n; ++i) wsmax = std::max(wsmax, dalle::lt_ws_bytes(p, i));
-    auto ws = lt_ws(out, wsmax);
-    auto ref = torch::empty_like(out);
-    hipEvent_t e0, e1;
-    TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "lt_bmm: events");
-    int best = 0;
-    double best_us = 1e30;
-    for (int i = 0; i < n; ++i) {
-      dalle::lt_run_idx(p, i, X1, X2, C, ws.data_ptr(), st);
-      ref.copy_(out);
-      TORCH_CHECK(hipEventRecord(e0, st) == hipSuccess, "lt_bmm: event");
-      for (int r = 0; r < reps; ++r) dalle::lt_run_idx(p, i, X1, X2, C, ws.data_ptr(), st);
-      TORCH_CHECK(hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess, "lt_bmm: event");
-      float ms = 0.f;
-      TORCH_CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess, "lt_bmm: event time");
-      const double us = 1000.0 * ms / std::max<int64_t>(reps, 1);
-      if (us < best_us && torch::equal(ref, out)) {
-        best_us = us;
-        best = i;
-      }
-    }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    dalle::lt_choose(p, best);
-  }
-  auto ws = lt_ws(out, dalle::lt_ws_bytes(p, dalle::lt_chosen(p)));
-  dalle::lt_run_idx(p, -1, X1, X2, C, ws.data_ptr(), st);
-  return dalle::lt_chosen(p);
-}
-
-// the same search, reported: [(solution, microseconds, reproducible, kernel name)] for this problem (does not
-// change the chosen solution)
-std::vector<std::tuple<int64_t, double, bool, std::string>> lt_bmm_survey(Tensor a, Tensor b, Tensor out, int64_t reps) {
-  CHECK_CUDA(out);
-  const dalle::LtProblem p = lt_problem_of(a, b, out);
-  hipStream_t st = cur_stream();
-  const int n = dalle::lt_count(p);
-  size_t wsmax = 1;
-  for (int i = 0; i < n; ++i) wsmax = std::max(wsmax, dalle::lt_ws_bytes(p, i));
-  auto ws = lt_ws(out, wsmax);
-  auto ref = torch::empty_like(out);
-  hipEvent_t e0, e1;
-  TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "lt_bmm_survey: events");
-  std::vector<std::tuple<int64_t, double, bool, std::string>> res;
-  for (int i = 0; i < n; ++i) {
-    dalle::lt_run_idx(p, i, b.data_ptr(), a.data_ptr(), out.data_ptr<float>(), ws.data_ptr(), st);
-    ref.copy_(out);
-    TORCH_CHECK(hipEventRecord(e0, st) == hipSuccess, "event");
-    for (int r = 0; r < reps; ++r) dalle::lt_run_idx(p, i, b.data_ptr(), a.data_ptr(), out.data_ptr<float>(), ws.data_ptr(), st);
-    TORCH_CHECK(hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess, "event");
-    float ms = 0.f;
-    TORCH_CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess, "event time");
-    res.emplace_back(i, 1000.0 * ms / std::max<int64_t>(reps, 1), torch::equal(ref, out), dalle::lt_solution_name(p, i));
-  }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return res;
-}
-
 static int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -261,8 +135,6 @@ static dalle::AttnGeom make_attn_geom(int T, int S, int n, int K, int H, int pat
   g.K = K;
   g.H = H;
   g.pattern = pattern;
-  if (const char* e = getenv("DALLE_AMD_ATTN_DIAG")) g.diag = atoi(e);
-  if (const char* e = getenv("DALLE_AMD_ATTN_STAGGER")) g.stagger = atoi(e);
   TORCH_CHECK(g.I % 32 == 0, "image grid must be a multiple of 32 tokens");
   TORCH_CHECK(n == T + g.I - 1, "sequence length must be text_len + image_seq_len - 1");
   return g;
@@ -611,17 +483,6 @@ void splitk_accum_(Tensor acc, Tensor part, bool accumulate) {
   dalle::splitk_accum(part.data_ptr<float>(), acc.data_ptr<float>(), n, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
 }
 
-// acc (R, C) (+)= sum_k part[k]^T with part (s, C, R): the weight-gradient fold of the transposed
-// split-K product (x^T g is the faster hipBLASLt problem for N_out > K_in)
-void splitk_accum_t_(Tensor acc, Tensor part, bool accumulate) {
-  CHECK_IN(acc, torch::kFloat32); CHECK_IN(part, torch::kFloat32);
-  TORCH_CHECK(acc.dim() == 2 && part.dim() == 3 && part.size(1) == acc.size(1) && part.size(2) == acc.size(0),
-              "splitk_accum_t: part (s, C, R) for acc (R, C)");
-  const int R = acc.size(0), C = acc.size(1);
-  TORCH_CHECK(R % 32 == 0 && C % 32 == 0, "splitk_accum_t: R, C multiples of 32");
-  dalle::splitk_accum_t(part.data_ptr<float>(), acc.data_ptr<float>(), R, C, (int)part.size(0), accumulate ? 1 : 0, cur_stream());
-}
-
 // C = A . B^T (+ bias): A (M, K), B (N, K) bf16, both K-contiguous; M, N multiples of 256, K of 64
 Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) {
   CHECK_IN(A, torch::kBFloat16); CHECK_IN(B, torch::kBFloat16);
@@ -762,21 +623,6 @@ Tensor permlane16_probe() {
   CHECK_CUDA(out);
   dalle::permlane16_probe((unsigned*)out.data_ptr<int>(), cur_stream());
   return out;
-}
-
-// dW (N, K) fp32 (+)= G^T X: G (M, N), X (M, K) bf16 row-major (tokens on the rows of both), the
-// hand-written MN-major MFMA GEMM split `splits` ways over the tokens (deterministic fold)
-void gemm_wgrad_(Tensor G, Tensor X, Tensor out, int64_t splits, bool accumulate) {
-  CHECK_IN(G, torch::kBFloat16); CHECK_IN(X, torch::kBFloat16); CHECK_IN(out, torch::kFloat32);
-  TORCH_CHECK(G.dim() == 2 && X.dim() == 2 && G.size(0) == X.size(0), "gemm_wgrad: G (M, N), X (M, K)");
-  const int M = G.size(0), N = G.size(1), K = X.size(1);
-  TORCH_CHECK(out.dim() == 2 && out.size(0) == N && out.size(1) == K, "gemm_wgrad: out must be (N, K)");
-  TORCH_CHECK(N % 256 == 0 && K % 256 == 0, "gemm_wgrad: N, K multiples of 256");
-  TORCH_CHECK(splits >= 1 && M % (splits * 64) == 0, "gemm_wgrad: M must be a multiple of 64 * splits");
-  Tensor ws;
-  if (splits > 1) ws = torch::empty({splits, N, K}, out.options());
-  TORCH_CHECK(dalle::gemm_wgrad(G.data_ptr(), X.data_ptr(), out.data_ptr<float>(), splits > 1 ? ws.data_ptr<float>() : nullptr, M,
-                                N, K, (int)splits, accumulate ? 1 : 0, cur_stream()));
 }
 
 // ---- decode-step skinny GEMMs (M <= 64): one launch each, epilogue fused ----
@@ -1346,7 +1192,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("gbias") = py::none());
   m.def("nonfinite", &nonfinite);
   m.def("splitk_accum_", &splitk_accum_);
-  m.def("splitk_accum_t_", &splitk_accum_t_);
   m.def("psgd_orthonormalize_", &psgd_orthonormalize_);
   m.def("psgd_reconstruct_", &psgd_reconstruct_);
   m.def("qkv_rope", &qkv_rope);
@@ -1375,17 +1220,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 cur_stream()), "gemm_2wg: M % 256, N % 128, K % 32 (K >= 64)");
     return C;
   });
-  m.def("lt_bmm_", &lt_bmm_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("tune") = true, py::arg("reps") = 3,
-        "out (s, N, K) fp32 = a (s, N, ms) . b (s, ms, K) bf16 on hipBLASLt with a measured solution per problem");
-  m.def("lt_bmm_survey", &lt_bmm_survey, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("reps") = 3);
-  m.def("attn_set_dq_stage", [](int64_t v) { dalle::attn_set_dq_stage((int)v); }, py::arg("stage"),
-        "dQ kernel text staging: 0 register pairs (default), 2 / 3 LDS-DMA tiles per barrier step");
-  m.def("attn_set_fwd_tps", [](int64_t t) { dalle::attn_set_fwd_tps((int)t); }, py::arg("tps"),
-        "text tiles per barrier step of the attention forward: 2 (default) or 3");
-  m.def("attn_set_dkdv_qt", [](int64_t qt) { dalle::attn_set_dkdv_qt((int)qt); }, py::arg("qt"),
-        "query tiles per barrier step of the text dK/dV kernel: 4 (default) or 2");
-  m.def("attn_set_pf", [](int64_t f, int64_t q) { dalle::attn_set_pf((int)f, (int)q); }, py::arg("fwd"), py::arg("dq"),
-        "attention forward / dQ: load the first local key tile before the text phase (1) or after it (0)");
   m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },
         py::arg("overlap"), py::arg("stagger_pct") = 0,
         "persistent plain GEMM: epilogue stores beside the next tile's first K-step; start stagger in % of a tile");
@@ -1402,11 +1236,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("persist") = -1);
   m.def("ff_in_geglu_pt", &ff_in_geglu_pt, py::arg("x"), py::arg("w1i"), py::arg("b1i") = py::none(), py::arg("persist") = -1);
   m.def("permlane16_probe", &permlane16_probe);
-  m.def("gemm_wgrad_", &gemm_wgrad_, py::arg("G"), py::arg("X"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
   m.def("embed_fwd", &embed_fwd);
   m.def("xent_colsum_", &xent_colsum_);
-  m.def("xent_set_reg", &dalle::xent_set_reg, "1: register-resident cross-entropy kernels where the vocabulary fits, 0: LDS form");
   m.def("conv3x3", &conv3x3, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("res") = py::none(),
         py::arg("mean") = py::none(), py::arg("rstd") = py::none(), py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
         py::arg("ups") = false);

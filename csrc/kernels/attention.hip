@@ -156,17 +156,6 @@ __device__ __forceinline__ void xcd_remap(int& grp, int& bh) {
   grp = j - (j / ng) * ng;
 }
 
-// measurement (AttnGeom::stagger): equal-length workgroups launched together stay in lockstep, so the 3
-// co-resident workgroups of a CU would wait on memory at the same moments; delay the first 768 (slot
-// s = L >> 8 of the breadth-first dispatch) by s x ticks
-__device__ __forceinline__ void attn_stagger(const AttnGeom& g) {
-  if (g.stagger <= 0) return;
-  const int L = blockIdx.x + blockIdx.y * gridDim.x;
-  if (L >= 768) return;
-  const unsigned long long until = __builtin_amdgcn_s_memrealtime() + (unsigned long long)((L >> 8) * g.stagger);
-  while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(4);
-}
-
 // first local (image) key tile needed by image query block qb
 __device__ __forceinline__ int local_lo_tile(const AttnGeom& g, int qb) {
   const int kq0 = qb * 32 - g.Tp;
@@ -396,7 +385,6 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TPS * TILE];  // 32 / 48 KB
   int grp, bh;
   xcd_remap(grp, bh);
-  attn_stagger(g);
   const int b = bh / g.H, h = bh - b * g.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
@@ -416,7 +404,7 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   SoftmaxState st;
   // phase B's first local (image) key tile, loaded NOW into registers: its HBM latency then hides under
   // phase A instead of being exposed after the last text pair (each local tile is read by one query tile)
-  const bool has_local = active && qb >= ntext && !(g.diag & 4);
+  const bool has_local = active && qb >= ntext;
   const int lo = has_local ? local_lo_tile(g, qb) : 0;
   s16x8 kr[4], vr[4];
   auto load_loc = [&](int t) {
@@ -450,12 +438,11 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Q is in registers before step 0 refills buffer 1
   __syncthreads();
   for (int si = 0; si < nsteps; ++si) {
-    const bool more = si + 1 < nsteps && !(g.diag & 1);
+    const bool more = si + 1 < nsteps;
     if (more) dma_step(si + 1, (si + 1) & 1);  // that buffer was released by the previous step's barrier
     const __bf16* S0 = smem + (si & 1) * (2 * TPS * TILE);
     const int ta = TPS * si, tb = ta + 1;
-    if (g.diag & 32) {
-    } else if (tb < my_text_end) {
+    if (tb < my_text_end) {
       const __bf16* const Ks[2] = {S0, S0 + TILE};
       const __bf16* const Vs[2] = {S0 + TPS * TILE, S0 + (TPS + 1) * TILE};
       const int kt[2] = {ta, tb};
@@ -466,14 +453,14 @@ __global__ __launch_bounds__(256, MINB) void attn_fwd_kernel(const __bf16* __res
       const int kt[1] = {ta};
       fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
-    if (TPS == 3 && !(g.diag & 32) && ta + 2 < my_text_end) {
+    if (TPS == 3 && ta + 2 < my_text_end) {
       const __bf16* const Ks[1] = {S0 + 2 * TILE};
       const __bf16* const Vs[1] = {S0 + (TPS + 2) * TILE};
       const int kt[1] = {ta + 2};
       fwd_tiles<1>(st, Ks, Vs, kt, qf, g, qb, qs, lane);
     }
     __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next step's tiles landed (this wave's pieces) before the barrier
-    if (!(g.diag & 2)) __syncthreads();
+    __syncthreads();
   }
 
   // ---- phase B: this wave's local (image) key tiles, private LDS slot {K, V} ----
@@ -605,7 +592,6 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   __shared__ float dsh[4][32];                                          // prologue: per wave row deltas
   int grp, bh;
   xcd_remap(grp, bh);
-  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int qb0 = grp * 4;
@@ -625,83 +611,60 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   // dK/dV kernels that run next on the stream
   bf16x8 qf[4], dof[4];
   float dl = 0.f;
-  if (!(g.diag & 256)) {
-    // Q (4 KB of contiguous storage rows) and dO (32 gathered 128-B token rows) of this wave through its 8 KB
-    // LDS slot (phase A's buffers are not in use yet), 8 lanes per row: every load instruction covers 8 whole
-    // 128-B lines, where the per-lane operand-layout loads touched 32 lines per instruction (round 4). delta
-    // = rowsum(dO * O) from the same registers, reduced over each row's 8 lanes (fixed xor tree).
-    __bf16* Ps = smem + wave * (2 * TILE);
-    float dpart[4];
+  {
+  // Q (4 KB of contiguous storage rows) and dO (32 gathered 128-B token rows) of this wave through its 8 KB
+  // LDS slot (phase A's buffers are not in use yet), 8 lanes per row: every load instruction covers 8 whole
+  // 128-B lines, where the per-lane operand-layout loads touched 32 lines per instruction (round 4). delta
+  // = rowsum(dO * O) from the same registers, reduced over each row's 8 lanes (fixed xor tree).
+  __bf16* Ps = smem + wave * (2 * TILE);
+  float dpart[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+    const int srow = (active ? qb * 32 : 0) + row;
+    const int toff = tok_row(g, srow);
+    const s16x8 qv = *reinterpret_cast<const s16x8*>(Q + base + (size_t)srow * 64 + col);
+    const s16x8 dv = ld_tok(dob, toff, col);
+    *reinterpret_cast<s16x8*>(Ps + lds_idx(row, col)) = qv;
+    *reinterpret_cast<s16x8*>(Ps + TILE + lds_idx(row, col)) = dv;
+    dpart[j] = 0.f;
+    if (!delta_ready) {
+      const s16x8 ov = ld_tok(outb, toff, col);
+      float fd[8], fo[8];
+      unpack8(dv, fd);
+      unpack8(ov, fo);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dpart[j] = fmaf(fd[i], fo[i], dpart[j]);
+    }
+  }
+  if (!delta_ready) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
-      const int srow = (active ? qb * 32 : 0) + row;
-      const int toff = tok_row(g, srow);
-      const s16x8 qv = *reinterpret_cast<const s16x8*>(Q + base + (size_t)srow * 64 + col);
-      const s16x8 dv = ld_tok(dob, toff, col);
-      *reinterpret_cast<s16x8*>(Ps + lds_idx(row, col)) = qv;
-      *reinterpret_cast<s16x8*>(Ps + TILE + lds_idx(row, col)) = dv;
-      dpart[j] = 0.f;
-      if (!delta_ready) {
-        const s16x8 ov = ld_tok(outb, toff, col);
-        float fd[8], fo[8];
-        unpack8(dv, fd);
-        unpack8(ov, fo);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dpart[j] = fmaf(fd[i], fo[i], dpart[j]);
+      dpart[j] += __shfl_xor(dpart[j], 1, 64);
+      dpart[j] += __shfl_xor(dpart[j], 2, 64);
+      dpart[j] += __shfl_xor(dpart[j], 4, 64);
+      const int row = 8 * j + (lane >> 3);
+      if ((lane & 7) == 0) {
+        dsh[wave][row] = dpart[j];
+        if (active) delta[(size_t)bh * g.Np + qb * 32 + row] = dpart[j];
       }
     }
-    if (!delta_ready) {
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot and the row deltas are written
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dpart[j] += __shfl_xor(dpart[j], 1, 64);
-        dpart[j] += __shfl_xor(dpart[j], 2, 64);
-        dpart[j] += __shfl_xor(dpart[j], 4, 64);
-        const int row = 8 * j + (lane >> 3);
-        if ((lane & 7) == 0) {
-          dsh[wave][row] = dpart[j];
-          if (active) delta[(size_t)bh * g.Np + qb * 32 + row] = dpart[j];
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot and the row deltas are written
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      qf[s2] = row_operand(Ps, s2, lane & 31, hl);
-      dof[s2] = row_operand(Ps + TILE, s2, lane & 31, hl);
-    }
-    dl = delta_ready ? delta[(size_t)bh * g.Np + qrow] : dsh[wave][lane & 31];
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __syncthreads();  // every wave has its operands in registers before phase A refills the buffers
-  } else {
-    const int qoff = tok_row(g, qrow);
-    const __bf16* qp = Q + base + (size_t)qrow * 64 + 8 * hl;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = ld16(qp + 16 * s);
-      const s16x8 d = ld_tok(dob, qoff, 16 * s + 8 * hl);
-      dof[s] = __builtin_bit_cast(bf16x8, d);
-      if (!delta_ready) {
-        const s16x8 o = ld_tok(outb, qoff, 16 * s + 8 * hl);
-        float fd[8], fo[8];
-        unpack8(d, fd);
-        unpack8(o, fo);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dl = fmaf(fd[i], fo[i], dl);
-      }
-    }
-    if (delta_ready) {
-      dl = delta[(size_t)bh * g.Np + qrow];
-    } else {
-      dl += __shfl_xor(dl, 32, 64);
-      if (active && hl == 0) delta[(size_t)bh * g.Np + qrow] = dl;
-    }
+  for (int s2 = 0; s2 < 4; ++s2) {
+    qf[s2] = row_operand(Ps, s2, lane & 31, hl);
+    dof[s2] = row_operand(Ps + TILE, s2, lane & 31, hl);
+  }
+  dl = delta_ready ? delta[(size_t)bh * g.Np + qrow] : dsh[wave][lane & 31];
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();  // every wave has its operands in registers before phase A refills the buffers
   }
   const float lq = lse[(size_t)bh * g.Np + qrow];
   f32x16 dq0 = {}, dq1 = {};
   // PREFETCH_LOCAL: phase B's first local key tile loaded before phase A (see attn_fwd_kernel)
-  const bool has_local = active && qb >= ntext && !(g.diag & 4);
+  const bool has_local = active && qb >= ntext;
   const int lo = has_local ? local_lo_tile(g, qb) : 0;
   s16x8 kr[4], vr[4];
   auto load_loc = [&](int t) {
@@ -731,17 +694,17 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
     __builtin_amdgcn_s_waitcnt(WAIT_VM0);
     __syncthreads();
     for (int si = 0; si < nsteps; ++si) {
-      const bool more = si + 1 < nsteps && !(g.diag & 1);
+      const bool more = si + 1 < nsteps;
       if (more) dma_step(si + 1, (si + 1) & 1);  // that buffer was released by the previous step's barrier
       const __bf16* S0 = smem + (si & 1) * (2 * TPS * TILE);
 #pragma unroll
       for (int t = 0; t < TPS; ++t) {
         const int tile = TPS * si + t;
-        if (tile < my_text_end && !(g.diag & 32))
+        if (tile < my_text_end)
           dq_tile(dq0, dq1, S0 + t * TILE, S0 + (TPS + t) * TILE, tile, qf, dof, lq, dl, g, qb, qs, lane);
       }
       __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next step's tiles landed (this wave's pieces) before the barrier
-      if (!(g.diag & 2)) __syncthreads();
+      __syncthreads();
     }
   } else {
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
@@ -766,14 +729,14 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   store_pair(0);
   __syncthreads();
   for (int pi = 0; pi < npairs; ++pi) {
-    const bool more = pi + 1 < npairs && !(g.diag & 1);
+    const bool more = pi + 1 < npairs;
     if (more) load_pair(pi + 1);
     const __bf16* S0 = smem + (pi & 1) * (4 * TILE);
     const int ta = 2 * pi, tb = 2 * pi + 1;
-    if (ta < my_text_end && !(g.diag & 32)) dq_tile(dq0, dq1, S0, S0 + 2 * TILE, ta, qf, dof, lq, dl, g, qb, qs, lane);
-    if (tb < my_text_end && !(g.diag & 32)) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
+    if (ta < my_text_end) dq_tile(dq0, dq1, S0, S0 + 2 * TILE, ta, qf, dof, lq, dl, g, qb, qs, lane);
+    if (tb < my_text_end) dq_tile(dq0, dq1, S0 + TILE, S0 + 3 * TILE, tb, qf, dof, lq, dl, g, qb, qs, lane);
     if (more) store_pair((pi + 1) & 1);
-    if (!(g.diag & 2)) __syncthreads();
+    __syncthreads();
   }
   }
 
@@ -796,7 +759,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
       __builtin_amdgcn_wave_barrier();
     }
   }
-  if (FUSE_LOCAL && active && qb >= ntext && ro.dqkv && !(g.diag & 64)) {
+  if (FUSE_LOCAL && active && qb >= ntext && ro.dqkv) {
     // key-centric pass over the diagonal tile: K / V rows of the tile's keys (lane = key) from the slot,
     // then the slot is refilled with this wave's Q / dO tile (lane = query row) and the row stats
     __bf16* P = smem + wave * (2 * TILE);
@@ -862,7 +825,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   // the epilogue's per-wave staging slot (4 KB at wave * 4 KB) overlaps other waves' phase-B slots
   __syncthreads();
 
-  if (!active || (g.diag & 128)) return;
+  if (!active) return;
   if (ro.dqkv) {  // the loop's last barrier released smem: each wave stages through its own 8 KB
     float* stage = reinterpret_cast<float*>(smem) + wave * 2048;
     rope_bwd_store_full(ro, g, bh, qb * 32, 0, dq0, dq1, ro.qscale, stage, lane);
@@ -899,7 +862,6 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_kernel(const __bf16* 
   __shared__ float stats[4][2][32];                                   // per wave {lse, delta}
   int grp, bh;
   xcd_remap(grp, bh);
-  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nkb = g.Np >> 5, ntext = g.Tp >> 5;
   const int kb = ntext + grp * 4 + wave;
@@ -1022,13 +984,12 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
   __shared__ float stats[2][QT][2][32];  // [stage][tile][lse | delta][row]
   int grp, bh;
   xcd_remap(grp, bh);
-  attn_stagger(g);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, c32 = lane & 31;
   const int nqb = g.Np >> 5, ntext = g.Tp >> 5;
   const int kb0 = grp * 2;
   // odd last key block (QT 4): all four waves work on it, wave w taking the query tile t = w of each
   // step, instead of two waves idling on the absent partner block
-  const bool tail = QT == 4 && kb0 + 1 >= ntext && !(g.diag & 512);
+  const bool tail = QT == 4 && kb0 + 1 >= ntext;
   const int kb = tail ? kb0 : kb0 + (wave & 1), par = tail ? wave : wave >> 1;
   const bool active = kb < ntext;
   const size_t base = (size_t)bh * g.Np * 64;
@@ -1128,7 +1089,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
   // (measured: issuing the second tile's score products ahead of the first tile's softmax -- a
   // two-tile software pipeline -- made this kernel slower at B128: 677-690 us against 642 us)
   for (int i = 0; i < nsteps; ++i) {
-    const bool more = i + 1 < nsteps && !(g.diag & 8);
+    const bool more = i + 1 < nsteps;
     if (more) load_step(i + 1);
     const int buf = i & 1;
 #pragma unroll
@@ -1144,7 +1105,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
       }
     }
     if (more) store_step((i + 1) & 1);
-    if (!(g.diag & 16)) __syncthreads();
+    __syncthreads();
   }
   // the other parity's waves hand their partials to the parity 0 wave of the same key block through
   // LDS (value-major layout: consecutive lanes on consecutive banks), which sums (fixed order) and
@@ -1205,92 +1166,17 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-// Occupancy variant per kernel (workgroups per CU the register budget is compiled for), overridable
-// with DALLE_AMD_ATTN_OCC="fwd,dq,dkdv_text,dkdv". Measured at B48 (profiles/r1_attn_occupancy.txt):
-// the forward is latency-bound at 2 waves/SIMD (178 VGPRs) and runs 225 -> 183 us at 3 (168 VGPRs,
-// 20 B/lane of spill); dq fits 148 VGPRs either way; the dK/dV kernels spill 184-292 B/lane at 3 and
-// slow down 1.9-2.8x, so they stay at 2.
-static int attn_occ(int which) {
-  static int occ[4] = {0, 0, 0, 0};
-  if (occ[0] == 0) {
-    int v[4] = {3, 3, 2, 2};
-    if (const char* e = getenv("DALLE_AMD_ATTN_OCC")) sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]);
-    for (int i = 0; i < 4; ++i) occ[i] = (v[i] == 3) ? 3 : 2;
-  }
-  return occ[which];
-}
-
-#define ATTN_LAUNCH(kern, which, grid, ...)                                                      \
-  do {                                                                                           \
-    if (attn_occ(which) == 3) hipLaunchKernelGGL(kern<3>, grid, dim3(256), 0, st, __VA_ARGS__); \
-    else hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, st, __VA_ARGS__);                      \
-  } while (0)
-
-// DALLE_AMD_ATTN_PF=<fwd>,<dq> (default 0,0; measured slower at occupancy 3: more spills): load phase B's first local key tile before phase A;
-// attn_set_pf overrides it at run time (benchmarks)
-static int g_attn_pf[2] = {-1, -1};
-static int attn_pf(int which) {
-  if (g_attn_pf[0] < 0) {
-    int v[2] = {0, 0};
-    if (const char* e = getenv("DALLE_AMD_ATTN_PF")) sscanf(e, "%d,%d", &v[0], &v[1]);
-    g_attn_pf[0] = v[0];
-    g_attn_pf[1] = v[1];
-  }
-  return g_attn_pf[which];
-}
-// DALLE_AMD_ATTN_FWD_TPS=2|3: text tiles staged per barrier step of the forward (attn_set_fwd_tps overrides)
-static int g_fwd_tps = -1;
-static int attn_fwd_tps() {
-  if (g_fwd_tps < 0) {
-    const char* e = getenv("DALLE_AMD_ATTN_FWD_TPS");
-    g_fwd_tps = (e && atoi(e) == 3) ? 3 : 2;
-  }
-  return g_fwd_tps;
-}
-void attn_set_fwd_tps(int t) { g_fwd_tps = t == 3 ? 3 : 2; }
-// DALLE_AMD_ATTN_DQ_STAGE=0|2|3: the dQ kernel's text-tile staging (0 register-staged pairs; 2 / 3 LDS-DMA, two /
-// three tiles per barrier step); attn_set_dq_stage overrides it at run time
-static int g_dq_stage = -1;
-static int attn_dq_stage() {
-  if (g_dq_stage < 0) {
-    const char* e = getenv("DALLE_AMD_ATTN_DQ_STAGE");
-    const int v = e ? atoi(e) : 0;
-    g_dq_stage = (v == 2 || v == 3) ? v : 0;
-  }
-  return g_dq_stage;
-}
-void attn_set_dq_stage(int v) { g_dq_stage = (v == 2 || v == 3) ? v : 0; }
-// DALLE_AMD_DKDV_QT=4|2: query tiles staged per barrier step of the text dK/dV kernel (default 4: half the
-// barrier steps, bitwise-identical results, -0.9 ms of attention per bench24 B128 step; attn_set_dkdv_qt
-// overrides it at run time)
-static int g_dkdv_qt = -1;
-static int attn_dkdv_qt() {
-  if (g_dkdv_qt < 0) {
-    const char* e = getenv("DALLE_AMD_DKDV_QT");
-    g_dkdv_qt = (e && atoi(e) == 2) ? 2 : 4;
-  }
-  return g_dkdv_qt;
-}
-void attn_set_dkdv_qt(int qt) { g_dkdv_qt = qt == 2 ? 2 : 4; }
-void attn_set_pf(int fwd, int dq) {
-  g_attn_pf[0] = fwd;
-  g_attn_pf[1] = dq;
-}
-
+// Occupancy per kernel (workgroups per CU the register budget is compiled for), measured at B48
+// (profiles/r1_attn_occupancy.txt): the forward is latency-bound at 2 waves/SIMD (178 VGPRs) and runs
+// 225 -> 183 us at 3 (168 VGPRs); dq fits 148 VGPRs at 3; the dK/dV kernels spill at 3 and slow down
+// 1.9-2.8x, so they stay at 2. Staging per barrier step: forward 2 text tiles (3 measured slower), dQ
+// register-staged text pairs (LDS-DMA measured slower), text dK/dV 4 query tiles (-0.9 ms per bench24
+// B128 step vs 2); local-tile prefetch off (more spills at occupancy 3). Round-4 numbers of every
+// variant: profiles/r4ab_switches_b128.txt, profiles/INDEX.md.
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
   dim3 grid((g.Np / 32 + 3) / 4, BH);
-  const bool pf = attn_pf(0) != 0;
-  const bool t3 = !pf && attn_fwd_tps() == 3;
-  const __bf16 *qq = (const __bf16*)q, *kk = (const __bf16*)k, *vv = (const __bf16*)v;
-  if (attn_occ(0) == 3) {
-    if (pf) hipLaunchKernelGGL((attn_fwd_kernel<3, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-    else if (t3) hipLaunchKernelGGL((attn_fwd_kernel<3, false, 3>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-    else hipLaunchKernelGGL((attn_fwd_kernel<3, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-  } else {
-    if (pf) hipLaunchKernelGGL((attn_fwd_kernel<2, true>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-    else if (t3) hipLaunchKernelGGL((attn_fwd_kernel<2, false, 3>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-    else hipLaunchKernelGGL((attn_fwd_kernel<2, false>), grid, dim3(256), 0, st, qq, kk, vv, (__bf16*)out, lse, g);
-  }
+  hipLaunchKernelGGL((attn_fwd_kernel<3, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                     (const __bf16*)v, (__bf16*)out, lse, g);
 }
 
 void attn_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
@@ -1299,80 +1185,22 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   const RopeOut ro{cosT, sinT, static_cast<__bf16*>(dqkv), qscale};
   dim3 grid((g.Np / 32 + 3) / 4, BH);
   // axial row / col: every image key tile is attended by exactly its own query tile -> dK / dV of the
-  // image keys inside the dQ kernel (rotary-fused output path; DALLE_AMD_ATTN_FUSE_LOCAL=0 disables)
-  const char* fl = getenv("DALLE_AMD_ATTN_FUSE_LOCAL");
-  const bool fuse_local = dqkv != nullptr && (g.pattern == 1 || g.pattern == 2) && !(fl && fl[0] == '0');
-  // DALLE_AMD_ATTN_BWD_CONC=1: delta by its own small kernel, then the dK/dV kernels on a side stream
-  // run concurrently with the dQ kernel (both latency / VALU bound, each ~50 % of wave-cycles waiting)
-  static const bool conc = [] { const char* e = getenv("DALLE_AMD_ATTN_BWD_CONC"); return e && e[0] == '1'; }();
+  // image keys inside the dQ kernel (rotary-fused output path)
+  const bool fuse_local = dqkv != nullptr && (g.pattern == 1 || g.pattern == 2);
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
-  hipStream_t kst = st;
-  static hipStream_t side[64] = {};
-  static hipEvent_t ev_in[64] = {}, ev_out[64] = {};
-  int dev = 0;
-  if (conc) {
-    (void)hipGetDevice(&dev);
-    if (side[dev] == nullptr) {
-      (void)hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
-      (void)hipEventCreateWithFlags(&ev_in[dev], hipEventDisableTiming);
-      (void)hipEventCreateWithFlags(&ev_out[dev], hipEventDisableTiming);
-    }
-    const long rows = (long)BH * g.Np;
-    hipLaunchKernelGGL(attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st, (const __bf16*)dout,
-                       (const __bf16*)out, delta, g, BH);
-    (void)hipEventRecord(ev_in[dev], st);
-    (void)hipStreamWaitEvent(side[dev], ev_in[dev], 0);
-    kst = side[dev];
-  }
-  auto launch_dkdv = [&](hipStream_t s2) {
-    // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
-    hipStream_t st = s2;
-    if (attn_dkdv_qt() == 4 && attn_occ(2) == 2)
-      hipLaunchKernelGGL((attn_bwd_dkdv_text_kernel<2, 4>), dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q,
-                         (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
-    else
-      ATTN_LAUNCH(attn_bwd_dkdv_text_kernel, 2, dim3((ntext + 1) / 2, BH), (const __bf16*)q, (const __bf16*)k,
-                  (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
-    // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
-    if (!fuse_local) ATTN_LAUNCH(attn_bwd_dkdv_kernel, 3, dim3((nimg + 3) / 4, BH), (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
-  };
-  if (conc) launch_dkdv(kst);
-  const int dr = conc ? 1 : 0;
-  const bool pfq = attn_pf(1) != 0;
-  const int stage = pfq ? 0 : attn_dq_stage();
-#define DQ_LAUNCH(MB, FL, PF, STG)                                                                                    \
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<MB, FL, PF, STG>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,  \
-                     (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, dr)
-#define DQ_STAGES(MB, FL)                   \
-  do {                                      \
-    if (stage == 2) DQ_LAUNCH(MB, FL, false, 2); \
-    else if (stage == 3) DQ_LAUNCH(MB, FL, false, 3); \
-    else DQ_LAUNCH(MB, FL, false, 0);       \
-  } while (0)
-  if (fuse_local) {
-    if (attn_occ(1) == 3) {
-      if (pfq) DQ_LAUNCH(3, true, true, 0);
-      else DQ_STAGES(3, true);
-    } else {
-      if (pfq) DQ_LAUNCH(2, true, true, 0);
-      else DQ_STAGES(2, true);
-    }
-  } else if (attn_occ(1) == 3) {
-    DQ_STAGES(3, false);
-  } else {
-    DQ_STAGES(2, false);
-  }
-#undef DQ_STAGES
-#undef DQ_LAUNCH
-  if (conc) {
-    // the caller's stream resumes only after the side-stream kernels: every later use of the outputs,
-    // and every reuse of the inputs' memory by the caching allocator, is ordered after them
-    (void)hipEventRecord(ev_out[dev], kst);
-    (void)hipStreamWaitEvent(st, ev_out[dev], 0);
-  } else {
-    launch_dkdv(st);
-  }
+  if (fuse_local)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, false, 0>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, 0);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false, false, 0>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, 0);
+  // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
+  hipLaunchKernelGGL((attn_bwd_dkdv_text_kernel<2, 4>), dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q,
+                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
+  // image key blocks (short, local patterns): four blocks per workgroup -- unless the dQ kernel did them
+  if (!fuse_local)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2>), dim3((nimg + 3) / 4, BH), dim3(256), 0, st, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, g, ro);
 }
 
 }  // namespace dalle

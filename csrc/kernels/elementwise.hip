@@ -262,37 +262,6 @@ void scale_residual_bwd(const float* g, const void* y, const float* scale, void*
                      D);
   column_sum(part, blocks, 2 * D, sink, st);
 }
-// Transposing fold: acc (R, C) (+)= sum_k part[k] (C, R)^T, the k slabs added in order. 32 x 32 tiles
-// through LDS (padded rows): slab reads coalesced along R... of the slab's rows, writes along acc's rows.
-__global__ __launch_bounds__(256) void splitk_accum_t_kernel(const float* __restrict__ part, float* __restrict__ acc, int R,
-                                                             int C, int s, int accumulate) {
-  __shared__ float tile[32][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  // slab element (c, r) for c = c0 + ty + 8 j, r = r0 + tx: consecutive lanes read consecutive r
-  for (int k = 0; k < s; ++k) {
-    const float* pk = part + (size_t)k * R * C;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += pk[(size_t)(c0 + ty + 8 * j) * R + r0 + tx];
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) tile[ty + 8 * j][tx] = v[j];
-  __syncthreads();
-  // acc element (r, c) for r = r0 + ty + 8 j, c = c0 + tx
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = r0 + ty + 8 * j;
-    float* d = acc + (size_t)r * C + c0 + tx;
-    const float t = tile[tx][ty + 8 * j];
-    *d = accumulate ? *d + t : t;
-  }
-}
-
-void splitk_accum_t(const float* part, float* acc, int R, int C, int s, int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(splitk_accum_t_kernel, dim3(R / 32, C / 32), dim3(256), 0, st, part, acc, R, C, s, accumulate);
-}
-
 void splitk_accum(const float* part, float* acc, long n, int s, int accumulate, hipStream_t st) {
   const long t = n / 4;
   hipLaunchKernelGGL(splitk_accum_kernel, dim3((t + 255) / 256), dim3(256), 0, st, part, acc, n, s, accumulate);

@@ -1021,38 +1021,6 @@ bool gemm_geglu_bwd(const void* dy, const void* w2t, const void* h, void* dh, fl
   return true;
 }
 
-// Weight gradient dW (N_out, K_in) fp32 = G^T X over Mtok tokens, G (Mtok, N_out) and X (Mtok, K_in)
-// bf16 row-major: the MN-major 8-phase kernel, token range split `splits` ways over blockIdx.y. One
-// split accumulates (or stores) straight into `out`; more write fp32 slabs to `ws` (splits x N x K)
-// that splitk_accum folds in split order (deterministic).
-void splitk_accum(const float* part, float* acc, long n, int s, int accumulate, hipStream_t st);
-int gemm_drain();
-bool gemm_wgrad(const void* G, const void* X, float* out, float* ws, int Mtok, int Nout, int Kin, int splits, int accumulate,
-                hipStream_t st) {
-  if (Nout % GBM || Kin % GBN || splits < 1 || Mtok % (splits * GBK)) return false;
-  if (splits > 1 && ws == nullptr) return false;
-  RopeEpi e{};
-  e.drain = gemm_drain();
-  const int tiles = (Nout / GBM) * (Kin / GBN);
-  const int kt = Mtok / splits;
-  dim3 grid(tiles, splits);
-  if (splits == 1) {
-    e.fout = out;
-    if (accumulate)
-      hipLaunchKernelGGL((gemm_nt_8ph_kernel<4, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
-                         (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
-    else
-      hipLaunchKernelGGL((gemm_nt_8ph_kernel<3, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
-                         (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
-    return true;
-  }
-  e.fout = ws;
-  hipLaunchKernelGGL((gemm_nt_8ph_kernel<3, 0, 1>), grid, dim3(G_THREADS), 0, st, (const __bf16*)G, (const __bf16*)X,
-                     (__bf16*)nullptr, (const __bf16*)nullptr, Nout, Kin, kt, e, 4);
-  splitk_accum(ws, out, (long)Nout * Kin, splits, accumulate, st);
-  return true;
-}
-
 // QKV projection + rotary into the attention storage layout (q pre-scaled); M = B*n rows
 bool gemm_qkv_rope(const void* A, const void* W, void* q, void* k, void* v, const float* cosT, const float* sinT, int M, int K,
                    int H, int T, int S, int n, int col_major, float qscale, hipStream_t st) {

@@ -13,8 +13,6 @@ struct AttnGeom {
   int K;        // conv window
   int H;        // heads
   int pattern;  // 0 full, 1 axial_row, 2 axial_col, 3 conv_like
-  int stagger = 0;  // measurement (DALLE_AMD_ATTN_STAGGER=<ticks>): the first 3 x 256 workgroups start (L >> 8) x ticks late
-  int diag = 0;  // measurement only (DALLE_AMD_ATTN_DIAG): skip parts of a kernel -- forward / dQ: 1 = the text-tile staging, 2 = its barriers, 4 = the local tiles, 32 = the text tiles' compute; dQ: 64 = the fused local dK/dV, 128 = the dQ stores, 256 = the round-3 per-lane prologue loads; text dK/dV: 8 = the staging, 16 = its barriers, 512 = off: the four-wave split of an odd last key block
 };
 struct RopeGeom {
   int T, Tp, S, logS, n, Np, H, col_major;

@@ -293,15 +293,8 @@ __global__ __launch_bounds__(64 * W) void xent_reg_kernel(__bf16* __restrict__ l
 }
 
 // which form runs: 2 = register-resident, 4 waves (V <= 8192, 16-B rows), 1 = register-resident, 16
-// waves (V <= 32768, 8-B rows), 0 = the LDS-accumulator kernel. DALLE_AMD_XENT_REG=0 forces the latter.
-static int g_xent_reg = -1;  // -1: DALLE_AMD_XENT_REG (default 1); xent_set_reg overrides (tests, A/B)
-void xent_set_reg(int v) { g_xent_reg = v; }
+// waves (V <= 32768, 8-B rows), 0 = the LDS-accumulator kernel (wider vocabularies).
 static int xent_form(int V) {
-  if (g_xent_reg < 0) {
-    const char* e = getenv("DALLE_AMD_XENT_REG");
-    g_xent_reg = e ? atoi(e) : 1;
-  }
-  if (!g_xent_reg) return 0;
   if (V % 8 == 0 && V <= 4 * 4 * 64 * 8) return 2;
   if (V % 4 == 0 && V <= 8 * 16 * 64 * 4) return 1;
   return 0;

@@ -100,51 +100,36 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
     return _cached(("t", id(w)), w, make)
 
 
-NT_INPUT_GRAD = os.environ.get("DALLE_AMD_NT_DGRAD", "1") != "0"
-# plain (epilogue-free) projection GEMMs on the hand-written register-epilogue kernel (csrc/kernels/gemm_pt.hip,
-# one tile per workgroup, whole-line epilogue stores) instead of hipBLASLt. DALLE_AMD_OWN_GEMM: "auto" (default) =
-# the (N, K) shapes in OWN_GEMM_SHAPES, measured faster than hipBLASLt at the training token counts
-# (benchmarks/bench_gemm_lines.py); "1" = every shape that tiles; "0" = none; "N:K,N:K,..." = those shapes
-_own_env = os.environ.get("DALLE_AMD_OWN_GEMM", "auto")
-OWN_GEMM_SHAPES = set()
-OWN_GEMM = 0 if _own_env == "0" else (2 if _own_env == "1" else 1)
-if ":" in _own_env:
-    OWN_GEMM_SHAPES = {tuple(int(v) for v in t.split(":")) for t in _own_env.split(",") if t}
-OWN_GEMM_MIN_M = 16384  # below this the grid does not fill the chip's 256 CUs several times over
+# Plain projections (no fused epilogue beyond a bias) run on the hand-scheduled assembly GEMM
+# (csrc/asm/gen_gemm.py: hipBLASLt's own gfx950 structure -- 4 waves, 128x128 AGPR quadrants, LDS-DMA two
+# K-steps ahead -- with every instruction placed by the generator) wherever the shape tiles; hipBLASLt
+# otherwise. DALLE_AMD_ASM_GEMM=0 sends every plain product to hipBLASLt (A/B).
+ASM_GEMM = os.environ.get("DALLE_AMD_ASM_GEMM", "0") != "0"
 
 
-def _own_gemm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+def _asm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     return (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
-            and a.is_contiguous() and b.is_contiguous() and a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0
-            and a.shape[1] % 64 == 0 and a.shape[1] >= 128)
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0
+            and a.shape[1] % 64 == 0 and a.shape[1] >= 256 and a.shape[1] == b.shape[1])
 
 
-def own_gemm_for(M: int, N: int, K: int) -> bool:
-    """Whether the plain product (M, K) x (N, K)^T goes to the hand-written GEMM (DALLE_AMD_OWN_GEMM policy)."""
-    if OWN_GEMM == 2:
-        return True
-    return OWN_GEMM == 1 and M >= OWN_GEMM_MIN_M and (N, K) in OWN_GEMM_SHAPES
-
-
-def mm_nt(a: torch.Tensor, b: torch.Tensor, bias=None) -> torch.Tensor:
-    """a (M, K) . b (N, K)^T (+ bias): the hand-written GEMM where the policy picks it and the shape tiles,
-    else hipBLASLt."""
-    if OWN_GEMM and _own_gemm_ok(a, b) and own_gemm_for(a.shape[0], b.shape[0], a.shape[1]):
-        _count("own_gemm")
-        return C().gemm_pt(a, b, bias, 10, 0)
+def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a (M, K) . b (N, K)^T (+ bias, the fp32 parameter): the assembly GEMM where the shape tiles, else
+    hipBLASLt (with the bias rounded to bf16, the library's epilogue type)."""
+    if ASM_GEMM and _asm_ok(a, b):
+        _count("asm_gemm")
+        bf = None if bias is None else bias.detach().float().contiguous()
+        return C().asm_gemm(a, b, bf, None)
     if bias is not None:
-        return torch.addmm(bias, a, b.t())
+        return torch.addmm(bf16_weight(bias), a, b.t())
     return torch.mm(a, b.t())
 
 
 def input_grad(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = g W for a Linear weight W (out, in), computed as g . (W^T)^T from the cached transposed bf16
-    copy: with W^T contiguous hipBLASLt runs the NT form of the product, 12-20 % faster than the NN form
-    at every training input-gradient shape (M = 61440: 1041 vs 895, 1230 vs 1100, 1432 vs 1192 TF/s;
-    ``benchmarks/bench_gemm_layouts.py``, profiles/r2_gemm_layouts.jsonl). DALLE_AMD_NT_DGRAD=0: NN form."""
-    if NT_INPUT_GRAD:
-        return mm_nt(g, bf16_weight_t(w))
-    return torch.mm(g, bf16_weight(w))
+    copy: the NT form of the product (hipBLASLt also runs it 12-20 % faster than the NN form at every
+    training input-gradient shape, profiles/r2_gemm_layouts.jsonl)."""
+    return mm_nt(g, bf16_weight_t(w))
 
 
 _tables: Dict[tuple, tuple] = {}
@@ -185,35 +170,6 @@ def _cs_from_tables(cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     return t
 
 
-# FF-in GEMM with the GEGLU forward in its epilogue (csrc/kernels/gemm_pt.hip EPI 3)
-FUSED_FF_IN = int(os.environ.get("DALLE_AMD_FUSED_FF_IN", "0"))
-
-
-def geglu_interleaved(t: torch.Tensor) -> torch.Tensor:
-    """bf16 copy of W1 (2F, K) / b1 (2F,) with rows in the fused FF-in kernel's order (cached per forward)."""
-    def make():
-        F = t.shape[0] // 2
-        return t.detach().index_select(0, geglu_interleave_index(F, t.device)).to(torch.bfloat16).contiguous()
-
-    return _cached(("geglu_i", id(t)), t, make)
-
-
-_perm_cache: Dict[tuple, torch.Tensor] = {}
-
-
-def geglu_interleave_index(F: int, device) -> torch.Tensor:
-    """Row order of W1 / b1 for the fused FF-in GEGLU GEMM: per 64-row group g, the 32 value rows
-    32g .. 32g+31 followed by the matching gate rows F + 32g .. F + 32g + 31, so each wave's 64 output
-    columns hold a feature's value and gate side by side (csrc/kernels/gemm_pt.hip EPI 3)."""
-    key = (F, str(device))
-    idx = _perm_cache.get(key)
-    if idx is None:
-        g = torch.arange(F // 32).view(-1, 1) * 32 + torch.arange(32).view(1, -1)  # (F/32, 32) feature ids
-        idx = torch.cat([g, g + F], dim=1).reshape(-1).to(device)
-        _perm_cache[key] = idx
-    return idx
-
-
 # ---------------------------------------------------------------------------------------------
 # Linear: bf16 GEMM forward, fp32 weight grads accumulated straight into the fp32 grad buffer
 # ---------------------------------------------------------------------------------------------
@@ -226,8 +182,6 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
     405/533/687/834, 3072x1024 718/929/1009/984, 1024x4096 965/1007/1083/1032, 8192x1024
     1077/1125/1114/1053; at M = 81920 (micro-batch 64, profiles/r3_wgrad_splits_m81920.txt) the same
     choices win except 1024x1024, where 16 splits beat 8 (936 vs 904 TF)."""
-    if SPLITK_WGRAD == 0:
-        return 1
     nk = N * K
     s = (16 if M >= 81920 else 8) if nk <= 1536 * 1024 else (4 if nk <= 4608 * 1024 else 2)
     while s > 1 and (M % s or M // s < 1024):
@@ -235,29 +189,17 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
     return s
 
 
-SPLITK_WGRAD = int(os.environ.get("DALLE_AMD_SPLITK", "1"))
-# split-K weight grads as x^T g + a transposing fold when N_out > K_in
-WGRAD_TRANSPOSED = int(os.environ.get("DALLE_AMD_WGRAD_T", "0"))
-# weight grads on the hand-written MN-major GEMM (gemm_wgrad_) instead of hipBLASLt (opt-in, see weight_grad)
-OWN_WGRAD = int(os.environ.get("DALLE_AMD_OWN_WGRAD", "0"))
-# QKV projection through the hand-written GEMM with the rotary in its epilogue: 2 = the register-epilogue
-# kernel (csrc/kernels/gemm_pt.hip: 427 us vs 449 us for the LDS-staged 8-phase one, 1 = csrc/kernels/gemm.hip,
-# and 473 us for hipBLASLt + a rotary pass at the bench24 B48 shape; profiles/r3_gemm_pt_vs_hipblaslt_8ph.jsonl)
-FUSED_QKV_ROPE = int(os.environ.get("DALLE_AMD_FUSED_QKV", "2"))
-# rotary backward fused into the attention-backward epilogues (csrc/kernels/attention.hip RopeOut)
-FUSED_ROPE_BWD = int(os.environ.get("DALLE_AMD_FUSED_ROPE_BWD", "1"))
-# GEGLU backward fused into the FF-out dgrad GEMM epilogue (csrc/kernels/gemm.hip EPI 2)
-FUSED_GEGLU_DGRAD = int(os.environ.get("DALLE_AMD_FUSED_GEGLU_DGRAD", "1"))
-# which kernel runs it: "8ph" (gemm.hip, LDS-staged epilogue) or "pt" (gemm_pt.hip main loop, one tile per
-# workgroup, the same LDS-staged epilogue: pt_epilogue_geglu_bwd_lds)
-GEGLU_DGRAD_KERNEL = os.environ.get("DALLE_AMD_GEGLU_DGRAD_KERNEL", "8ph")
+# the QKV projection runs on the hand-written GEMM with the rotary in its register epilogue, writing the attention
+# storage layout directly (csrc/kernels/gemm_pt.hip: 427 us vs 473 us for hipBLASLt + a rotary pass at the
+# bench24 B48 shape, profiles/r3_gemm_pt_vs_hipblaslt_8ph.jsonl); the rotary backward runs in the attention-
+# backward epilogues and the GEGLU backward in the FF-out dgrad GEMM's epilogue (csrc/kernels/gemm.hip EPI 2).
 
 
 # weight-grad inputs kept token-contiguous: the LN outputs feeding the QKV and FF-in GEMMs are saved as
 # X^T (one bf16 transpose kernel, ~60 us per 168 MB) instead of X, and dW = g^T X runs on hipBLASLt with
 # a token-contiguous B operand: 3072x1024 1128 vs 847 TF/s, 8192x1024 1334 vs 1130 at M = 81920
-# (profiles/r3s5_wgrad_nt_vs_tn_m81920.txt). DALLE_AMD_WGRAD_XT=0 restores the token-major form.
-WGRAD_XT = int(os.environ.get("DALLE_AMD_WGRAD_XT", "1"))
+# (profiles/r3s5_wgrad_nt_vs_tn_m81920.txt).
+WGRAD_XT = True
 
 
 class XT:
@@ -277,7 +219,7 @@ class XT:
 # per 168 MB; the 1024x4096 product runs at 1265 vs 1106 TF/s in isolation): small but consistent in the full
 # step -- micro-batch 64 229.50 / 229.41 vs 229.54 / 229.63 ms, micro-batch 128 459.41 / 458.95 vs 460.09 /
 # 461.66 ms (same box each, profiles/r3s5_wgrad_xt_ab.txt)
-WGRAD_GT = int(os.environ.get("DALLE_AMD_WGRAD_GT", "1"))
+WGRAD_GT = True
 
 
 def saved_gemm_input(x2: torch.Tensor, enabled: Optional[bool] = None):
@@ -308,12 +250,6 @@ def wgrad_t_splits(M: int, N: int, K: int, form: str) -> int:
     return s
 
 
-# split-K weight grads on hipBLASLt with a measured solution per problem (csrc/blaslt/lt_tuned.cpp: every
-# supported solution timed once on first use, fastest bitwise-reproducible kept) instead of torch.bmm's
-# heuristic pick
-WGRAD_LT = int(os.environ.get("DALLE_AMD_WGRAD_LT", "0"))
-
-
 def _weight_grad_t(gw, fused: bool, g2, x2):
     """dW = g^T x with G and/or X given token-contiguous (XT): split-K batched hipBLASLt GEMM whose
     operands are strided views of the transposed copies (no gather), fp32 partials + the fold kernel."""
@@ -328,12 +264,7 @@ def _weight_grad_t(gw, fused: bool, g2, x2):
     b = xt.view(K, s, ms).transpose(0, 1).transpose(1, 2) if xt is not None else x2.view(s, ms, K)
     if s > 1:
         out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=a.device)
-        if WGRAD_LT:
-            part = torch.empty(s, N, K, dtype=torch.float32, device=a.device)
-            C().lt_bmm_(a, b, part, True, 3)
-            _count("wgrad_lt")
-        else:
-            part = torch.bmm(a, b, out_dtype=torch.float32)
+        part = torch.bmm(a, b, out_dtype=torch.float32)
         C().splitk_accum_(out, part, fused)
         return None if fused else out
     if fused:
@@ -353,91 +284,16 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2):
     if isinstance(x2, XT) or isinstance(g2, XT):
         return _weight_grad_t(gw, fused, g2, x2)
     M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
-    if OWN_WGRAD and N % 256 == 0 and K % 256 == 0 and g2.is_contiguous() and x2.is_contiguous():
-        # hand-written MN-major MFMA kernel; 15-20 % slower than hipBLASLt on the training shapes
-        # (profiles/r2_wgrad_mn_major_vs_hipblaslt.jsonl), so opt-in only
-        s = max(1, min(16, 256 // ((N // 256) * (K // 256))))
-        while s > 1 and M % (64 * s):
-            s -= 1
-        if M % 64 == 0:
-            out = gw if fused else torch.zeros(N, K, dtype=torch.float32, device=g2.device)
-            C().gemm_wgrad_(g2, x2, out, s, True)
-            return None if fused else out
     s = wgrad_splits(M, N, K)
     if s > 1:
         out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
-        if WGRAD_TRANSPOSED and N > K and N % 32 == 0 and K % 32 == 0:
-            # x^T g is the faster hipBLASLt problem in isolation when N_out > K_in (3072x1024: 961 vs 836
-            # TF/s, 8192x1024: 1192 vs 1111 at M = 61440, profiles/r2_wgrad_layouts.jsonl) but the full
-            # step measured the same (185.7 / 185.9 vs 185.0 / 186.1 ms, same box): opt-in
-            part = torch.bmm(x2.view(s, M // s, K).transpose(1, 2), g2.view(s, M // s, N), out_dtype=torch.float32)
-            C().splitk_accum_t_(out, part, fused)
-        else:
-            part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
-            C().splitk_accum_(out, part, fused)
+        part = torch.bmm(g2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
+        C().splitk_accum_(out, part, fused)
         return None if fused else out
     if fused:
         torch.addmm(gw, g2.t(), x2, out_dtype=torch.float32, out=gw)
         return None
     return torch.mm(g2.t(), x2, out_dtype=torch.float32)
-
-
-class _WgradOverlap:
-    """Weight-gradient GEMMs on a side HIP stream. Inside the fused stack's backward the wgrads
-    (dW = g^T x, accumulated into the arena) depend on nothing the main stream produces afterwards, so
-    they run concurrently with the next dgrad GEMMs, the attention backward and the bandwidth-bound
-    LN / GEGLU kernels. Inputs are kept alive on the host and released only after the main stream
-    has been made to wait for the side-stream work that read them (a GPU-side event wait, ``LAG``
-    submissions later) -- ``record_stream`` instead would defer the caching allocator's reuse of these
-    GB-sized blocks and force fresh allocations. The order of the accumulations into a shared block's
-    grad is unchanged (one side stream), so results are bitwise the same.
-
-    Off by default (``DALLE_AMD_WGRAD_STREAM=1`` enables it): on the bench24 step the concurrent
-    GEMMs contend for the CUs and L2 and the step is ~2% SLOWER (257.3 / 258.1 vs 262.9 samples/s on
-    one box, profiles/r1_wgrad_side_stream.txt)."""
-
-    LAG = 4
-
-    def __init__(self):
-        self.enabled = os.environ.get("DALLE_AMD_WGRAD_STREAM", "0") == "1"
-        self._streams = {}
-        self.stream = None
-        self._pending = []
-
-    def begin(self, device: torch.device) -> bool:
-        if not (self.enabled and device.type == "cuda") or torch.cuda.is_current_stream_capturing():
-            return False
-        st = self._streams.get(device.index)
-        if st is None:
-            st = self._streams[device.index] = torch.cuda.Stream(device=device)
-        self.stream = st
-        return True
-
-    def end(self):
-        if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
-            self.stream = None
-            self._pending.clear()
-
-    def __call__(self, w, g2, x2):
-        st = self.stream
-        if st is None:
-            return weight_grad(w, g2, x2)
-        main = torch.cuda.current_stream()
-        st.wait_stream(main)
-        with torch.cuda.stream(st):
-            r = weight_grad(w, g2, x2)
-            ev = torch.cuda.Event()
-            ev.record(st)
-        assert r is None, "side-stream weight grads must accumulate into the arena"
-        self._pending.append((ev, g2, x2))
-        while len(self._pending) > self.LAG:
-            old, _, _ = self._pending.pop(0)
-            main.wait_event(old)  # later main-stream reuse of those blocks is ordered after the read
-        return None
-
-
-_wgrad = _WgradOverlap()
 
 
 def grad_sink(p: torch.Tensor, needed: bool = True):
@@ -639,11 +495,7 @@ class _AttnCore(torch.autograd.Function):
         q, k, v, out, lse, cos, sin = ctx.saved_tensors
         B, T, S, n, K, H, pattern, col = ctx.geo
         gout = gout.to(torch.bfloat16).contiguous()
-        if FUSED_ROPE_BWD:
-            dqkv = C().attn_bwd_rope(q, k, v, out, gout, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125)
-        else:
-            dq, dk, dv = C().attn_bwd(q, k, v, out, gout, lse, B, T, S, n, K, H, pattern)
-            dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125)
+        dqkv = C().attn_bwd_rope(q, k, v, out, gout, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125)
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -691,12 +543,9 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     h2 = h.view(-1, d)
     wq = bf16_weight(w_qkv)
     col = pattern == PATTERN_IDS["axial_col"]
-    if FUSED_QKV_ROPE and (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0:
+    if (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0 and d >= 128:
         # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
-        if FUSED_QKV_ROPE == 2 and d >= 128:
-            q, k, v = C().qkv_rope_pt(h2, wq, _cs_from_tables(cos, sin), T, S, H, n, col, 0.125)
-        else:
-            q, k, v = C().qkv_rope(h2, wq, cos, sin, T, S, H, n, col, 0.125)
+        q, k, v = C().qkv_rope_pt(h2, wq, _cs_from_tables(cos, sin), T, S, H, n, col, 0.125)
         _count("qkv_rope")
     else:
         qkv = torch.mm(h2, wq.t()).view(B, n, -1)
@@ -704,7 +553,7 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
         del qkv
     out, lse = C().attn_fwd(q, k, v, B, T, S, n, K, H, pattern)
     wo = bf16_weight(w_out)
-    y = mm_nt(out.view(-1, out.shape[-1]), wo, bf16_weight(b_out))
+    y = mm_nt(out.view(-1, out.shape[-1]), wo, b_out)
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None
@@ -720,17 +569,12 @@ def _attn_core_bwd(saved, params, dy):
     dy = dy.view(-1, dy.shape[-1])
     o2 = out.view(-1, out.shape[-1])
     do = input_grad(dy, w_out).view(out.shape)
-    dwo = _wgrad(w_out, dy, o2)
-    if FUSED_ROPE_BWD:  # rotary backward inside the attention-backward epilogues
-        dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
-        del do
-    else:
-        dq, dk, dv = C().attn_bwd(q, k, v, out, do, lse, B, T, S, n, K, H, pattern)
-        del do
-        dqkv = C().rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).view(B * n, -1)
-        del dq, dk, dv
+    dwo = weight_grad(w_out, dy, o2)
+    # rotary backward inside the attention-backward epilogues
+    dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
+    del do
     dh = input_grad(dqkv, w_qkv).view(x.shape)
-    dwq = _wgrad(w_qkv, dqkv, h2)
+    dwq = weight_grad(w_qkv, dqkv, h2)
     return dh, dwq, dwo
 
 
@@ -739,16 +583,11 @@ def _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save: bool = T
     d = inp.shape[-1]
     h2 = h.view(-1, d)
     w1b, w2b = bf16_weight(w1), bf16_weight(w2)
-    if FUSED_FF_IN and _own_gemm_ok(h2, w1b) and w1b.shape[0] % 64 == 0:
-        # FF-in GEMM + bias + GEGLU in one kernel (W1 / b1 rows interleaved per 64-column group)
-        a, u = C().ff_in_geglu_pt(h2, geglu_interleaved(w1), geglu_interleaved(b1))
-        _count("ff_in_geglu")
-    else:
-        a = torch.addmm(bf16_weight(b1), h2, w1b.t())
-        u = C().geglu_fwd(a)
+    a = mm_nt(h2, w1b, b1)
+    u = C().geglu_fwd(a)
     if not save:
         del a
-    y = mm_nt(u, w2b, bf16_weight(b2))
+    y = mm_nt(u, w2b, b2)
     s = scale.reshape(-1).contiguous()
     if not save:
         return y, s, None
@@ -762,21 +601,18 @@ def _ff_core_bwd(saved, params, dy, sk):
     ln_w, ln_b, w1, b1, w2, b2, scale = params
     dy = dy.view(-1, dy.shape[-1])
     M, F = dy.shape[0], w2b.shape[1]
-    if FUSED_GEGLU_DGRAD and M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
+    if M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
-        if GEGLU_DGRAD_KERNEL == "pt" and dy.shape[1] >= 128:
-            da, db1 = C().ff_dgrad_geglu_pt(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None, 0)
-        else:
-            da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
+        da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
         _count("ff_dgrad_geglu")
-        dw2 = _wgrad(w2, saved_gemm_input(dy, WGRAD_GT), u)
+        dw2 = weight_grad(w2, saved_gemm_input(dy, WGRAD_GT), u)
     else:
         du = input_grad(dy, w2)
-        dw2 = _wgrad(w2, dy, u)
+        dw2 = weight_grad(w2, dy, u)
         da, db1 = C().geglu_bwd_bias(a, du, sk[3] if sk is not None else None)
         del du
     dh = input_grad(da, w1).view(x.shape)
-    dw1 = _wgrad(w1, da, h2)
+    dw1 = weight_grad(w1, da, h2)
     return dh, dw1, db1, dw2
 
 
@@ -853,7 +689,7 @@ def _residual_chain(res, y, s, sign, nxt):
     """res + sign * s * y (fp32) and, when ``nxt`` (the LN spec of the sublayer that reads it) is given, its
     LayerNorm(+shift) in the same kernel (ln_shift_fwd_res: one read of the residual stream instead of two)."""
     s = s if sign > 0 else -s
-    if nxt is None or not FUSED_SEQUENTIAL:
+    if nxt is None:
         xo = torch.empty_like(res)
         C().scale_residual_out(res.contiguous(), y, s, xo)
         return xo, None
@@ -1066,7 +902,7 @@ class _ReversibleFused(torch.autograd.Function):
         final = _final_at([fa[1] + ga[1] for fa, ga in blocks]) if hook is not None else None
         sinks = [(_sinks(fa[1], [p.requires_grad for p in fa[1]]), _sinks(ga[1], [p.requires_grad for p in ga[1]]))
                  for fa, ga in blocks]
-        if FUSED_SEQUENTIAL and all(a is not None and b is not None for a, b in sinks):
+        if all(a is not None and b is not None for a, b in sinks):
             dx = _ReversibleFused._backward_chained(blocks, stored, sinks, y1, y2, dy1, dy2, hook, final)
             return (dx, None, None, *([None] * len(ctx.params)))
         with torch.no_grad():
@@ -1182,7 +1018,6 @@ def reversible_stack(x, layers, geom: AttnGeometry, text_len: int, image_size: i
 # -- so the fp32 residual stream is read once per boundary in each direction instead of twice.
 # Parameter grads go straight to the flat-arena sinks (required; otherwise the per-sublayer nodes run).
 # ---------------------------------------------------------------------------------------------
-FUSED_SEQUENTIAL = int(os.environ.get("DALLE_AMD_FUSED_SEQUENTIAL", "1"))
 
 # per sublayer kind: (index of the LayerScale param, of the output-projection bias) in its param tuple
 _SCALE_BIAS = {"attn": (5, 4), "ff": (6, 5)}
@@ -1235,18 +1070,12 @@ class _SequentialFused(torch.autograd.Function):
                 reset = True
         sinks = [[grad_sink(p) for p in prm] for _, _, prm in subs]
         g = gout.float().contiguous()
-        overlap = _wgrad.begin(g.device)
-        try:
-            g = _SequentialFused._backward(subs, saved_all, sinks, g, handoff=not reset)
-        finally:
-            if overlap:
-                _wgrad.end()
+        g = _SequentialFused._backward(subs, saved_all, sinks, g, handoff=not reset)
         return (g, None, *([None] * len(ctx.params)))
 
     @staticmethod
     def _backward(subs, saved_all, sinks, g, handoff: bool = True):
-        # weight grads on the side stream (_wgrad) are not ordered before the hand-off: no early hand-off then
-        hook = _grad_ready_hook if (_wgrad.stream is None and handoff) else None
+        hook = _grad_ready_hook if handoff else None
         final = _final_at([prm for _, _, prm in subs]) if hook is not None else None
         with torch.no_grad():
             kind, args, prm = subs[-1]
@@ -1299,7 +1128,7 @@ def sequential_stack(x, subs):
             if id(p) not in seen:
                 seen.add(id(p))
                 uniq.append(p)
-    if not (FUSED_SEQUENTIAL and FUSE_WGRAD) or any(not p.requires_grad or grad_sink(p) is None for p in uniq):
+    if not FUSE_WGRAD or any(not p.requires_grad or grad_sink(p) is None for p in uniq):
         return None
     return _SequentialFused.apply(x, subs, *uniq)
 

@@ -31,7 +31,6 @@ hip_sources = [
     "csrc/kernels/embed.hip",
     "csrc/kernels/conv.hip",
     "csrc/optim/lamb.hip",
-    "csrc/blaslt/lt_tuned.cpp",
     "csrc/asm/asm_gemm.cpp",
 ]
 

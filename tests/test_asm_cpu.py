@@ -1,0 +1,37 @@
+"""The assembly kernels build on a GPU-less host: gen_gemm.py emits gfx950 assembly that clang assembles and
+ld.lld links into a code object whose kernel descriptors carry the register / LDS budget the schedule assumes
+(one 256-thread workgroup per CU: 512 VGPR+AGPR, 128 KB LDS); the generator never emits a scalar-memory store."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(LLVM, "clang")), reason="ROCm LLVM not installed")
+def test_asm_gemm_builds(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import gen_gemm
+
+    s = tmp_path / "g.s"
+    gen_gemm.main(str(s))
+    text = s.read_text()
+    assert not re.search(r"\bs_(store|atomic|dcache|buffer_store|scratch_store)", text)
+    o, co = tmp_path / "g.o", tmp_path / "g.hsaco"
+    subprocess.run([os.path.join(LLVM, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                    str(s), "-o", str(o)], check=True)
+    subprocess.run([os.path.join(LLVM, "ld.lld"), "-shared", str(o), "-o", str(co)], check=True)
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)], capture_output=True, text=True,
+                           check=True).stdout
+    for name, _ in gen_gemm.KERNELS:
+        assert f".name:           {name}" in notes
+    assert notes.count(".vgpr_count:     512") == len(gen_gemm.KERNELS)
+    assert notes.count(".group_segment_fixed_size: 131072") == len(gen_gemm.KERNELS)
+    # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads, 2 barriers in the loop body
+    body = text.split("dalle_gemm_nt_plain_kloop:")[1].split("s_cbranch_scc0")[0]
+    assert body.count("v_mfma_f32_16x16x32_bf16") == 128
+    assert body.count(" lds") == 16 and body.count("ds_read_b128") == 32 and body.count("s_barrier") == 2

@@ -115,27 +115,6 @@ def test_weight_grad_splitk(cuda, N, K, arena):
     assert _rel(got, want) < 1e-4
 
 
-@pytest.mark.parametrize("M,N,K,splits", [(64, 256, 256, 1), (640, 512, 256, 5), (2048, 256, 768, 4), (4096, 1024, 512, 16),
-                                          (1024, 768, 1024, 2)])
-def test_gemm_wgrad_mn_major(cuda, M, N, K, splits):
-    """Hand-written MN-major MFMA weight-grad GEMM (ds_read_b64_tr_b16 fragments, split over tokens):
-    store and accumulate forms vs fp32 torch, and split counts must agree closely with each other."""
-    from dalle_amd.ops.hip_ops import C
-
-    torch.manual_seed(1)
-    g = torch.randn(M, N, device=cuda).bfloat16()
-    x = torch.randn(M, K, device=cuda).bfloat16()
-    want = g.float().t() @ x.float()
-    out = torch.full((N, K), 3.0, device=cuda)
-    C().gemm_wgrad_(g, x, out, splits, False)
-    assert _rel(out, want) < 1e-5
-    C().gemm_wgrad_(g, x, out, splits, True)
-    assert _rel(out, 2 * want) < 1e-5
-    one = torch.zeros(N, K, device=cuda)
-    C().gemm_wgrad_(g, x, one, 1, True)
-    assert _rel(one, want) < 1e-5
-
-
 def test_splitk_accum(cuda):
     from dalle_amd.ops.hip_ops import C
 

@@ -228,53 +228,62 @@ def test_layernorm_shift_random_geometry(cuda, T, S, D, shift, seed):
 
 
 @pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
-def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type, monkeypatch):
+def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type):
     """attn_bwd_rope (rotary backward in the attention-backward epilogues) == attn_bwd + rope_bwd."""
+    from dalle_amd.models.patterns import PATTERN_IDS
     from dalle_amd.ops import hip_ops
 
+    C = hip_ops.C()
     torch.manual_seed(3)
     T, S, B, H = 257, 32, 2, 3
     n = T + S * S - 1
     geom = AttnGeometry(T, S, 5)
     qkv = (torch.randn(B, n, 3 * H * 64, device=cuda)).to(torch.bfloat16)
     g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
-    grads = []
-    for fused in (1, 0):
-        monkeypatch.setattr(hip_ops, "FUSED_ROPE_BWD", fused)
-        x = qkv.clone().requires_grad_(True)
-        hip_ops.attention_core(x, H, geom, attn_type).backward(g)
-        grads.append(x.grad.float())
+    x = qkv.clone().requires_grad_(True)
+    hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+    cos, sin = rotary_tables(T, S, 64, device=cuda)
+    col, pat = attn_type == "axial_col", PATTERN_IDS[attn_type]
+    q, k, v = C.rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+    out, lse = C.attn_fwd(q, k, v, B, T, S, n, geom.kernel_size, H, pat)
+    dq, dk, dv = C.attn_bwd(q, k, v, out, g, lse, B, T, S, n, geom.kernel_size, H, pat)
+    grads = [x.grad.float(), C.rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).float().view_as(x.grad)]
     # one bf16 rounding (fused) vs two (separate pass)
     assert _rel(grads[0], grads[1]) < 8e-3, attn_type
 
 
 @pytest.mark.parametrize("S", [16, 32])
 @pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
-def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S, monkeypatch):
-    """Axial patterns: the image keys' dK / dV computed inside the dQ kernel (default) must equal the
-    separate key-centric kernel's (DALLE_AMD_ATTN_FUSE_LOCAL=0), and both the fp32 reference."""
+def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S):
+    """Axial patterns: the image keys' dK / dV computed inside the dQ kernel (the rotary-fused backward the
+    model runs) must equal the separate key-centric kernel's (attn_bwd + rope_bwd), and the fp32 reference."""
+    from dalle_amd.models.patterns import PATTERN_IDS
     from dalle_amd.ops import hip_ops
 
+    C = hip_ops.C()
     torch.manual_seed(5)
     T, B, H = 65, 2, 2
     n = T + S * S - 1
     geom = AttnGeometry(T, S, 5)
     qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
     g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
-    grads = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DALLE_AMD_ATTN_FUSE_LOCAL", flag)
-        x = qkv.clone().requires_grad_(True)
-        hip_ops.attention_core(x, H, geom, attn_type).backward(g)
-        torch.cuda.synchronize()
-        grads.append(x.grad.float())
-    assert torch.isfinite(grads[0]).all()
-    assert _rel(grads[0], grads[1]) < 1e-6, attn_type
-    xr = qkv.float().requires_grad_(True)
+    x = qkv.clone().requires_grad_(True)
+    hip_ops.attention_core(x, H, geom, attn_type).backward(g)
+    fused = x.grad.float()
     cos, sin = rotary_tables(T, S, 64, device=cuda)
+    col = attn_type == "axial_col"
+    pat = PATTERN_IDS[attn_type]
+    q, k, v = C.rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+    out, lse = C.attn_fwd(q, k, v, B, T, S, n, geom.kernel_size, H, pat)
+    dq, dk, dv = C.attn_bwd(q, k, v, out, g, lse, B, T, S, n, geom.kernel_size, H, pat)
+    sep = C.rope_bwd(dq, dk, dv, cos, sin, B, T, S, H, n, col, 0.125).float().view_as(fused)
+    torch.cuda.synchronize()
+    assert torch.isfinite(fused).all()
+    assert _rel(fused, sep) < 1e-6, attn_type
+    xr = qkv.float().requires_grad_(True)
     q, k, v = ref.qkv_rotary(xr, H, cos, sin)
     ref.sparse_attention_core(q, k, v, geom, attn_type).backward(g.float())
-    assert _rel(grads[0], xr.grad) < 3e-2, attn_type
+    assert _rel(fused, xr.grad) < 3e-2, attn_type
 
 
 def test_segmented_uniform8bit_matches_per_part(cuda):
@@ -370,11 +379,11 @@ def test_transpose_cast_bf16_bitwise(cuda, shape):
     assert torch.equal(got, w.bfloat16().t().contiguous())
 
 
-@pytest.mark.parametrize("V", [8192, 32356, 1064, 516, 1000])
-@pytest.mark.parametrize("reg", [1, 0])
-def test_xent_colsum(cuda, V, reg):
-    """Fused CE + in-place dlogits + bias-gradient column sums (both kernel forms: register-resident and
-    LDS accumulator) against fp32 PyTorch; the column sums are of the bf16 dlogits the GEMMs consume."""
+@pytest.mark.parametrize("V", [8192, 32356, 1064, 516, 1000, 40548])
+def test_xent_colsum(cuda, V):
+    """Fused CE + in-place dlogits + bias-gradient column sums (register-resident forms up to 32768 columns,
+    the LDS-accumulator form beyond) against fp32 PyTorch; the column sums are of the bf16 dlogits the GEMMs
+    consume."""
     from dalle_amd.ops import hip_ops
 
     C = hip_ops.C()
@@ -387,22 +396,14 @@ def test_xent_colsum(cuda, V, reg):
     (loss_ref.sum() * 0.25).backward()
     buf = logits.clone()
     db = torch.full((V,), 0.5, device=cuda)
-    try:
-        C.xent_set_reg(reg)
-        loss = C.xent_colsum_(buf, labels, 0.25, db)
-        torch.cuda.synchronize()
-    finally:
-        C.xent_set_reg(1)
+    loss = C.xent_colsum_(buf, labels, 0.25, db)
+    torch.cuda.synchronize()
     assert torch.allclose(loss, loss_ref, atol=2e-3, rtol=1e-3)
     assert _rel(buf, ref_logits.grad) < 1e-2
     assert torch.allclose(db - 0.5, buf.float().sum(0), atol=1e-4, rtol=1e-4)  # += into the sink
     buf2 = logits.clone()
     db2 = torch.full((V,), 0.5, device=cuda)
-    C.xent_set_reg(reg)
-    try:
-        C.xent_colsum_(buf2, labels, 0.25, db2)
-    finally:
-        C.xent_set_reg(1)
+    C.xent_colsum_(buf2, labels, 0.25, db2)
     assert torch.equal(buf2, buf) and torch.equal(db2, db)  # deterministic
 
 
@@ -451,88 +452,3 @@ def test_weight_grad_token_contiguous_input(cuda, M, N, K, fused, form):
     assert _rel(got, got2) < 1e-5
 
 
-@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like"])
-def test_text_dkdv_four_tiles_per_step_bitwise(cuda, attn_type, monkeypatch):
-    """The text dK/dV kernel staging four query tiles per barrier step (attn_set_dkdv_qt(4)) walks each
-    wave's query tiles in the same order as the two-tile form: bitwise-identical gradients. Its default
-    four-wave split of the odd last key block (the text key at position 256 here) only regroups that
-    block's fp32 partial sums: every other gradient stays bitwise, that key's dK / dV agree to rounding."""
-    from dalle_amd.ops import hip_ops
-
-    C = hip_ops.C()
-    torch.manual_seed(9)
-    T, S, B, H = 257, 32, 2, 3
-    n = T + S * S - 1
-    geom = AttnGeometry(T, S, 5)
-    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
-    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
-    grads = []
-    try:
-        for qt, diag in ((2, "0"), (4, "512"), (4, "0")):
-            C.attn_set_dkdv_qt(qt)
-            monkeypatch.setenv("DALLE_AMD_ATTN_DIAG", diag)
-            x = qkv.clone().requires_grad_(True)
-            hip_ops.attention_core(x, H, geom, attn_type).backward(g)
-            torch.cuda.synchronize()
-            grads.append(x.grad.clone())
-    finally:
-        C.attn_set_dkdv_qt(4)
-    assert torch.isfinite(grads[0].float()).all()
-    assert torch.equal(grads[0], grads[1]), attn_type
-    tail = grads[2]
-    same = grads[1].clone()
-    same[:, T - 1, H * 64:] = tail[:, T - 1, H * 64:]
-    assert torch.equal(same, tail), attn_type  # only the odd key block (token 256) regroups its sums
-    a, b = tail[:, T - 1, H * 64:].float(), grads[1][:, T - 1, H * 64:].float()
-    assert torch.allclose(a, b, rtol=2e-2, atol=2e-2 * float(b.abs().max())), attn_type
-
-
-@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
-def test_attention_forward_three_tiles_per_step(cuda, attn_type):
-    """The forward staging three text tiles per barrier step (attn_set_fwd_tps(3)) regroups the online-softmax
-    updates only: same output and log-sum-exp up to fp32 rounding of the rescaled accumulators."""
-    from dalle_amd.ops import hip_ops
-
-    C = hip_ops.C()
-    torch.manual_seed(10)
-    T, S, B, H = 257, 32, 2, 3
-    n = T + S * S - 1
-    geom = AttnGeometry(T, S, 5)
-    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
-    outs = []
-    try:
-        for tps in (2, 3):
-            C.attn_set_fwd_tps(tps)
-            outs.append(hip_ops.attention_core(qkv, H, geom, attn_type).float())
-            torch.cuda.synchronize()
-    finally:
-        C.attn_set_fwd_tps(2)
-    assert torch.isfinite(outs[1]).all()
-    assert _rel(outs[0], outs[1]) < 2e-3, attn_type
-
-
-@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col", "conv_like", "full"])
-def test_dq_dma_staging_bitwise(cuda, attn_type):
-    """The dQ kernel with its text tiles LDS-DMA'd two or three per barrier step (attn_set_dq_stage(2 | 3))
-    accumulates the same tiles in the same order as the register-staged form: bitwise-identical gradients."""
-    from dalle_amd.ops import hip_ops
-
-    C = hip_ops.C()
-    torch.manual_seed(12)
-    T, S, B, H = 257, 32, 2, 3
-    n = T + S * S - 1
-    geom = AttnGeometry(T, S, 5)
-    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
-    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
-    grads = []
-    try:
-        for stage in (0, 2, 3):
-            C.attn_set_dq_stage(stage)
-            x = qkv.clone().requires_grad_(True)
-            hip_ops.attention_core(x, H, geom, attn_type).backward(g)
-            torch.cuda.synchronize()
-            grads.append(x.grad.clone())
-    finally:
-        C.attn_set_dq_stage(0)
-    assert torch.isfinite(grads[0].float()).all()
-    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2]), attn_type

@@ -191,23 +191,32 @@ def test_sequential_fused_stack_matches_per_sublayer(cuda, monkeypatch):
         assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 1e-2
 
 
-def test_wgrad_side_stream_bitwise(cuda, monkeypatch):
-    """Weight grads on a side HIP stream (DALLE_AMD_WGRAD_STREAM=1) give bitwise the same arena grads."""
+def test_asm_gemm_step_matches_hipblaslt(cuda, monkeypatch):
+    """The bench24 geometry (every plain projection tiles) with the plain products on the assembly GEMM vs on
+    hipBLASLt: same loss and arena grads to bf16 rounding, and the assembly path really ran."""
+    from dalle_amd.config import bench24
     from dalle_amd.ops import hip_ops
 
     torch.manual_seed(0)
-    cfg = _cfg(False)
+    cfg = bench24()
     m = DALLE(cfg).to(cuda)
     arena = FlatArena(m.parameters(), device=cuda)
+    m.grad_arena = arena
     text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
     img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
-    grads = []
+    out = {}
     for on in (True, False):
-        monkeypatch.setattr(hip_ops._wgrad, "enabled", on)
+        monkeypatch.setattr(hip_ops, "ASM_GEMM", on)
+        hip_ops.PATH_COUNTS.clear()
         arena.zero_grad()
-        m(text, img, return_loss=True).backward()
-        grads.append(arena.grad.clone())
-    assert torch.equal(grads[0], grads[1])
+        loss = m(text, img, return_loss=True)
+        loss.backward()
+        torch.cuda.synchronize()
+        out[on] = (loss.item(), arena.grad.clone(), hip_ops.PATH_COUNTS.get("asm_gemm", 0))
+    assert out[True][2] > 0 and out[False][2] == 0
+    assert abs(out[True][0] - out[False][0]) <= 2e-3 * abs(out[False][0])
+    rel = ((out[True][1] - out[False][1]).norm() / out[False][1].norm()).item()
+    assert rel < 2e-2, rel
 
 
 def _lamb_setup(cuda, seed=0):
