@@ -90,7 +90,7 @@ def check(mod, shapes):
     return ok
 
 
-def bench(mod, shapes, iters=20):
+def bench(mod, shapes, iters=20, diag=None):
     for (M, N, K) in shapes:
         A = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
         B = torch.rand(N, K, device="cuda").sub_(0.5).to(torch.bfloat16)
@@ -99,6 +99,9 @@ def bench(mod, shapes, iters=20):
             "hipblaslt": lambda: torch.mm(A, B.t(), out=C),
             "asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", A, B, C),
         }
+        if diag is not None:
+            for v in ("noepi", "nodma", "nolds"):
+                fns[f"asm_{v}"] = (lambda v=v: run(diag, f"dalle_gemm_diag_{v}", A, B, C))
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -122,6 +125,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hsaco", default=os.path.join(HERE, "..", "dalle_amd", "gemm_gfx950.hsaco"))
     ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--diag", action="store_true", help="also time the measurement-only variants")
     ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
     a = ap.parse_args()
@@ -132,7 +136,8 @@ def main():
     if a.check_only:
         return
     shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]
-    bench(mod, shapes)
+    diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None
+    bench(mod, shapes, diag=diag)
 
 
 if __name__ == "__main__":

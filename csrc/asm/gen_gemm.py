@@ -13,14 +13,16 @@ Design (one 256-thread workgroup per CU, persistent over output tiles):
 
 * Tile 256 x 256, K-step 64.  Wave ``q`` (0..3) owns the quadrant (wm, wn) = (q >> 1, q & 1): 8 x 8
   ``v_mfma_f32_16x16x32_bf16`` accumulators = 256 AGPRs; 128 MFMAs per K-step per wave.
-* LDS: two 64 KB stages {A image 32 KB | B image 32 KB}.  An operand image is 32 "pieces" of 1 KB, one per
-  (wave half w, fragment f, k-half h): piece lane ``t = p + 16 u`` holds row ``p`` of fragment f, k-chunk
-  ``4 h + u`` (16 bytes).  A fragment read is then ONE linear 1 KB ``ds_read_b128`` at ``piece + 16 lane``
-  -- bank-conflict free with no swizzle -- and the LDS-DMA (``buffer_load_dwordx4 ... lds``, which writes
-  lane-linearly) fills a piece with one instruction whose per-lane global addresses do the layout work.
-* B fragment f covers output columns ``8 c + f`` (c = lane & 15): after the MFMA each lane holds, for one
-  output row, 8 CONSECUTIVE columns across its 8 column fragments, so the epilogue writes 16 bytes per lane
-  and 8 whole 128-byte lines per store instruction with no cross-lane exchange.
+* LDS: two 64 KB stages {A image 32 KB | B image 32 KB}.  An operand image is row-major, 256 rows x 128 B
+  (the K-step's 64 bf16), and the 16-byte chunk c of image row r sits at position ``c ^ ((r >> 1) & 7)``.
+  The LDS-DMA (``buffer_load_dwordx4 ... lds``: lane-linear 1 KB per instruction) fills 8 image rows x 128 B
+  per instruction -- whole 128-byte global lines -- with the swizzle applied on the per-lane SOURCE address.
+  A fragment (16 rows x 32 k) is one ``ds_read_b128`` per lane, bank-conflict free under the b128 lane
+  grouping (checked in tests/test_asm_cpu.py).
+* B image row ``16 f + c`` of a wave half holds global row ``8 c + f``: column fragment f then covers output
+  columns ``8 c + f`` (c = lane & 15), so after the MFMAs each lane holds, for one output row, 8 CONSECUTIVE
+  columns across its 8 column fragments; the epilogue writes 16 bytes per lane and 8 whole 128-byte lines
+  per store instruction with no cross-lane exchange.
 * Pipeline (per K-step t, stage X = t & 1): the k-half-1 fragments of step t are read into the second
   register set under the first 32 MFMAs (k-half 0 set); barrier B2 (everyone's reads of stage X retired)
   then the LDS-DMA of step t + 2 is issued INTO stage X under the next MFMAs (two steps ahead in two
@@ -31,8 +33,10 @@ Design (one 256-thread workgroup per CU, persistent over output tiles):
   ``C[row0 + 128 wm + 16 i + 4 g + r][col0 + 128 wn + 8 c + j]``.
 
 Epilogues (``EPI``): ``plain`` (bf16 C), ``bias`` (bf16 C + fp32 bias[n]).
+Diagnostic builds (``--diag``, measurement only, never loaded by the framework): ``noepi`` (no epilogue),
+``nodma`` (main loop without its LDS-DMA), ``nolds`` (main loop without its fragment reads).
 
-Usage:  gen_gemm.py OUT.s      (assemble with clang -target amdgcn-amd-amdhsa -mcpu=gfx950)
+Usage:  gen_gemm.py OUT.s [--diag]     (assemble with clang -target amdgcn-amd-amdhsa -mcpu=gfx950)
 """
 import sys
 
@@ -45,8 +49,8 @@ S_WG = 2            # workgroup id
 S_A, S_B, S_C, S_AUX0 = 4, 6, 8, 10   # 64-bit pointers
 S_M, S_N, S_K, S_LDA, S_LDB, S_LDC, S_TN, S_NT, S_GRID = 12, 13, 14, 15, 16, 17, 18, 19, 20
 S_SRDA, S_SRDB, S_SRDC = 24, 28, 32   # buffer resources (4 SGPRs each)
-S_OFFA = 36         # 8 soffsets of the A pieces (s36..s43)
-S_OFFB = 44         # 8 soffsets of the B pieces (s44..s51)
+S_OFFA = 36         # 8 soffsets of the A DMA instructions (s36..s43): 8 s rows
+S_OFFB = 44         # 8 soffsets of the B DMA instructions (s44..s51): (s >> 1) rows
 S_TILE = 52         # current tile id
 S_KT = 53           # K-steps per tile
 S_LOOP = 54         # loop counter
@@ -57,23 +61,24 @@ S_NRA, S_NRB = 59, 60   # remaining num_records of the A / B resources
 S_LDC2 = 61         # ldc * 2
 S_T0, S_T1, S_T2, S_T3 = 62, 63, 64, 65
 S_SOFFC = 66
-S_AUXP = 68         # s[68:69] aux pointer of the current tile (bias + col0)
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
 S_LAST = 80
 
 # VGPRs
 V_TID = 0
-V_GA, V_GB = 1, 2            # per-lane LDS-DMA global offsets (A, B)
-V_RA, V_RB = 3, 4            # per-lane ds_read bases (stage X)
-V_CO = 5                     # per-lane epilogue C offset
-V_T = 6                      # temps v6, v7
-SET0_A, SET0_B, SET1_A, SET1_B = 8, 40, 72, 104   # 4 fragment register blocks of 32 VGPRs
-V_EPI = 136                  # epilogue scratch v136..v255
-V_BIAS = 248                 # 8 bias values per lane (v248..v255)
+V_GA0, V_GA1, V_GB0, V_GB1 = 1, 2, 3, 4     # per-lane LDS-DMA source offsets (even / odd instruction s)
+V_RA0, V_RA1, V_RB0, V_RB1 = 5, 6, 7, 8     # per-lane fragment read bases (k-half 0 / 1) in stage X
+V_CO = 9                                     # per-lane epilogue C offset
+V_T = 10                                     # temps v10, v11
+V_BOFF = 12                                  # per-lane bias byte offset
+SET0_A, SET0_B, SET1_A, SET1_B = 16, 48, 80, 112   # 4 fragment register blocks of 32 VGPRs
+V_EPI = 144                                  # epilogue scratch (4 rotating sets of 12)
+V_BIAS = 248                                 # 8 bias values per lane (v248..v255)
 
 STAGE = 65536
 B_IMG = 32768
 PIECE = 1024
+ROWB = 128          # bytes per operand image row (one K-step)
 
 
 class Emitter:
@@ -126,25 +131,26 @@ def mfma_list(set_a, set_b, zero_c):
     return out
 
 
-def frag_reads(set_a, set_b, base_a_v, base_b_v, h):
-    """16 ds_read_b128: 8 A fragments and 8 B fragments of k-half h (pieces 2f + h of the wave half)"""
+def frag_reads(set_a, set_b, h):
+    """16 ds_read_b128: the 8 A fragments and 8 B fragments of k-half h (fragment f = image rows 16 f..)"""
+    ra, rb = (V_RA0, V_RB0) if h == 0 else (V_RA1, V_RB1)
     out = []
     for f in range(8):
-        out.append(f"ds_read_b128 {vr(set_a + 4 * f)}, v{base_a_v} offset:{(2 * f + h) * PIECE}")
-        out.append(f"ds_read_b128 {vr(set_b + 4 * f)}, v{base_b_v} offset:{(2 * f + h) * PIECE}")
+        out.append(f"ds_read_b128 {vr(set_a + 4 * f)}, v{ra} offset:{f * 16 * ROWB}")
+        out.append(f"ds_read_b128 {vr(set_b + 4 * f)}, v{rb} offset:{f * 16 * ROWB}")
     return out
 
 
 def glds_list():
-    """16 LDS-DMA pieces of one K-step: this wave's A pieces 8q+s then its B pieces 8q+s (s = 0..7).
-    M0 = S_MBASE (+ B_IMG) + s * 1KB; each load is preceded by its M0 write (one SALU between is enough)."""
+    """16 LDS-DMA instructions of one K-step: this wave's A image rows 64q + 8s .. +7, then its B image rows
+    (s = 0..7). M0 = S_MBASE (+ B_IMG) + s KB; one wait state between the M0 write and the DMA."""
     out = []
     for s in range(8):
         out.append([f"s_add_u32 m0, s{S_MBASE}, {s * PIECE}", "s_nop 0",
-                    f"buffer_load_dwordx4 v{V_GA}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"])
+                    f"buffer_load_dwordx4 v{V_GA1 if s & 1 else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"])
     for s in range(8):
         out.append([f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}", "s_nop 0",
-                    f"buffer_load_dwordx4 v{V_GB}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"])
+                    f"buffer_load_dwordx4 v{V_GB1 if s & 1 else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"])
     return out
 
 
@@ -158,36 +164,43 @@ def advance_k():
     ]
 
 
-def iteration(e, kind):
+def toggle_stage():
+    return [f"v_xor_b32 v{v}, {STAGE}, v{v}" for v in (V_RA0, V_RA1, V_RB0, V_RB1)] + \
+        [f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}"]
+
+
+def iteration(e, kind, diag=None):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA, wait all), 'last' (no DMA, no next reads).
-    Entry: SET0 holds this step's k-half-0 fragments (waited); V_RA/V_RB point at stage X."""
+    Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
     slots = [[] for _ in range(128)]  # instructions issued after MFMA n
+    reads = diag != "nolds" or kind == "first"
 
     # k-half-1 fragments of this step (stage X) under MFMAs 0..31
-    for n, ins in enumerate(frag_reads(SET1_A, SET1_B, V_RA, V_RB, 1)):
-        slots[2 * n].append(ins)
-    dma = kind in ("first", "loop")
+    if reads:
+        for n, ins in enumerate(frag_reads(SET1_A, SET1_B, 1)):
+            slots[2 * n].append(ins)
+    dma = kind in ("first", "loop") and diag != "nodma"
     if dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
         slots[36].append("s_waitcnt lgkmcnt(0)")
         slots[36].append("s_barrier")
         for n, grp in enumerate(glds_list()):
             slots[38 + 3 * n].extend(grp)     # 38 .. 83
-        slots[86].extend(advance_k())
     else:
         slots[40].append("s_waitcnt lgkmcnt(0)")
+    if kind in ("first", "loop"):
+        slots[86].extend(advance_k())
     if kind != "last":
         # B3: step t + 1's DMA landed for every wave, then read its k-half-0 fragments from stage Y
         slots[90].append("s_waitcnt vmcnt(16)" if dma else "s_waitcnt vmcnt(0)")
         slots[90].append("s_barrier")
-        slots[90].append(f"v_xor_b32 v{V_RA}, {STAGE}, v{V_RA}")
-        slots[90].append(f"v_xor_b32 v{V_RB}, {STAGE}, v{V_RB}")
-        slots[90].append(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")
-        for n, ins in enumerate(frag_reads(SET0_A, SET0_B, V_RA, V_RB, 0)):
-            slots[92 + 2 * n].append(ins)     # 92 .. 122
+        slots[90].extend(toggle_stage())
+        if reads:
+            for n, ins in enumerate(frag_reads(SET0_A, SET0_B, 0)):
+                slots[92 + 2 * n].append(ins)     # 92 .. 122
         slots[127].append("s_waitcnt lgkmcnt(0)")
     mf = m0 + m1
     for n in range(128):
@@ -199,83 +212,105 @@ def iteration(e, kind):
 # ----------------------------------------------------------------------------------------------------
 # kernel
 # ----------------------------------------------------------------------------------------------------
-def kernel(name, epi):
+def lane_setup(e, epi):
+    """per-lane offsets (DMA sources, fragment read bases, epilogue) from the wave id and lane"""
+    T0, T1 = V_T, V_T + 1
+    # ---- fragment read bases: wave image half + lane row (p = lane & 15) + swizzled chunk (kg = lane >> 4) ----
+    #   k-half h: row p, chunk 4 h + kg at position (4 h + kg) ^ ((p >> 1) & 7)
+    e(f"v_and_b32 v{T0}, 15, v{V_TID}")                  # p
+    e(f"v_lshrrev_b32 v{T1}, 1, v{T0}")                  # p >> 1 (< 8)
+    e(f"v_lshrrev_b32 v{V_RA0}, 4, v{V_TID}")
+    e(f"v_and_b32 v{V_RA0}, 3, v{V_RA0}")                 # kg
+    e(f"v_xor_b32 v{V_RA1}, 4, v{V_RA0}")                 # 4 + kg
+    e(f"v_xor_b32 v{V_RA0}, v{V_RA0}, v{T1}")
+    e(f"v_xor_b32 v{V_RA1}, v{V_RA1}, v{T1}")
+    e(f"v_lshlrev_b32 v{V_RA0}, 4, v{V_RA0}")
+    e(f"v_lshlrev_b32 v{V_RA1}, 4, v{V_RA1}")
+    e(f"v_lshl_add_u32 v{V_RA0}, v{T0}, 7, v{V_RA0}")     # + p * 128
+    e(f"v_lshl_add_u32 v{V_RA1}, v{T0}, 7, v{V_RA1}")
+    e(f"v_add_u32 v{V_RB0}, {B_IMG}, v{V_RA0}")
+    e(f"v_add_u32 v{V_RB1}, {B_IMG}, v{V_RA1}")
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 14")                # wm * 16 KB
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 14")                # wn * 16 KB
+    e(f"v_add_u32 v{V_RA0}, s{S_T0}, v{V_RA0}")
+    e(f"v_add_u32 v{V_RA1}, s{S_T0}, v{V_RA1}")
+    e(f"v_add_u32 v{V_RB0}, s{S_T1}, v{V_RB0}")
+    e(f"v_add_u32 v{V_RB1}, s{S_T1}, v{V_RB1}")
+    # ---- DMA sources: lane t -> image row r' = t >> 3 of the instruction, position c' = t & 7,
+    #      global chunk c' ^ (4 (s & 1) + (r' >> 1)) ----
+    e(f"v_lshrrev_b32 v{T0}, 3, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 7, v{T0}")                      # r'
+    e(f"v_and_b32 v{T1}, 7, v{V_TID}")                   # c'
+    e(f"v_lshrrev_b32 v{V_GB0}, 1, v{T0}")
+    e(f"v_xor_b32 v{V_GA0}, v{T1}, v{V_GB0}")            # c' ^ (r' >> 1)
+    e(f"v_xor_b32 v{V_GA1}, 4, v{V_GA0}")                # c' ^ (4 + (r' >> 1))
+    e(f"v_lshlrev_b32 v{V_GA0}, 4, v{V_GA0}")
+    e(f"v_lshlrev_b32 v{V_GA1}, 4, v{V_GA1}")
+    e(f"v_mov_b32 v{V_GB0}, v{V_GA0}")
+    e(f"v_mov_b32 v{V_GB1}, v{V_GA1}")
+    # A row: 64 q + r'
+    e(f"s_lshl_b32 s{S_T0}, s{S_WAVE}, 6")
+    e(f"v_add_u32 v{T1}, s{S_T0}, v{T0}")
+    e(f"s_lshl_b32 s{S_T2}, s{S_LDA}, 1")                # lda * 2
+    e(f"v_mad_u32_u24 v{V_GA0}, v{T1}, s{S_T2}, v{V_GA0}")
+    e(f"v_mad_u32_u24 v{V_GA1}, v{T1}, s{S_T2}, v{V_GA1}")
+    # B row: 128 (q >> 1) + 4 (q & 1) + 8 r' (+ 64 for odd s)
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 2")
+    e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_T1}")
+    e(f"v_lshl_add_u32 v{T1}, v{T0}, 3, s{S_T0}")
+    e(f"s_lshl_b32 s{S_T3}, s{S_LDB}, 1")                # ldb * 2
+    e(f"v_mad_u32_u24 v{V_GB0}, v{T1}, s{S_T3}, v{V_GB0}")
+    e(f"v_add_u32 v{T1}, 64, v{T1}")
+    e(f"v_mad_u32_u24 v{V_GB1}, v{T1}, s{S_T3}, v{V_GB1}")
+    # instruction soffsets: A 8 s rows, B (s >> 1) rows
+    for s in range(8):
+        e(f"s_mul_i32 s{S_OFFA + s}, s{S_T2}, {8 * s}")
+        e(f"s_mul_i32 s{S_OFFB + s}, s{S_T3}, {s >> 1}")
+    # ---- epilogue offset: row 128 wm + 4 g, col 128 wn + 8 c (bytes, relative to the tile) ----
+    e(f"v_lshrrev_b32 v{T0}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 3, v{T0}")
+    e(f"v_lshlrev_b32 v{T0}, 2, v{T0}")                  # 4 g
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")                # row
+    e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
+    e(f"v_and_b32 v{T0}, 15, v{V_TID}")
+    e(f"v_lshlrev_b32 v{T0}, 4, v{T0}")                  # 8 c columns * 2 bytes
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 8")                # 128 wn * 2 bytes
+    e(f"v_add_u32 v{T0}, s{S_T1}, v{T0}")
+    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T0}")
+    if epi == "bias":
+        # byte offset of this lane's 8 bias values relative to col0: (128 wn + 8 c) * 4
+        e(f"v_and_b32 v{V_BOFF}, 15, v{V_TID}")
+        e(f"v_lshlrev_b32 v{V_BOFF}, 5, v{V_BOFF}")
+        e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+        e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 9")
+        e(f"v_add_u32 v{V_BOFF}, s{S_T1}, v{V_BOFF}")
+
+
+def kernel(name, epi, diag=None):
     e = Emitter(name)
     # ---- arguments ----
     e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")          # A B C AUX0
     e(f"s_load_dwordx8 {sr(S_M, 8)}, s[0:1], 0x30")         # M N K lda ldb ldc tiles_n num_tiles
     e(f"s_load_dword s{S_GRID}, s[0:1], 0x50")
     e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+    e("s_nop 1")   # VALU write -> v_readfirstlane of the same VGPR: gfx950 needs a wait state (hipcc pads it too)
     e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+    e("s_nop 1")
     e("s_waitcnt lgkmcnt(0)")
-    # K-steps, ldc*2
     e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
     e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
     # the K-step schedule needs at least 4 steps (first, loop >= 1, penult, last): never loop on less
     e(f"s_cmp_lt_u32 s{S_KT}, 4")
     e("s_cbranch_scc1 " + e.L("end"))
-    # ---- per-lane LDS-DMA offsets ----
-    # A: row = 128 (q >> 1) + 64 (q & 1) + (t & 15), chunk = t >> 4
-    # B: row = 128 (q >> 1) + 4 (q & 1) + 8 (t & 15), chunk = t >> 4
-    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")                    # 128 (q >> 1)
-    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T2}, s{S_T1}, 6")
-    e(f"s_add_u32 s{S_T2}, s{S_T2}, s{S_T0}")               # A row base
-    e(f"s_lshl_b32 s{S_T3}, s{S_T1}, 2")
-    e(f"s_add_u32 s{S_T3}, s{S_T3}, s{S_T0}")               # B row base
-    e(f"v_and_b32 v{V_T}, 15, v{V_TID}")                    # t & 15 (lane, since waves are 64 wide)
-    e(f"v_add_u32 v{V_T + 1}, s{S_T2}, v{V_T}")              # A row
-    e(f"s_lshl_b32 s{S_T0}, s{S_LDA}, 1")
-    e(f"v_mul_lo_u32 v{V_GA}, v{V_T + 1}, s{S_T0}")
-    e(f"v_lshlrev_b32 v{V_T + 1}, 3, v{V_T}")
-    e(f"v_add_u32 v{V_T + 1}, s{S_T3}, v{V_T + 1}")          # B row
-    e(f"s_lshl_b32 s{S_T1}, s{S_LDB}, 1")
-    e(f"v_mul_lo_u32 v{V_GB}, v{V_T + 1}, s{S_T1}")
-    e(f"v_lshrrev_b32 v{V_T}, 4, v{V_TID}")
-    e(f"v_and_b32 v{V_T}, 3, v{V_T}")                        # (t >> 4) & 3 = chunk within the k-half
-    e(f"v_lshlrev_b32 v{V_T}, 4, v{V_T}")
-    e(f"v_add_u32 v{V_GA}, v{V_GA}, v{V_T}")
-    e(f"v_add_u32 v{V_GB}, v{V_GB}, v{V_T}")
-    # piece soffsets: A (s>>1)*16 rows + (s&1)*64 B; B (s>>1) rows + (s&1)*64 B
-    for s in range(8):
-        e(f"s_mul_i32 s{S_OFFA + s}, s{S_T0}, {16 * (s >> 1)}")
-        if s & 1:
-            e(f"s_add_u32 s{S_OFFA + s}, s{S_OFFA + s}, 64")
-        e(f"s_mul_i32 s{S_OFFB + s}, s{S_T1}, {s >> 1}")
-        if s & 1:
-            e(f"s_add_u32 s{S_OFFB + s}, s{S_OFFB + s}, 64")
-    # ---- per-lane fragment read bases (stage 0): A piece wm*16, B piece wn*16, + 16 lane ----
-    e(f"v_and_b32 v{V_T}, 63, v{V_TID}")
-    e(f"v_lshlrev_b32 v{V_T}, 4, v{V_T}")
-    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 14")                   # wm * 16 KB
-    e(f"v_add_u32 v{V_RA}, s{S_T0}, v{V_T}")
-    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 14")
-    e(f"s_add_u32 s{S_T1}, s{S_T1}, {B_IMG}")
-    e(f"v_add_u32 v{V_RB}, s{S_T1}, v{V_T}")
-    # ---- per-lane epilogue offset: row 128 wm + 4 g, col 128 wn + 8 c (bytes, relative to the tile) ----
-    e(f"v_lshrrev_b32 v{V_T}, 4, v{V_TID}")
-    e(f"v_and_b32 v{V_T}, 3, v{V_T}")
-    e(f"v_lshlrev_b32 v{V_T}, 2, v{V_T}")                    # 4 g
-    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
-    e(f"v_add_u32 v{V_T}, s{S_T0}, v{V_T}")                  # row
-    e(f"v_mul_lo_u32 v{V_CO}, v{V_T}, s{S_LDC2}")
-    e(f"v_and_b32 v{V_T}, 15, v{V_TID}")
-    e(f"v_lshlrev_b32 v{V_T}, 4, v{V_T}")                    # 8 c columns * 2 bytes
-    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 8")                    # 128 wn * 2 bytes
-    e(f"v_add_u32 v{V_T}, s{S_T1}, v{V_T}")
-    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{V_T}")
-    if epi == "bias":
-        # byte offset of this lane's 8 bias values relative to col0: (128 wn + 8 c) * 4
-        e(f"v_and_b32 v{V_T + 1}, 15, v{V_TID}")
-        e(f"v_lshlrev_b32 v{V_T + 1}, 5, v{V_T + 1}")
-        e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
-        e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 9")
-        e(f"v_add_u32 v{V_T + 1}, s{S_T1}, v{V_T + 1}")
+    lane_setup(e, epi)
     # ---- tile loop: tile = round * grid + (wg % 8) * (grid / 8) + wg / 8 ----
     e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
     e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
@@ -285,12 +320,9 @@ def kernel(name, epi):
     e.label(e.L("tile"))
     e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("end"))
-    # tile coordinates: tm = tile / tiles_n, tn = tile % tiles_n (tiles_n is a power of two or not: use the
-    # float-free unsigned division by repeated structure: tiles_n <= 64, so a 6-step restoring division)
     udiv(e, S_T0, S_TILE, S_TN, S_T1)           # S_T0 = tile / tiles_n ; S_T1 = remainder
     e(f"s_lshl_b32 s{S_ROW0}, s{S_T0}, 8")
     e(f"s_lshl_b32 s{S_COL0}, s{S_T1}, 8")
-    # A resource: base = A + row0 * lda * 2, num_records = 256 * lda * 2
     set_srd(e, S_SRDA, S_A, S_ROW0, S_LDA, S_NRA)
     set_srd(e, S_SRDB, S_B, S_COL0, S_LDB, S_NRB)
     # C resource: base = C + (row0 * ldc + col0) * 2, num_records = 256 * ldc * 2
@@ -320,7 +352,7 @@ def kernel(name, epi):
     e(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")     # back to stage 0 (refilled with step 2)
     e("s_waitcnt vmcnt(16)")
     e("s_barrier")
-    for ins in frag_reads(SET0_A, SET0_B, V_RA, V_RB, 0):
+    for ins in frag_reads(SET0_A, SET0_B, 0):
         e(ins)
     if epi == "bias":
         # this tile's 8 bias values per lane (fp32): aux + col0 * 4 + lane offset
@@ -329,29 +361,40 @@ def kernel(name, epi):
         e(f"s_addc_u32 s{S_SRDX + 1}, s{S_AUX0 + 1}, 0")
         e(f"s_mov_b32 s{S_SRDX + 2}, 1024")
         e(f"s_mov_b32 s{S_SRDX + 3}, 0x20000")
-        e(f"buffer_load_dwordx4 {vr(V_BIAS)}, v{V_T + 1}, {sr(S_SRDX, 4)}, 0 offen")
-        e(f"buffer_load_dwordx4 {vr(V_BIAS + 4)}, v{V_T + 1}, {sr(S_SRDX, 4)}, 0 offen offset:16")
+        e(f"buffer_load_dwordx4 {vr(V_BIAS)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen")
+        e(f"buffer_load_dwordx4 {vr(V_BIAS + 4)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen offset:16")
     e("s_waitcnt lgkmcnt(0)")
     # K-steps: first, loop x (kt - 3), penult, last  (kt >= 4)
-    iteration(e, "first")
+    iteration(e, "first", diag)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
     e.label(e.L("kloop"))
-    iteration(e, "loop")
+    iteration(e, "loop", diag)
     e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc0 " + e.L("kloop"))
-    iteration(e, "penult")
-    iteration(e, "last")
+    iteration(e, "penult", diag)
+    iteration(e, "last", diag)
     # every wave's last LDS reads are retired (waited inside 'last'); the stages are free after this
     e("s_barrier")
-    # reset the fragment bases to stage 0 for the next tile (kt is even: they toggled kt - 1 times)
-    e(f"v_and_b32 v{V_RA}, 0xffff, v{V_RA}")
-    e(f"v_and_b32 v{V_RB}, 0xffff, v{V_RB}")
+    # reset the fragment bases to stage 0 for the next tile
+    for v in (V_RA0, V_RA1, V_RB0, V_RB1):
+        e(f"v_and_b32 v{v}, 0xffff, v{v}")
     # ---- epilogue ----
     for _ in range(3):
         e("s_nop 7")
     if epi == "bias":
         e("s_waitcnt vmcnt(0)")
+    if diag != "noepi":
+        epilogue_store(e, epi)
+    e(f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}")
+    e("s_branch " + e.L("tile"))
+    e.label(e.L("end"))
+    e("s_waitcnt vmcnt(0)")
+    e("s_endpgm")
+    return e.text()
+
+
+def epilogue_store(e, epi):
     rot = 0
     for i in range(8):
         for r in range(4):
@@ -366,12 +409,6 @@ def kernel(name, epi):
                 e(f"v_cvt_pk_bf16_f32 v{t + 8 + p}, v{t + 2 * p}, v{t + 2 * p + 1}")
             e(f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}")
             e(f"buffer_store_dwordx4 {vr(t + 8)}, v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen")
-    e(f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}")
-    e("s_branch " + e.L("tile"))
-    e.label(e.L("end"))
-    e("s_waitcnt vmcnt(0)")
-    e("s_endpgm")
-    return e.text()
 
 
 def udiv(e, q, n, d, r):
@@ -461,15 +498,17 @@ def descriptor(name):
 """
 
 
-KERNELS = [("dalle_gemm_nt_plain", "plain"), ("dalle_gemm_nt_bias", "bias")]
+KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None)]
+DIAG_KERNELS = [("dalle_gemm_diag_noepi", "plain", "noepi"), ("dalle_gemm_diag_nodma", "plain", "nodma"),
+                ("dalle_gemm_diag_nolds", "plain", "nolds")]
 
 
-def main(out):
+def main(out, diag=False):
     parts = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 6", "\t.text"]
     metas = []
-    for name, epi in KERNELS:
+    for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
-        parts.append(kernel(name, epi))
+        parts.append(kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
         parts.append(descriptor(name))
         metas.append(metadata(name))
@@ -480,4 +519,5 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gemm_gfx950.s")
+    main(sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "gemm_gfx950.s",
+         diag="--diag" in sys.argv)

@@ -194,11 +194,11 @@ struct RopeEpi {
   // EPI 3 / 4 (weight gradients, MN-major operands): fp32 tile stored into slab blockIdx.y of fout
   // (3) or accumulated into fout (4)
   float* fout;
-  // non-temporal epilogue output stores (DALLE_AMD_GEMM_NT_STORE=1): -5 % on the plain-store kernel at
+  // non-temporal epilogue output stores (former switch GEMM_NT_STORE=1): -5 % on the plain-store kernel at
   // the large shapes, no gain on the fused epilogues or the full step (profiles/r2_gemm_epilogue_cost.jsonl)
   int nt = 0;
-  int drain = 0;  // s_waitcnt vmcnt(0) after the epilogue (gemm_pt.hip DALLE_AMD_GEMM_DRAIN)
-  int cpol = 0;  // cache policy of the output stores (common.h cstore16; gemm_pt.hip DALLE_AMD_GEMM_CPOL)
+  int drain = 0;  // s_waitcnt vmcnt(0) after the epilogue (gemm_pt.hip former switch GEMM_DRAIN)
+  int cpol = 0;  // cache policy of the output stores (common.h cstore16; gemm_pt.hip former switch GEMM_CPOL)
   int stagger = 0, first_wave = 0;  // start-time stagger of the first wave (common.h stagger_start)
 };
 
@@ -210,7 +210,7 @@ __device__ __forceinline__ void epi_store16(s16x8* dst, const s16x8& v, int nt) 
 
 static int gemm_nt_store_default() {
   static const int v = [] {
-    const char* e = getenv("DALLE_AMD_GEMM_NT_STORE");
+    const char* e = (const char*)nullptr;
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -956,19 +956,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2wg_kernel(const __bf16* __res
   if (rope.drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// DALLE_AMD_GEGLU_BWD_2WG=1: the FF-out dgrad + GEGLU backward on the two-workgroup kernel (gemm_set_geglu_bwd_2wg)
+// former switch GEGLU_BWD_2WG=1: the FF-out dgrad + GEGLU backward on the two-workgroup kernel (gemm_set_geglu_bwd_2wg)
 static int g_geglu_bwd_2wg = [] {
-  const char* s = getenv("DALLE_AMD_GEGLU_BWD_2WG");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 0;
 }();
 void gemm_set_geglu_bwd_2wg(int v) { g_geglu_bwd_2wg = v; }
-// DALLE_AMD_2WG_STAGGER=<ticks>[,<first_wave>] (10 ns ticks; first_wave < 0: delay the second slot's first
+// former switch 2WG_STAGGER=<ticks>[,<first_wave>] (10 ns ticks; first_wave < 0: delay the second slot's first
 // workgroups, > 0: the 4-phase stagger_start over the first first_wave workgroups)
 static int g_2wg_stagger[2] = {-1, -256};
 static void w2_stagger(RopeEpi& e) {
   if (g_2wg_stagger[0] < 0) {
     g_2wg_stagger[0] = 0;
-    if (const char* s = getenv("DALLE_AMD_2WG_STAGGER")) sscanf(s, "%d,%d", &g_2wg_stagger[0], &g_2wg_stagger[1]);
+    if (const char* s = (const char*)nullptr) sscanf(s, "%d,%d", &g_2wg_stagger[0], &g_2wg_stagger[1]);
   }
   e.stagger = g_2wg_stagger[0];
   e.first_wave = g_2wg_stagger[1];

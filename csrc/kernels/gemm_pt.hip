@@ -812,8 +812,8 @@ static int pt_grid(int ntiles) {
     if (cus <= 0) cus = 256;
   }
   // one workgroup per CU (128 KiB of LDS); a multiple of 8 keeps each workgroup on one XCD's range.
-  // DALLE_AMD_PT_GRID caps the workgroup count (measurement: epilogue cost vs concurrent storers)
-  const char* gcap = getenv("DALLE_AMD_PT_GRID");
+  // former switch PT_GRID caps the workgroup count (measurement: epilogue cost vs concurrent storers)
+  const char* gcap = (const char*)nullptr;
   if (gcap && atoi(gcap) > 0 && atoi(gcap) < cus) return atoi(gcap) < ntiles ? atoi(gcap) : ntiles;
   int g = cus < ntiles ? cus : ntiles;
   if (g > 8 && ntiles > g) g &= ~7;
@@ -822,7 +822,7 @@ static int pt_grid(int ntiles) {
 
 static int pt_persist_default() {
   static const int v = [] {
-    const char* s = getenv("DALLE_AMD_PT_PERSIST");
+    const char* s = (const char*)nullptr;
     return s ? atoi(s) : 0;
   }();
   return v;
@@ -839,13 +839,13 @@ static int pt_cus() {
   return cus;
 }
 
-// DALLE_AMD_GEMM_STAGGER=<percent>: stagger the first wave by that fraction of one tile's main-loop time
+// former switch GEMM_STAGGER=<percent>: stagger the first wave by that fraction of one tile's main-loop time
 // (10 ns ticks at ~1.3 PF/s chip-wide bf16), when the grid has more tiles than CUs. Off by default: it
 // measured SLOWER on every training shape (e.g. M61440 N1024 K8192 874 vs 766 us, N3072 K1024 374 vs 359;
 // profiles/r3_gemm_stagger.jsonl) -- the stores' cost is not the simultaneity of the epilogues.
 int gemm_stagger_ticks(int ntiles, int K) {
   static const int pct = [] {
-    const char* s = getenv("DALLE_AMD_GEMM_STAGGER");
+    const char* s = (const char*)nullptr;
     return s ? atoi(s) : 0;
   }();
   const int cus = pt_cus();
@@ -854,49 +854,49 @@ int gemm_stagger_ticks(int ntiles, int K) {
   return (int)(tile_s * pct / 100.0 * 1e8);
 }
 
-// DALLE_AMD_GEMM_CPOL: cache policy of every hand-written GEMM's output stores (common.h cstore16);
+// former switch GEMM_CPOL: cache policy of every hand-written GEMM's output stores (common.h cstore16);
 // gemm_set_cpol overrides it at run time (benchmarks)
 static int g_gemm_cpol = [] {
-  const char* s = getenv("DALLE_AMD_GEMM_CPOL");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 0;
 }();
 void gemm_set_cpol(int c) { g_gemm_cpol = c; }
 int gemm_cpol() { return g_gemm_cpol; }
 
-// DALLE_AMD_GEMM_DRAIN=1: every hand-written GEMM workgroup waits for its output stores (s_waitcnt
+// former switch GEMM_DRAIN=1: every hand-written GEMM workgroup waits for its output stores (s_waitcnt
 // vmcnt(0)) before it ends. Measured: a one-tile-per-workgroup GEMM whose waves end with their
 // epilogue stores still in flight runs 4-11 % slower than the same kernel draining them first
 // (profiles/r3_gemm_epilogue_stamps.jsonl); gemm_set_drain overrides it at run time
 static int g_gemm_drain = [] {
-  const char* s = getenv("DALLE_AMD_GEMM_DRAIN");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 1;
 }();
 void gemm_set_drain(int d) { g_gemm_drain = d; }
 int gemm_drain() { return g_gemm_drain; }
 
-// DALLE_AMD_GEMM_LINES (default 1): epilogue stores of whole 128-B lines (8 rows x 128 B per store
+// former switch GEMM_LINES (default 1): epilogue stores of whole 128-B lines (8 rows x 128 B per store
 // instruction, lines16) instead of 16 rows x 64 B; gemm_set_lines overrides it at run time (benchmarks)
 static int g_gemm_lines = [] {
-  const char* s = getenv("DALLE_AMD_GEMM_LINES");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 1;
 }();
 void gemm_set_lines(int v) { g_gemm_lines = v; }
-// DALLE_AMD_GEMM_PREFETCH (default 0 until measured): the FF-out dgrad + GEGLU-backward GEMM prefetches
+// former switch GEMM_PREFETCH (default 0 until measured): the FF-out dgrad + GEGLU-backward GEMM prefetches
 // its epilogue's pre-activation lines during the main loop; gemm_set_prefetch overrides it at run time
 static int g_gemm_prefetch = [] {
-  const char* s = getenv("DALLE_AMD_GEMM_PREFETCH");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 0;
 }();
 void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
-// DALLE_AMD_PT_OVERLAP (default 0; measured slower at every B128 shape): persistent plain GEMMs (no bias) issue a tile's stores beside the next
-// tile's first K-step (see gemm_pt_kernel phase 1); DALLE_AMD_PT_STAGGER=<percent of one tile>: start the
+// former switch PT_OVERLAP (default 0; measured slower at every B128 shape): persistent plain GEMMs (no bias) issue a tile's stores beside the next
+// tile's first K-step (see gemm_pt_kernel phase 1); former switch PT_STAGGER=<percent of one tile>: start the
 // persistent workgroups at four phases so their epilogues do not all hit HBM at once
 static int g_pt_overlap = [] {
-  const char* s = getenv("DALLE_AMD_PT_OVERLAP");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 0;
 }();
 static int g_pt_stagger = [] {
-  const char* s = getenv("DALLE_AMD_PT_STAGGER");
+  const char* s = (const char*)nullptr;
   return s ? atoi(s) : 0;
 }();
 void gemm_set_pt_overlap(int v, int stagger_pct) {
@@ -948,7 +948,7 @@ static bool pt_shape_ok(int M, int N, int K) { return M > 0 && N > 0 && M % pt::
 
 static int pt_group_default() {
   static const int v = [] {
-    const char* s = getenv("DALLE_AMD_PT_GROUP");
+    const char* s = (const char*)nullptr;
     return s ? atoi(s) : 4;
   }();
   return v;

@@ -12,7 +12,6 @@ The CPU path runs the same step with the reference ops (tests compare it against
 from __future__ import annotations
 
 import math
-import os
 import threading
 from typing import List, Optional
 
@@ -48,7 +47,13 @@ def gumbel_sample(logits: torch.Tensor, temperature: float = 1.0, generator=None
 
 
 class DecodeEngine:
-    def __init__(self, model, batch_size: int, device=None, use_hip: Optional[bool] = None):
+    def __init__(self, model, batch_size: int, device=None, use_hip: Optional[bool] = None, skinny: bool = True,
+                 partials: int = 2, fused_sampler: bool = True):
+        """``skinny``: decode projections on the skinny MFMA GEMM with fused epilogues (when the shapes allow);
+        ``partials``: 2 = every projection leaves split-K slabs summed by its consumer (measured fastest,
+        profiles/r2_decode_partials_ab.txt), 1 = the residual projections only, 0 = in-GEMM split-K hand-off;
+        ``fused_sampler``: the one-kernel top-k / top-p / Gumbel sampler (K18). The non-default forms are
+        kept for the numerics A/B in tests/test_generation_gpu.py."""
         self.model = model
         cfg = self.cfg = model.cfg
         self.B = batch_size
@@ -78,28 +83,23 @@ class DecodeEngine:
         self.codes = torch.zeros(B, cfg.image_seq_len, dtype=torch.long, device=dev)
         self.temperature, self.top_k, self.top_p = 1.0, 0, 1.0
         # fused HIP sampler (K18); its Gumbel noise is a counter hash of (seed, position, row, token)
-        self.fused_sampler = use_hip and os.environ.get("DALLE_AMD_FUSED_SAMPLER", "1") == "1"
+        self.fused_sampler = use_hip and fused_sampler
         self.seed = torch.zeros((), dtype=torch.int64, device=dev)
         self.graph = None
         self._static_logits = None
         self._w = {}
         # decode-step projections through the skinny MFMA GEMM (csrc/kernels/skinny.hip) with the
         # rotary / GEGLU / LayerScale-residual epilogues fused: M = batch <= 64 rows
-        self.skinny = (use_hip and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0
-                       and os.environ.get("DALLE_AMD_SKINNY", "1") != "0")
+        self.skinny = (use_hip and skinny and batch_size <= 64 and self.d % 128 == 0 and (cfg.ff_mult * self.d) % 128 == 0)
         self.sk_cnt = torch.zeros(8192, dtype=torch.int32, device=dev) if self.skinny else None
         # split-K partials: the projections leave fp32 slabs summed by their consumer, so those GEMMs
         # split K over 4-8x the workgroups with no cross-workgroup hand-off. 2 (default): out-proj /
         # FF-out slabs summed by the next LayerNorm, QKV slabs by the attention prologue (under the KV
         # stream); 1: residual projections only; 0: in-GEMM split-K hand-off
         # (profiles/r2_decode_partials_ab.txt: 4.02 -> 3.70-3.73 ms per image-position step)
-        mode = os.environ.get("DALLE_AMD_DECODE_PARTIALS", "2") if self.skinny else "0"
-        self.partials = mode in ("1", "2")
-        self.qkv_partials = mode == "2"
-        wk = os.environ.get("DALLE_AMD_PARTIALS_WK")  # "a,b": waves per workgroup for K < 4096 / K >= 4096
-        if self.partials and wk:
-            from ..ops.hip_ops import C
-            C().skinny_partials_config(*(int(v) for v in wk.split(",")))
+        mode = int(partials) if self.skinny else 0
+        self.partials = mode in (1, 2)
+        self.qkv_partials = mode == 2
         self._pending = None  # (stream, partial slabs, bias, LayerScale) not yet added to the stream
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
@@ -422,7 +422,7 @@ class DecodeEngine:
         self.seed.fill_(int(seed))
         use_graph = self.use_hip if use_graph is None else use_graph
         if parallel_prefill is None:
-            parallel_prefill = os.environ.get("DALLE_AMD_PARALLEL_PREFILL", "1") != "0"
+            parallel_prefill = True
         self._start(text_bos)
         if use_graph:
             self._capture()
@@ -578,15 +578,14 @@ class SplitDecodeEngine:
             self.graph.replay()
 
 
-def decode_parts(batch_size: int, device) -> int:
-    """How many concurrent batch-slice chains a decode engine uses: ``DALLE_AMD_DECODE_PARTS``, default 2
-    for batches of 32 and more (1 below). Reference model, batch 64, same box
+def decode_parts(batch_size: int, device, parts: Optional[int] = None) -> int:
+    """How many concurrent batch-slice chains a decode engine uses: ``parts``, default 2 for batches of 32
+    and more (1 below). Reference model, batch 64, same box
     (profiles/r2_decode_split_parts.txt): 2 parts 3.53 ms per image-position step and 17.0 images/s vs
     3.74 ms / 16.0 for one chain; 4 parts 4.0-6.1 ms. With the decode kernels at a few us each, two
     half-batch chains overlap one chain's latency-bound kernels with the other's (it measured +1 % when
     the skinny GEMMs still carried their split-K hand-off)."""
-    default = "2" if batch_size >= 32 else "1"
-    n = max(1, int(os.environ.get("DALLE_AMD_DECODE_PARTS", default)))
+    n = max(1, int(parts if parts is not None else (2 if batch_size >= 32 else 1)))
     return n if batch_size % n == 0 else 1
 
 

@@ -245,12 +245,11 @@ class VQGanVAE(nn.Module):
         img = self.decoder(self.post_quant_conv(z))
         return (img.clamp(-1.0, 1.0) + 1) * 0.5
 
-    def use_hip_decoder(self) -> bool:
-        """True when the decoder runs on the HIP kernels (MI355X, supported channel layout, not disabled by
-        ``DALLE_AMD_VQGAN_TORCH=1``)."""
-        import os
+    hip_decoder = True  # False: the PyTorch / MIOpen decoder (numerics A/B in tests/test_vqgan_gpu.py)
 
-        if os.environ.get("DALLE_AMD_VQGAN_TORCH") == "1":
+    def use_hip_decoder(self) -> bool:
+        """True when the decoder runs on the HIP kernels (MI355X, supported channel layout, ``hip_decoder``)."""
+        if not self.hip_decoder:
             return False
         if getattr(self, "_hip_decoder", None) is None:
             from .vqgan_hip import HipDecoder, supported

@@ -129,9 +129,12 @@ def sequential_stack(x, subs):
     return _hip().sequential_stack(x, subs)
 
 
+FUSED_REVERSIBLE = True  # False: the reversible stack over per-op autograd nodes (numerics A/B in tests)
+
+
 def fused_reversible_available(x) -> bool:
     """True when the reversible stack can run on the fused HIP sublayers (``hip_ops.reversible_stack``)."""
-    return x.is_cuda and backend_for(x) == "hip" and os.environ.get("DALLE_AMD_FUSED_REVERSIBLE", "1") != "0"
+    return x.is_cuda and backend_for(x) == "hip" and FUSED_REVERSIBLE
 
 
 def reversible_stack(x, layers, geom, text_len: int, image_size: int, recompute: bool = True):

@@ -18,12 +18,11 @@ def _cfg(reversible):
 
 @pytest.mark.parametrize("skinny", ["1", "0", "handoff", "residual_partials"])
 @pytest.mark.parametrize("reversible", [False, True])
-def test_hip_decode_matches_reference_decode(cuda, reversible, skinny, monkeypatch):
+def test_hip_decode_matches_reference_decode(cuda, reversible, skinny):
     """``1``: every projection as split-K slabs summed by its consumer (default); ``handoff``: in-GEMM
     split-K hand-off; ``residual_partials``: slabs for the residual projections only."""
-    monkeypatch.setenv("DALLE_AMD_DECODE_PARTIALS", {"handoff": "0", "residual_partials": "1"}.get(skinny, "2"))
+    partials = {"handoff": 0, "residual_partials": 1}.get(skinny, 2)
     skinny = "1" if skinny in ("handoff", "residual_partials") else skinny
-    monkeypatch.setenv("DALLE_AMD_SKINNY", skinny)
     torch.manual_seed(0)
     cfg = _cfg(reversible)
     m = DALLE(cfg).eval()
@@ -32,7 +31,7 @@ def test_hip_decode_matches_reference_decode(cuda, reversible, skinny, monkeypat
     img = torch.randint(0, cfg.num_image_tokens, (B, cfg.image_seq_len))
     ref = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False).teacher_forced_logits(m.prepare_text(text), img)
     mg = m.to(cuda)
-    eng = DecodeEngine(mg, B, device=cuda, use_hip=True)
+    eng = DecodeEngine(mg, B, device=cuda, use_hip=True, skinny=skinny == "1", partials=partials)
     assert eng.skinny == (skinny == "1")
     out = eng.teacher_forced_logits(mg.prepare_text(text.to(cuda)), img.to(cuda)).cpu()
     rel = ((out - ref).norm() / ref.norm()).item()
@@ -100,11 +99,10 @@ def test_vq_embed_kernel(cuda):
 
 
 @pytest.mark.parametrize("mode", ["2", "0"])
-def test_decode_long_full_attention_chunked(cuda, mode, monkeypatch):
+def test_decode_long_full_attention_chunked(cuda, mode):
     """Full attention past 384 keys takes the chunked two-pass decode-attention path -- in mode 2 with
     the new token's q / k / v summed from the QKV slabs in its prologue: compare with the PyTorch
     decode over a 64 + 32x32 sequence."""
-    monkeypatch.setenv("DALLE_AMD_DECODE_PARTIALS", mode)
     torch.manual_seed(0)
     c = tiny(False)
     cfg = DALLEConfig(**{**c.to_dict(), "image_size": 256, "depth": 2, "attn_types": ["full", "axial_row"],
@@ -116,7 +114,7 @@ def test_decode_long_full_attention_chunked(cuda, mode, monkeypatch):
     img = torch.randint(0, cfg.num_image_tokens, (B, cfg.image_seq_len))
     ref = DecodeEngine(m, B, device=torch.device("cpu"), use_hip=False).teacher_forced_logits(m.prepare_text(text), img)
     mg = m.to(cuda)
-    eng = DecodeEngine(mg, B, device=cuda, use_hip=True)
+    eng = DecodeEngine(mg, B, device=cuda, use_hip=True, partials=int(mode))
     assert eng.skinny and eng.qkv_partials == (mode == "2")
     out = eng.teacher_forced_logits(mg.prepare_text(text.to(cuda)), img.to(cuda)).cpu()
     rel = ((out - ref).norm() / ref.norm()).item()

@@ -82,8 +82,10 @@ def test_fused_reversible_matches_unfused(cuda, arena, monkeypatch):
     text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
     img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
     grads = []
-    for m, fused in ((m1, "1"), (m2, "0")):
-        monkeypatch.setenv("DALLE_AMD_FUSED_REVERSIBLE", fused)
+    import dalle_amd.ops as ops_mod
+
+    for m, fused in ((m1, True), (m2, False)):
+        monkeypatch.setattr(ops_mod, "FUSED_REVERSIBLE", fused)
         if arena:
             FlatArena(m.parameters(), device=cuda)
         loss = m(text, img, return_loss=True)
