@@ -100,7 +100,7 @@ def bench(mod, shapes, iters=20, diag=None):
             "asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", A, B, C),
         }
         if diag is not None:
-            for v in ("noepi", "nodma", "nolds"):
+            for v in ("noepi", "nodma"):
                 fns[f"asm_{v}"] = (lambda v=v: run(diag, f"dalle_gemm_diag_{v}", A, B, C))
         for f in fns.values():
             f()

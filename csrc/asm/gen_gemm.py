@@ -34,7 +34,7 @@ Design (one 256-thread workgroup per CU, persistent over output tiles):
 
 Epilogues (``EPI``): ``plain`` (bf16 C), ``bias`` (bf16 C + fp32 bias[n]).
 Diagnostic builds (``--diag``, measurement only, never loaded by the framework): ``noepi`` (no epilogue),
-``nodma`` (main loop without its LDS-DMA), ``nolds`` (main loop without its fragment reads).
+``nodma`` (main loop without its LDS-DMA; wrong results by design).
 
 Usage:  gen_gemm.py OUT.s [--diag]     (assemble with clang -target amdgcn-amd-amdhsa -mcpu=gfx950)
 """
@@ -164,43 +164,57 @@ def advance_k():
     ]
 
 
-def toggle_stage():
-    return [f"v_xor_b32 v{v}, {STAGE}, v{v}" for v in (V_RA0, V_RA1, V_RB0, V_RB1)] + \
-        [f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}"]
+def toggle_reads():
+    """the fragment read bases move to the other stage (at B3: the next step's data)"""
+    return [f"v_xor_b32 v{v}, {STAGE}, v{v}" for v in (V_RA0, V_RA1, V_RB0, V_RB1)]
 
 
-def iteration(e, kind, diag=None):
+# slot map of one K-step (instructions issued after MFMA n, n = 0..127), measured on the B128 shapes
+# (profiles/r5_asm_gemm_diag.txt): the LDS-DMA costs issue time roughly per instruction unless spread out
+# (16 DMAs every 3 MFMAs: 1402 TF at K = 8192; packed one per MFMA: 1298; every ~5.6: +8 %), while waiting
+# for it to land costs nothing measurable (no-wait variant: +0.6 %) -- so the DMA is spread over the whole
+# step after B2 and B3 sits in the middle of it.
+B2_SLOT = 36
+B3_SLOT = 90
+DMA_SLOTS = [40 + round(5.6 * n) for n in range(16)]          # 40 .. 124
+ADVANCE_SLOT = 126
+
+
+def iteration(e, kind, diag=None, extra=0):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA, wait all), 'last' (no DMA, no next reads).
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
     slots = [[] for _ in range(128)]  # instructions issued after MFMA n
-    reads = diag != "nolds" or kind == "first"
-
     # k-half-1 fragments of this step (stage X) under MFMAs 0..31
-    if reads:
-        for n, ins in enumerate(frag_reads(SET1_A, SET1_B, 1)):
-            slots[2 * n].append(ins)
+    for n, ins in enumerate(frag_reads(SET1_A, SET1_B, 1)):
+        slots[2 * n].append(ins)
     dma = kind in ("first", "loop") and diag != "nodma"
     if dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
-        slots[36].append("s_waitcnt lgkmcnt(0)")
-        slots[36].append("s_barrier")
+        slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
+        slots[B2_SLOT].append("s_barrier")
         for n, grp in enumerate(glds_list()):
-            slots[38 + 3 * n].extend(grp)     # 38 .. 83
+            slots[DMA_SLOTS[n]].extend(grp)
     else:
-        slots[40].append("s_waitcnt lgkmcnt(0)")
+        slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
     if kind in ("first", "loop"):
-        slots[86].extend(advance_k())
+        # after this step's last DMA: the resources move one K-step and the DMA base to the other stage
+        slots[ADVANCE_SLOT].extend(advance_k() + [f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}"])
     if kind != "last":
-        # B3: step t + 1's DMA landed for every wave, then read its k-half-0 fragments from stage Y
-        slots[90].append("s_waitcnt vmcnt(16)" if dma else "s_waitcnt vmcnt(0)")
-        slots[90].append("s_barrier")
-        slots[90].extend(toggle_stage())
-        if reads:
-            for n, ins in enumerate(frag_reads(SET0_A, SET0_B, 0)):
-                slots[92 + 2 * n].append(ins)     # 92 .. 122
+        # B3: step t + 1's DMA (issued during the previous step) landed for every wave; the DMA of this
+        # step issued so far may stay in flight. Then read step t + 1's k-half-0 fragments from stage Y.
+        younger = (sum(1 for sl in DMA_SLOTS if sl <= B3_SLOT) if dma else 0) + (extra if kind == "first" else 0)
+        assert younger < 64
+        slots[B3_SLOT].append(f"s_waitcnt vmcnt({younger})" if kind != "penult" else "s_waitcnt vmcnt(0)")
+        slots[B3_SLOT].append("s_barrier")
+        slots[B3_SLOT].extend(toggle_reads())
+        busy = set(DMA_SLOTS) if dma else set()
+        free = [n for n in range(B3_SLOT + 2, 124) if n not in busy]
+        pick = [free[round(i * (len(free) - 1) / 15)] for i in range(16)]
+        for n, ins in zip(pick, frag_reads(SET0_A, SET0_B, 0)):
+            slots[n].append(ins)
         slots[127].append("s_waitcnt lgkmcnt(0)")
     mf = m0 + m1
     for n in range(128):
@@ -212,7 +226,7 @@ def iteration(e, kind, diag=None):
 # ----------------------------------------------------------------------------------------------------
 # kernel
 # ----------------------------------------------------------------------------------------------------
-def lane_setup(e, epi):
+def lane_setup(e, epi, diag=None):
     """per-lane offsets (DMA sources, fragment read bases, epilogue) from the wave id and lane"""
     T0, T1 = V_T, V_T + 1
     # ---- fragment read bases: wave image half + lane row (p = lane & 15) + swizzled chunk (kg = lane >> 4) ----
@@ -294,6 +308,61 @@ def lane_setup(e, epi):
         e(f"v_add_u32 v{V_BOFF}, s{S_T1}, v{V_BOFF}")
 
 
+def setup_operands(e):
+    """tile coordinates of S_TILE, the A / B resources at the tile's panels, DMA base at stage 0"""
+    udiv(e, S_T0, S_TILE, S_TN, S_T1)           # S_T0 = tile / tiles_n ; S_T1 = remainder
+    e(f"s_lshl_b32 s{S_ROW0}, s{S_T0}, 8")
+    e(f"s_lshl_b32 s{S_COL0}, s{S_T1}, 8")
+    set_srd(e, S_SRDA, S_A, S_ROW0, S_LDA, S_NRA)
+    set_srd(e, S_SRDB, S_B, S_COL0, S_LDB, S_NRB)
+    e(f"s_lshl_b32 s{S_MBASE}, s{S_WAVE}, 13")  # stage-0 DMA base of this wave's pieces: q * 8 KB
+
+
+def setup_output(e):
+    """C resource of the tile at (S_ROW0, S_COL0): base = C + (row0 * ldc + col0) * 2, 256 rows"""
+    e(f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{S_LDC}")
+    e(f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{S_LDC}")
+    e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}")
+    e(f"s_addc_u32 s{S_T1}, s{S_T1}, 0")
+    e(f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 1")
+    e(f"s_add_u32 s{S_SRDC}, s{S_C}, s{S_T0}")
+    e(f"s_addc_u32 s{S_SRDC + 1}, s{S_C + 1}, s{S_T1}")
+    e(f"s_lshl_b32 s{S_SRDC + 2}, s{S_LDC2}, 8")
+    e(f"s_mov_b32 s{S_SRDC + 3}, 0x20000")
+
+
+def prologue_dma(e):
+    """K-steps 0 and 1 of the tile into stages 0 and 1 (32 DMA instructions per wave)"""
+    for _ in range(2):
+        for grp in glds_list():
+            for ins in grp:
+                e(ins)
+        for ins in advance_k():
+            e(ins)
+        e(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")
+    # S_MBASE is back at stage 0 (refilled with step 2)
+
+
+def body_head(e, epi, older_stores):
+    """step 0's fragments and the tile's epilogue operands, then the first K-step. ``older_stores``: the
+    previous tile's epilogue stores issued after this tile's DMA prologue (they count in vmcnt)."""
+    for ins in frag_reads(SET0_A, SET0_B, 0):
+        e(ins)
+    nb = 0
+    if epi == "bias":
+        # this tile's 8 bias values per lane (fp32): aux + col0 * 4 + lane offset
+        e(f"s_lshl_b32 s{S_T0}, s{S_COL0}, 2")
+        e(f"s_add_u32 s{S_SRDX}, s{S_AUX0}, s{S_T0}")
+        e(f"s_addc_u32 s{S_SRDX + 1}, s{S_AUX0 + 1}, 0")
+        e(f"s_mov_b32 s{S_SRDX + 2}, 1024")
+        e(f"s_mov_b32 s{S_SRDX + 3}, 0x20000")
+        e(f"buffer_load_dwordx4 {vr(V_BIAS)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen")
+        e(f"buffer_load_dwordx4 {vr(V_BIAS + 4)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen offset:16")
+        nb = 2
+    e("s_waitcnt lgkmcnt(0)")
+    return older_stores + nb
+
+
 def kernel(name, epi, diag=None):
     e = Emitter(name)
     # ---- arguments ----
@@ -310,62 +379,30 @@ def kernel(name, epi, diag=None):
     # the K-step schedule needs at least 4 steps (first, loop >= 1, penult, last): never loop on less
     e(f"s_cmp_lt_u32 s{S_KT}, 4")
     e("s_cbranch_scc1 " + e.L("end"))
-    lane_setup(e, epi)
-    # ---- tile loop: tile = round * grid + (wg % 8) * (grid / 8) + wg / 8 ----
+    lane_setup(e, epi, diag)
+    # ---- persistent tiles: tile = round * grid + (wg % 8) * (grid / 8) + wg / 8 ----
     e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
     e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
     e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
     e(f"s_lshr_b32 s{S_T1}, s{S_WG}, 3")
     e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
-    e.label(e.L("tile"))
     e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("end"))
-    udiv(e, S_T0, S_TILE, S_TN, S_T1)           # S_T0 = tile / tiles_n ; S_T1 = remainder
-    e(f"s_lshl_b32 s{S_ROW0}, s{S_T0}, 8")
-    e(f"s_lshl_b32 s{S_COL0}, s{S_T1}, 8")
-    set_srd(e, S_SRDA, S_A, S_ROW0, S_LDA, S_NRA)
-    set_srd(e, S_SRDB, S_B, S_COL0, S_LDB, S_NRB)
-    # C resource: base = C + (row0 * ldc + col0) * 2, num_records = 256 * ldc * 2
-    e(f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{S_LDC}")
-    e(f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{S_LDC}")
-    e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}")
-    e(f"s_addc_u32 s{S_T1}, s{S_T1}, 0")
-    e(f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 1")
-    e(f"s_add_u32 s{S_SRDC}, s{S_C}, s{S_T0}")
-    e(f"s_addc_u32 s{S_SRDC + 1}, s{S_C + 1}, s{S_T1}")
-    e(f"s_lshl_b32 s{S_SRDC + 2}, s{S_LDC2}, 8")
-    e(f"s_mov_b32 s{S_SRDC + 3}, 0x20000")
-    # stage-0 DMA base of this wave's pieces: q * 8 KB
-    e(f"s_lshl_b32 s{S_MBASE}, s{S_WAVE}, 13")
-    # prologue: K-steps 0 and 1 into stages 0 and 1
-    for grp in glds_list():
-        for ins in grp:
-            e(ins)
-    for ins in advance_k():
-        e(ins)
-    e(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")
-    for grp in glds_list():
-        for ins in grp:
-            e(ins)
-    for ins in advance_k():
-        e(ins)
-    e(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")     # back to stage 0 (refilled with step 2)
-    e("s_waitcnt vmcnt(16)")
-    e("s_barrier")
-    for ins in frag_reads(SET0_A, SET0_B, 0):
-        e(ins)
-    if epi == "bias":
-        # this tile's 8 bias values per lane (fp32): aux + col0 * 4 + lane offset
-        e(f"s_lshl_b32 s{S_T0}, s{S_COL0}, 2")
-        e(f"s_add_u32 s{S_SRDX}, s{S_AUX0}, s{S_T0}")
-        e(f"s_addc_u32 s{S_SRDX + 1}, s{S_AUX0 + 1}, 0")
-        e(f"s_mov_b32 s{S_SRDX + 2}, 1024")
-        e(f"s_mov_b32 s{S_SRDX + 3}, 0x20000")
-        e(f"buffer_load_dwordx4 {vr(V_BIAS)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen")
-        e(f"buffer_load_dwordx4 {vr(V_BIAS + 4)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen offset:16")
-    e("s_waitcnt lgkmcnt(0)")
-    # K-steps: first, loop x (kt - 3), penult, last  (kt >= 4)
-    iteration(e, "first", diag)
+    setup_operands(e)
+    setup_output(e)
+    prologue_dma(e)
+    e("s_waitcnt vmcnt(16)")                    # step 0 landed (this wave's part) ...
+    e("s_barrier")                              # ... and every wave's
+    # first tile of the workgroup: nothing older than its DMA prologue
+    extra = body_head(e, epi, 0)
+    iteration(e, "first", diag, extra)
+    e("s_branch " + e.L("steps"))
+    # later tiles: the previous tile's 32 epilogue stores were issued after this tile's DMA prologue
+    e.label(e.L("next"))
+    extra = body_head(e, epi, 32 if diag != "noepi" else 0)
+    iteration(e, "first", diag, extra)
+    e.label(e.L("steps"))
+    # K-steps: first (above), loop x (kt - 3), penult, last  (kt >= 4)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
     e.label(e.L("kloop"))
     iteration(e, "loop", diag)
@@ -376,18 +413,26 @@ def kernel(name, epi, diag=None):
     iteration(e, "last", diag)
     # every wave's last LDS reads are retired (waited inside 'last'); the stages are free after this
     e("s_barrier")
-    # reset the fragment bases to stage 0 for the next tile
-    for v in (V_RA0, V_RA1, V_RB0, V_RB1):
+    for v in (V_RA0, V_RA1, V_RB0, V_RB1):       # fragment bases back at stage 0
         e(f"v_and_b32 v{v}, 0xffff, v{v}")
-    # ---- epilogue ----
-    for _ in range(3):
+    for _ in range(3):                            # MFMA -> v_accvgpr_read wait states
         e("s_nop 7")
-    if epi == "bias":
-        e("s_waitcnt vmcnt(0)")
+    # ---- next tile's DMA prologue goes out BEFORE this tile's epilogue stores: its latency hides under them ----
+    e(f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}")
+    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("final"))
+    setup_operands(e)          # the C resource still addresses the finished tile
+    prologue_dma(e)
     if diag != "noepi":
         epilogue_store(e, epi)
-    e(f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}")
-    e("s_branch " + e.L("tile"))
+    setup_output(e)
+    # step 0 landed: 16 DMA of step 1 and the 32 stores are younger
+    e(f"s_waitcnt vmcnt({16 + (32 if diag != 'noepi' else 0)})")
+    e("s_barrier")
+    e("s_branch " + e.L("next"))
+    e.label(e.L("final"))
+    if diag != "noepi":
+        epilogue_store(e, epi)
     e.label(e.L("end"))
     e("s_waitcnt vmcnt(0)")
     e("s_endpgm")
@@ -499,8 +544,7 @@ def descriptor(name):
 
 
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None)]
-DIAG_KERNELS = [("dalle_gemm_diag_noepi", "plain", "noepi"), ("dalle_gemm_diag_nodma", "plain", "nodma"),
-                ("dalle_gemm_diag_nolds", "plain", "nolds")]
+DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma")]
 
 
 def main(out, diag=False):
