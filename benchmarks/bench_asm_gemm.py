@@ -51,7 +51,7 @@ class Module:
 def gemm_args(A, B, C, aux0=None, grid=256):
     M, K = A.shape
     N = B.shape[0]
-    assert M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and K >= 256
+    assert M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and K >= 256
     assert A.stride(1) == 1 and B.stride(1) == 1 and C.stride(1) == 1
     tiles_n = N // 256
     nt = (M // 256) * tiles_n
@@ -130,7 +130,7 @@ def main():
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
     a = ap.parse_args()
     mod = Module(a.hsaco)
-    ok = check(mod, [(256, 256, 256), (512, 768, 320), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096)])
+    ok = check(mod, [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096)])
     if not ok:
         sys.exit(1)
     if a.check_only:

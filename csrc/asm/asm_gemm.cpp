@@ -71,7 +71,7 @@ int asm_gemm_grid(int num_tiles) {
 
 bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, const void* aux0, const void* aux1,
                  const void* aux2, int M, int N, int K, int lda, int ldb, int ldc, int ld_aux, int flags, hipStream_t st) {
-  if (M <= 0 || N <= 0 || M % 256 || N % 256 || K % 64 || K < 256) return false;
+  if (M <= 0 || N <= 0 || M % 256 || N % 256 || K % 128 || K < 256) return false;
   GemmArgs args;
   std::memset(&args, 0, sizeof(args));
   args.a = A; args.b = B; args.c = C; args.aux0 = aux0; args.aux1 = aux1; args.aux2 = aux2;

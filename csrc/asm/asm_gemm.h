@@ -1,5 +1,5 @@
 // Hand-scheduled assembly GEMMs (csrc/asm/gen_gemm.py): C[M, N] = A[M, K] . B[N, K]^T, bf16 operands,
-// fp32 accumulation. M, N multiples of 256, K a multiple of 64 and >= 256; rows of A / B / C are lda / ldb /
+// fp32 accumulation. M, N multiples of 256, K a multiple of 128 and >= 256; rows of A / B / C are lda / ldb /
 // ldc elements apart. Returns false (launches nothing) for unsupported shapes.
 #pragma once
 #include <hip/hip_runtime.h>

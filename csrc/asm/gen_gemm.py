@@ -61,6 +61,7 @@ S_NRA, S_NRB = 59, 60   # remaining num_records of the A / B resources
 S_LDC2 = 61         # ldc * 2
 S_T0, S_T1, S_T2, S_T3 = 62, 63, 64, 65
 S_SOFFC = 66
+S_TM, S_TNI, S_GDIV, S_GMOD = 67, 68, 69, 70   # tile row / column index, grid / tiles_n, grid % tiles_n
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
 S_LAST = 80
 
@@ -180,9 +181,12 @@ DMA_SLOTS = [40 + round(5.6 * n) for n in range(16)]          # 40 .. 124
 ADVANCE_SLOT = 126
 
 
-def iteration(e, kind, diag=None, extra=0):
+def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=()):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
-    'penult' (no DMA, wait all), 'last' (no DMA, no next reads).
+    'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
+    ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
+    tile's K-step 0 (penult) / 1 (last), so that tile starts with both stages loaded and the DMA issue hides
+    under these steps' MFMAs. ``pre``: scalar instructions spread over MFMAs 1..33 (next-tile setup).
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
@@ -190,7 +194,9 @@ def iteration(e, kind, diag=None, extra=0):
     # k-half-1 fragments of this step (stage X) under MFMAs 0..31
     for n, ins in enumerate(frag_reads(SET1_A, SET1_B, 1)):
         slots[2 * n].append(ins)
-    dma = kind in ("first", "loop") and diag != "nodma"
+    for n, ins in enumerate(pre):
+        slots[1 + n % 33].append(ins)
+    dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
     if dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
         slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
@@ -199,7 +205,7 @@ def iteration(e, kind, diag=None, extra=0):
             slots[DMA_SLOTS[n]].extend(grp)
     else:
         slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
-    if kind in ("first", "loop"):
+    if dma or kind in ("first", "loop"):
         # after this step's last DMA: the resources move one K-step and the DMA base to the other stage
         slots[ADVANCE_SLOT].extend(advance_k() + [f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}"])
     if kind != "last":
@@ -207,7 +213,7 @@ def iteration(e, kind, diag=None, extra=0):
         # step issued so far may stay in flight. Then read step t + 1's k-half-0 fragments from stage Y.
         younger = (sum(1 for sl in DMA_SLOTS if sl <= B3_SLOT) if dma else 0) + (extra if kind == "first" else 0)
         assert younger < 64
-        slots[B3_SLOT].append(f"s_waitcnt vmcnt({younger})" if kind != "penult" else "s_waitcnt vmcnt(0)")
+        slots[B3_SLOT].append(f"s_waitcnt vmcnt({younger})")
         slots[B3_SLOT].append("s_barrier")
         slots[B3_SLOT].extend(toggle_reads())
         busy = set(DMA_SLOTS) if dma else set()
@@ -309,13 +315,29 @@ def lane_setup(e, epi, diag=None):
 
 
 def setup_operands(e):
-    """tile coordinates of S_TILE, the A / B resources at the tile's panels, DMA base at stage 0"""
-    udiv(e, S_T0, S_TILE, S_TN, S_T1)           # S_T0 = tile / tiles_n ; S_T1 = remainder
-    e(f"s_lshl_b32 s{S_ROW0}, s{S_T0}, 8")
-    e(f"s_lshl_b32 s{S_COL0}, s{S_T1}, 8")
+    """row0 / col0 of tile (S_TM, S_TNI), the A / B resources at the tile's panels, DMA base at stage 0"""
+    e(f"s_lshl_b32 s{S_ROW0}, s{S_TM}, 8")
+    e(f"s_lshl_b32 s{S_COL0}, s{S_TNI}, 8")
     set_srd(e, S_SRDA, S_A, S_ROW0, S_LDA, S_NRA)
     set_srd(e, S_SRDB, S_B, S_COL0, S_LDB, S_NRB)
     e(f"s_lshl_b32 s{S_MBASE}, s{S_WAVE}, 13")  # stage-0 DMA base of this wave's pieces: q * 8 KB
+
+
+def next_tile():
+    """tile += grid as (row, column) indices: tni += grid % tiles_n, tm += grid / tiles_n, carry (no branch)"""
+    return [f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}",
+            f"s_add_u32 s{S_TNI}, s{S_TNI}, s{S_GMOD}",
+            f"s_add_u32 s{S_TM}, s{S_TM}, s{S_GDIV}",
+            f"s_cmp_ge_u32 s{S_TNI}, s{S_TN}",
+            f"s_cselect_b32 s{S_T0}, s{S_TN}, 0",
+            f"s_sub_u32 s{S_TNI}, s{S_TNI}, s{S_T0}",
+            f"s_cselect_b32 s{S_T0}, 1, 0",
+            f"s_add_u32 s{S_TM}, s{S_TM}, s{S_T0}"]
+
+
+def emit_all(e, ins):
+    for i in ins:
+        e(i)
 
 
 def setup_output(e):
@@ -376,8 +398,11 @@ def kernel(name, epi, diag=None):
     e("s_waitcnt lgkmcnt(0)")
     e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
     e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
-    # the K-step schedule needs at least 4 steps (first, loop >= 1, penult, last): never loop on less
+    # the K-step schedule needs an even number of at least 4 steps (first, loop >= 1, penult, last; the next
+    # tile's prefetch lands in stage 0 / 1): never run on anything else (the host rejects those shapes too)
     e(f"s_cmp_lt_u32 s{S_KT}, 4")
+    e("s_cbranch_scc1 " + e.L("end"))
+    e(f"s_bitcmp1_b32 s{S_KT}, 0")
     e("s_cbranch_scc1 " + e.L("end"))
     lane_setup(e, epi, diag)
     # ---- persistent tiles: tile = round * grid + (wg % 8) * (grid / 8) + wg / 8 ----
@@ -388,6 +413,8 @@ def kernel(name, epi, diag=None):
     e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
     e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("end"))
+    udiv(e, S_TM, S_TILE, S_TN, S_TNI)
+    udiv(e, S_GDIV, S_GRID, S_TN, S_GMOD)
     setup_operands(e)
     setup_output(e)
     prologue_dma(e)
@@ -409,28 +436,33 @@ def kernel(name, epi, diag=None):
     e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc0 " + e.L("kloop"))
-    iteration(e, "penult", diag)
-    iteration(e, "last", diag)
-    # every wave's last LDS reads are retired (waited inside 'last'); the stages are free after this
-    e("s_barrier")
+    # the last two K-steps: with a successor tile they load its steps 0 and 1 (next_tile + operand setup
+    # ride in penult's first MFMA gaps); the finished tile's C resource stays until its stores are out
+    e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
+    e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("final"))
+    pre = next_tile()
+    sub = Emitter(e.prefix)
+    setup_operands(sub)
+    pre += [l.strip() for l in sub.lines]
+    iteration(e, "penult", diag, prefetch=True, pre=pre)
+    iteration(e, "last", diag, prefetch=True)
     for v in (V_RA0, V_RA1, V_RB0, V_RB1):       # fragment bases back at stage 0
         e(f"v_and_b32 v{v}, 0xffff, v{v}")
     for _ in range(3):                            # MFMA -> v_accvgpr_read wait states
         e("s_nop 7")
-    # ---- next tile's DMA prologue goes out BEFORE this tile's epilogue stores: its latency hides under them ----
-    e(f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}")
-    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
-    e("s_cbranch_scc0 " + e.L("final"))
-    setup_operands(e)          # the C resource still addresses the finished tile
-    prologue_dma(e)
     if diag != "noepi":
         epilogue_store(e, epi)
     setup_output(e)
-    # step 0 landed: 16 DMA of step 1 and the 32 stores are younger
+    # the next tile's step 0 landed: its step 1 (16 DMA) and the 32 stores are younger
     e(f"s_waitcnt vmcnt({16 + (32 if diag != 'noepi' else 0)})")
     e("s_barrier")
     e("s_branch " + e.L("next"))
     e.label(e.L("final"))
+    iteration(e, "penult", diag)
+    iteration(e, "last", diag)
+    for _ in range(3):
+        e("s_nop 7")
     if diag != "noepi":
         epilogue_store(e, epi)
     e.label(e.L("end"))

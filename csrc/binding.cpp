@@ -501,13 +501,13 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
 }
 
 // ---- hand-scheduled assembly GEMMs (csrc/asm/gen_gemm.py): C = A . B^T (+ fp32 bias) ----
-// A (M, K), B (N, K) bf16 (row strides free, K-contiguous); M, N multiples of 256, K of 64, K >= 256
+// A (M, K), B (N, K) bf16 (row strides free, K-contiguous); M, N multiples of 256, K of 128, K >= 256
 Tensor asm_gemm(Tensor A, Tensor B, c10::optional<Tensor> bias, c10::optional<Tensor> out) {
   TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "asm_gemm: bf16 cuda");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "asm_gemm: A (M, K) and B (N, K)");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "asm_gemm: K-contiguous operands");
   const int M = A.size(0), N = B.size(0), K = A.size(1);
-  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 256, "asm_gemm: M, N multiples of 256, K of 64 (>= 256)");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K >= 256, "asm_gemm: M, N multiples of 256, K of 128 (>= 256)");
   TORCH_CHECK((int64_t)M * A.stride(0) * 2 < (1ll << 40) && A.stride(0) < (1 << 20) && B.stride(0) < (1 << 20), "asm_gemm: strides");
   const void* bp = nullptr;
   if (bias.has_value() && bias->defined()) {

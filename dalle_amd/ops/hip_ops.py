@@ -110,7 +110,7 @@ ASM_GEMM = os.environ.get("DALLE_AMD_ASM_GEMM", "0") != "0"
 def _asm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     return (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
             and a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0
-            and a.shape[1] % 64 == 0 and a.shape[1] >= 256 and a.shape[1] == b.shape[1])
+            and a.shape[1] % 128 == 0 and a.shape[1] >= 256 and a.shape[1] == b.shape[1])
 
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
