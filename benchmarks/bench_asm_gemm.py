@@ -90,7 +90,7 @@ def check(mod, shapes):
     return ok
 
 
-def bench(mod, shapes, iters=20, diag=None):
+def bench(mod, shapes, iters=20, diag=None, rounds=5):
     for (M, N, K) in shapes:
         A = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
         B = torch.rand(N, K, device="cuda").sub_(0.5).to(torch.bfloat16)
@@ -100,13 +100,13 @@ def bench(mod, shapes, iters=20, diag=None):
             "asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", A, B, C),
         }
         if diag is not None:
-            for v in ("noepi", "nodma"):
+            for v in ("noepi", "nodma", "nosplit", "nostagger"):
                 fns[f"asm_{v}"] = (lambda v=v: run(diag, f"dalle_gemm_diag_{v}", A, B, C))
         for f in fns.values():
             f()
         torch.cuda.synchronize()
         times = {k: [] for k in fns}
-        for _ in range(5):   # interleaved rounds
+        for _ in range(rounds):   # interleaved rounds
             for k, f in fns.items():
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -126,18 +126,21 @@ def main():
     ap.add_argument("--hsaco", default=os.path.join(HERE, "..", "dalle_amd", "gemm_gfx950.hsaco"))
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--diag", action="store_true", help="also time the measurement-only variants")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
     a = ap.parse_args()
     mod = Module(a.hsaco)
-    ok = check(mod, [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096)])
+    ok = check(mod, [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096),
+                     (25600, 768, 512), (9 * 256, 1024, 512), (17 * 256, 256, 512), (259 * 256, 3 * 256, 512)])
     if not ok:
         sys.exit(1)
     if a.check_only:
         return
     shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]
     diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None
-    bench(mod, shapes, diag=diag)
+    bench(mod, shapes, iters=a.iters, diag=diag, rounds=a.rounds)
 
 
 if __name__ == "__main__":

@@ -61,9 +61,13 @@ S_NRA, S_NRB = 59, 60   # remaining num_records of the A / B resources
 S_LDC2 = 61         # ldc * 2
 S_T0, S_T1, S_T2, S_T3 = 62, 63, 64, 65
 S_SOFFC = 66
-S_TM, S_TNI, S_GDIV, S_GMOD = 67, 68, 69, 70   # tile row / column index, grid / tiles_n, grid % tiles_n
+S_TM, S_TNI = 67, 68  # tile row / column index
+# grouped tile order (8 tile rows per group, column-major inside a group): 8 * tiles_n, its division magic,
+# tiles in full groups, first row of the partial group, its row count and division magic
+S_G8, S_MAGG, S_FULL, S_TMFULL, S_ROWREM, S_MAGR = 69, 70, 71, 76, 77, 78
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
-S_LAST = 80
+S_KV, S_WRAP, S_S0B = 79, 80, 81   # K-slice of the next DMA, 128 - 2 K (the wrap step), first slice * 128
+S_LAST = 84
 
 # VGPRs
 V_TID = 0
@@ -132,37 +136,92 @@ def mfma_list(set_a, set_b, zero_c):
     return out
 
 
+READ_ORDER = [("A", 0)] + [("B", j) for j in range(8)] + [("A", i) for i in range(1, 8)]   # consumption order
+
+
 def frag_reads(set_a, set_b, h):
-    """16 ds_read_b128: the 8 A fragments and 8 B fragments of k-half h (fragment f = image rows 16 f..)"""
+    """16 ds_read_b128: the 8 A fragments and 8 B fragments of k-half h (fragment f = image rows 16 f..), in
+    the order the i-major MFMAs consume them (A0, B0..B7, A1..A7) so that counted lgkmcnt waits release
+    each MFMA as soon as its two operands are in"""
     ra, rb = (V_RA0, V_RB0) if h == 0 else (V_RA1, V_RB1)
     out = []
-    for f in range(8):
-        out.append(f"ds_read_b128 {vr(set_a + 4 * f)}, v{ra} offset:{f * 16 * ROWB}")
-        out.append(f"ds_read_b128 {vr(set_b + 4 * f)}, v{rb} offset:{f * 16 * ROWB}")
+    for op, f in READ_ORDER:
+        if op == "A":
+            out.append(f"ds_read_b128 {vr(set_a + 4 * f)}, v{ra} offset:{f * 16 * ROWB}")
+        else:
+            out.append(f"ds_read_b128 {vr(set_b + 4 * f)}, v{rb} offset:{f * 16 * ROWB}")
     return out
+
+
+def set0_waits(set1_slots):
+    """{n: lgkmcnt} waits placed before MFMA n (n = 1..63) of a step whose k-half-0 fragments were the last 16
+    LDS reads of the previous step (A0 / B0 waited there): MFMA n needs read index max(idx(A[n // 8]),
+    idx(B[n % 8])); the k-half-1 reads issued in this step's slots before it are younger and may stay
+    pending.  lgkmcnt holds 4 bits: counts above 15 are clamped (a stricter wait)."""
+    idx = {k: n for n, k in enumerate(READ_ORDER)}
+    waits, have = {}, idx[("B", 0)]
+    for n in range(1, 64):
+        need = max(idx[("A", n // 8)], idx[("B", n % 8)])
+        if need > have:
+            younger = sum(1 for sl in set1_slots if sl <= n - 1)
+            waits[n] = min(15, 15 - need + younger)
+            have = need
+    return waits
 
 
 def glds_list():
-    """16 LDS-DMA instructions of one K-step: this wave's A image rows 64q + 8s .. +7, then its B image rows
-    (s = 0..7). M0 = S_MBASE (+ B_IMG) + s KB; one wait state between the M0 write and the DMA."""
+    """16 LDS-DMA instructions of one K-step as (M0 write, DMA) pairs: this wave's A image rows 64q + 8s .. +7,
+    then its B image rows (s = 0..7); M0 = S_MBASE (+ B_IMG) + s KB.  The M0 write needs one wait state
+    before its DMA: in a slot schedule it goes one MFMA ahead (the MFMA is the wait state, no s_nop)."""
     out = []
     for s in range(8):
-        out.append([f"s_add_u32 m0, s{S_MBASE}, {s * PIECE}", "s_nop 0",
-                    f"buffer_load_dwordx4 v{V_GA1 if s & 1 else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"])
+        out.append((f"s_add_u32 m0, s{S_MBASE}, {s * PIECE}",
+                    f"buffer_load_dwordx4 v{V_GA1 if s & 1 else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"))
     for s in range(8):
-        out.append([f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}", "s_nop 0",
-                    f"buffer_load_dwordx4 v{V_GB1 if s & 1 else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"])
+        out.append((f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}",
+                    f"buffer_load_dwordx4 v{V_GB1 if s & 1 else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
     return out
 
 
+STAGGER = True      # per-XCD K start (the diagnostic nostagger build turns it off)
+
+
 def advance_k():
-    """move both operand resources one K-step (128 bytes) forward"""
+    """move both operand resources one K-slice (128 bytes) forward; with the staggered start a tile walks its
+    slices s0, s0 + 1, .., kt - 1, 0, .., s0 - 1, so past the last slice the resources step back by 2 K - 128"""
+    if not STAGGER:
+        return [
+            f"s_add_u32 s{S_SRDA}, s{S_SRDA}, 128", f"s_addc_u32 s{S_SRDA + 1}, s{S_SRDA + 1}, 0",
+            f"s_sub_u32 s{S_NRA}, s{S_NRA}, 128", f"s_mov_b32 s{S_SRDA + 2}, s{S_NRA}",
+            f"s_add_u32 s{S_SRDB}, s{S_SRDB}, 128", f"s_addc_u32 s{S_SRDB + 1}, s{S_SRDB + 1}, 0",
+            f"s_sub_u32 s{S_NRB}, s{S_NRB}, 128", f"s_mov_b32 s{S_SRDB + 2}, s{S_NRB}",
+        ]
     return [
-        f"s_add_u32 s{S_SRDA}, s{S_SRDA}, 128", f"s_addc_u32 s{S_SRDA + 1}, s{S_SRDA + 1}, 0",
-        f"s_sub_u32 s{S_NRA}, s{S_NRA}, 128", f"s_mov_b32 s{S_SRDA + 2}, s{S_NRA}",
-        f"s_add_u32 s{S_SRDB}, s{S_SRDB}, 128", f"s_addc_u32 s{S_SRDB + 1}, s{S_SRDB + 1}, 0",
-        f"s_sub_u32 s{S_NRB}, s{S_NRB}, 128", f"s_mov_b32 s{S_SRDB + 2}, s{S_NRB}",
+        f"s_add_u32 s{S_KV}, s{S_KV}, 1",
+        f"s_cmp_eq_u32 s{S_KV}, s{S_KT}",
+        f"s_cselect_b32 s{S_T2}, s{S_WRAP}, 128",       # byte step (low word)
+        f"s_cselect_b32 s{S_T3}, -1, 0",                 # its sign extension
+        f"s_cselect_b32 s{S_KV}, 0, s{S_KV}",
+        f"s_add_u32 s{S_SRDA}, s{S_SRDA}, s{S_T2}", f"s_addc_u32 s{S_SRDA + 1}, s{S_SRDA + 1}, s{S_T3}",
+        f"s_sub_u32 s{S_NRA}, s{S_NRA}, s{S_T2}", f"s_mov_b32 s{S_SRDA + 2}, s{S_NRA}",
+        f"s_add_u32 s{S_SRDB}, s{S_SRDB}, s{S_T2}", f"s_addc_u32 s{S_SRDB + 1}, s{S_SRDB + 1}, s{S_T3}",
+        f"s_sub_u32 s{S_NRB}, s{S_NRB}, s{S_T2}", f"s_mov_b32 s{S_SRDB + 2}, s{S_NRB}",
     ]
+
+
+def stagger_setup(e):
+    """first K-slice of every tile of this workgroup: (XCD) * (kt / 8) -- the 8 XCDs stream different K
+    columns of A / B at any moment (no channel hot spot at long row pitches) while the 32 CUs of one XCD
+    keep walking the same slices (their shared panels stay L2 hits)"""
+    if STAGGER:
+        e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
+        e(f"s_lshr_b32 s{S_T1}, s{S_KT}, 3")
+        e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
+        e(f"s_lshl_b32 s{S_S0B}, s{S_T0}, 7")
+    else:
+        e(f"s_mov_b32 s{S_S0B}, 0")
+    e(f"s_lshl_b32 s{S_T0}, s{S_K}, 1")
+    e(f"s_sub_u32 s{S_WRAP}, 128, s{S_T0}")
 
 
 def toggle_reads():
@@ -179,49 +238,90 @@ B2_SLOT = 36
 B3_SLOT = 90
 DMA_SLOTS = [40 + round(5.6 * n) for n in range(16)]          # 40 .. 124
 ADVANCE_SLOT = 126
+# split release (default): the k-half-1 A fragments are read first and a barrier (BA) frees the stage's A image
+# early, so its 8 DMAs start under MFMA 20 while the B fragments are still being read; a second barrier (BB)
+# frees the B image for the other 8.  16 DMAs over MFMAs 20..124 instead of 40..124.
+SPLIT = True
+SPLIT_SET1_SLOTS = [2 * n for n in range(8)] + [22 + 3 * n for n in range(8)]   # A0..A7, then B0..B7
+BA_SLOT, BB_SLOT = 18, 46
+SPLIT_DMA_SLOTS = [20 + 4 * n for n in range(8)] + [54 + 10 * n for n in range(8)]   # 20 .. 48, 54 .. 124
 
 
-def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=()):
+STORE_SLOTS = [3 + 4 * n for n in range(8)]                   # deferred epilogue stores: before B2
+
+
+def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
     ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
     tile's K-step 0 (penult) / 1 (last), so that tile starts with both stages loaded and the DMA issue hides
-    under these steps' MFMAs. ``pre``: scalar instructions spread over MFMAs 1..33 (next-tile setup).
+    under these steps' MFMAs. ``pre``: scalar instructions spread in order over MFMAs 1..33 (next-tile setup).
+    ``stores``: instruction groups (the previous tile's deferred epilogue stores) issued early in the step,
+    older than this step's DMA; ``extra``: VMEM operations issued after the previous step's DMA and before
+    this step's B3 that B3 need not wait for (the stores here plus whatever the caller issued).
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
     slots = [[] for _ in range(128)]  # instructions issued after MFMA n
-    # k-half-1 fragments of this step (stage X) under MFMAs 0..31
-    for n, ins in enumerate(frag_reads(SET1_A, SET1_B, 1)):
-        slots[2 * n].append(ins)
+    # k-half-1 fragments of this step (stage X) under MFMAs 0..31 (0..43 split: all A first)
+    if SPLIT:
+        set1_slots = SPLIT_SET1_SLOTS
+        reads = frag_reads(SET1_A, SET1_B, 1)
+        reads = [r for r in reads if f", v{V_RA1} " in r] + [r for r in reads if f", v{V_RB1} " in r]
+        assert len(reads) == 16
+        dma_slots = SPLIT_DMA_SLOTS
+    else:
+        set1_slots = [2 * n for n in range(16)]
+        reads = frag_reads(SET1_A, SET1_B, 1)
+        dma_slots = DMA_SLOTS
+    for n, ins in zip(set1_slots, reads):
+        slots[n].append(ins)
+    # the k-half-0 fragments still in flight from the previous step: wait for each as its MFMA comes up
+    for n, cnt in set0_waits(sorted(set1_slots)).items():
+        slots[n - 1].append(f"s_waitcnt lgkmcnt({cnt})")
+    # pre: before the first M0 write (an SALU add: it rewrites SCC, which the pre sequences use)
+    pre_end = BA_SLOT if SPLIT else 34
     for n, ins in enumerate(pre):
-        slots[1 + n % 33].append(ins)
+        slots[1 + n * (pre_end - 1) // len(pre)].append(ins)
+    assert len(stores) <= len(STORE_SLOTS)
+    for n, grp in enumerate(stores):
+        slots[STORE_SLOTS[n]].extend(grp)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
-    if dma:
+    if dma and SPLIT:
+        # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
+        # BB after the B reads: its B image.  Each refilled with step t + 2's piece.
+        slots[BA_SLOT].append("s_waitcnt lgkmcnt(0)")
+        slots[BA_SLOT].append("s_barrier")
+        slots[BB_SLOT].append("s_waitcnt lgkmcnt(0)")
+        slots[BB_SLOT].append("s_barrier")
+    elif dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
         slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
         slots[B2_SLOT].append("s_barrier")
-        for n, grp in enumerate(glds_list()):
-            slots[DMA_SLOTS[n]].extend(grp)
     else:
-        slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
+        slots[max(set1_slots) + 2].append("s_waitcnt lgkmcnt(0)")
+    if dma:
+        for n, (m0w, ins) in enumerate(glds_list()):
+            slots[dma_slots[n] - 1].append(m0w)
+            slots[dma_slots[n]].append(ins)
     if dma or kind in ("first", "loop"):
         # after this step's last DMA: the resources move one K-step and the DMA base to the other stage
         slots[ADVANCE_SLOT].extend(advance_k() + [f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}"])
     if kind != "last":
         # B3: step t + 1's DMA (issued during the previous step) landed for every wave; the DMA of this
         # step issued so far may stay in flight. Then read step t + 1's k-half-0 fragments from stage Y.
-        younger = (sum(1 for sl in DMA_SLOTS if sl <= B3_SLOT) if dma else 0) + (extra if kind == "first" else 0)
+        younger = (sum(1 for sl in dma_slots if sl <= B3_SLOT) if dma else 0) + extra
         assert younger < 64
         slots[B3_SLOT].append(f"s_waitcnt vmcnt({younger})")
         slots[B3_SLOT].append("s_barrier")
         slots[B3_SLOT].extend(toggle_reads())
-        busy = set(DMA_SLOTS) if dma else set()
+        busy = set(dma_slots) if dma else set()
         free = [n for n in range(B3_SLOT + 2, 124) if n not in busy]
         pick = [free[round(i * (len(free) - 1) / 15)] for i in range(16)]
         for n, ins in zip(pick, frag_reads(SET0_A, SET0_B, 0)):
             slots[n].append(ins)
-        slots[127].append("s_waitcnt lgkmcnt(0)")
+        # MFMA 0 of the next step needs A0 / B0 (the first two of these 16 reads)
+        slots[127].append(f"s_waitcnt lgkmcnt({16 - 2})")
     mf = m0 + m1
     for n in range(128):
         e(mf[n])
@@ -320,19 +420,72 @@ def setup_operands(e):
     e(f"s_lshl_b32 s{S_COL0}, s{S_TNI}, 8")
     set_srd(e, S_SRDA, S_A, S_ROW0, S_LDA, S_NRA)
     set_srd(e, S_SRDB, S_B, S_COL0, S_LDB, S_NRB)
+    if STAGGER:
+        for srd, nr in ((S_SRDA, S_NRA), (S_SRDB, S_NRB)):
+            e(f"s_add_u32 s{srd}, s{srd}, s{S_S0B}")
+            e(f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0")
+            e(f"s_sub_u32 s{nr}, s{nr}, s{S_S0B}")
+            e(f"s_mov_b32 s{srd + 2}, s{nr}")
+        e(f"s_lshr_b32 s{S_KV}, s{S_S0B}, 7")
     e(f"s_lshl_b32 s{S_MBASE}, s{S_WAVE}, 13")  # stage-0 DMA base of this wave's pieces: q * 8 KB
 
 
+def tile_coords():
+    """(S_TM, S_TNI) of tile S_TILE in the grouped order: tile rows in groups of 8, column-major inside a
+    group, so the 32 tiles an XCD takes per round (consecutive ids) form an 8 x 4 block -- 8 A panels and 4 B
+    panels in its L2 instead of 1 A panel and 32 B panels (the row-major order at tiles_n = 32).  The partial
+    last group (tile rows % 8 rows) is column-major over its own rows.  Divisions are multiply-high by
+    ceil(2^32 / d) (exact for ids < 2^20, d < 2^12).  Branch-free SALU (spread over MFMA gaps)."""
+    return [f"s_mul_hi_u32 s{S_T0}, s{S_TILE}, s{S_MAGG}",          # group
+            f"s_mul_i32 s{S_T1}, s{S_T0}, s{S_G8}",
+            f"s_sub_u32 s{S_T1}, s{S_TILE}, s{S_T1}",                # id inside the group
+            f"s_and_b32 s{S_T2}, s{S_T1}, 7",
+            f"s_lshl_b32 s{S_T0}, s{S_T0}, 3",
+            f"s_add_u32 s{S_TM}, s{S_T0}, s{S_T2}",
+            f"s_lshr_b32 s{S_TNI}, s{S_T1}, 3",
+            f"s_sub_u32 s{S_T1}, s{S_TILE}, s{S_FULL}",              # id inside the partial group
+            f"s_mul_hi_u32 s{S_T0}, s{S_T1}, s{S_MAGR}",
+            f"s_cmp_eq_u32 s{S_MAGR}, 0",                            # one row: column = id
+            f"s_cselect_b32 s{S_T0}, s{S_T1}, s{S_T0}",
+            f"s_mul_i32 s{S_T2}, s{S_T0}, s{S_ROWREM}",
+            f"s_sub_u32 s{S_T2}, s{S_T1}, s{S_T2}",
+            f"s_add_u32 s{S_T2}, s{S_T2}, s{S_TMFULL}",
+            f"s_cmp_ge_u32 s{S_TILE}, s{S_FULL}",
+            f"s_cselect_b32 s{S_TM}, s{S_T2}, s{S_TM}",
+            f"s_cselect_b32 s{S_TNI}, s{S_T0}, s{S_TNI}"]
+
+
 def next_tile():
-    """tile += grid as (row, column) indices: tni += grid % tiles_n, tm += grid / tiles_n, carry (no branch)"""
-    return [f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}",
-            f"s_add_u32 s{S_TNI}, s{S_TNI}, s{S_GMOD}",
-            f"s_add_u32 s{S_TM}, s{S_TM}, s{S_GDIV}",
-            f"s_cmp_ge_u32 s{S_TNI}, s{S_TN}",
-            f"s_cselect_b32 s{S_T0}, s{S_TN}, 0",
-            f"s_sub_u32 s{S_TNI}, s{S_TNI}, s{S_T0}",
-            f"s_cselect_b32 s{S_T0}, 1, 0",
-            f"s_add_u32 s{S_TM}, s{S_TM}, s{S_T0}"]
+    return [f"s_add_u32 s{S_TILE}, s{S_TILE}, s{S_GRID}"] + tile_coords()
+
+
+def tile_order_setup(e):
+    """the constants of tile_coords (once per kernel)"""
+    e(f"s_lshl_b32 s{S_G8}, s{S_TN}, 3")
+    magic(e, S_MAGG, S_G8)
+    e(f"s_lshr_b32 s{S_T3}, s{S_M}, 8")                    # tile rows
+    e(f"s_and_b32 s{S_ROWREM}, s{S_T3}, 7")
+    e(f"s_andn2_b32 s{S_TMFULL}, s{S_T3}, 7")
+    e(f"s_mul_i32 s{S_FULL}, s{S_TMFULL}, s{S_TN}")
+    magic(e, S_MAGR, S_ROWREM)
+    e(f"s_cmp_lt_u32 s{S_ROWREM}, 2")
+    e(f"s_cselect_b32 s{S_MAGR}, 0, s{S_MAGR}")
+
+
+def magic(e, q, d):
+    """s[q] = ceil(2^32 / s[d]) = floor((2^32 - 1) / s[d]) + 1 for 2 <= s[d] < 2^16 (restoring division)"""
+    e(f"s_mov_b32 s{q}, 0")
+    e(f"s_mov_b32 s{S_T1}, 0")
+    for b in range(31, -1, -1):
+        lab = e.fresh("mag")
+        e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 1")
+        e(f"s_or_b32 s{S_T1}, s{S_T1}, 1")
+        e(f"s_cmp_ge_u32 s{S_T1}, s{d}")
+        e(f"s_cbranch_scc0 {lab}")
+        e(f"s_sub_u32 s{S_T1}, s{S_T1}, s{d}")
+        e(f"s_or_b32 s{q}, s{q}, {hex(1 << b)}")
+        e.label(lab)
+    e(f"s_add_u32 s{q}, s{q}, 1")
 
 
 def emit_all(e, ins):
@@ -356,9 +509,10 @@ def setup_output(e):
 def prologue_dma(e):
     """K-steps 0 and 1 of the tile into stages 0 and 1 (32 DMA instructions per wave)"""
     for _ in range(2):
-        for grp in glds_list():
-            for ins in grp:
-                e(ins)
+        for m0, dma in glds_list():
+            e(m0)
+            e("s_nop 0")
+            e(dma)
         for ins in advance_k():
             e(ins)
         e(f"s_xor_b32 s{S_MBASE}, {STAGE}, s{S_MBASE}")
@@ -386,6 +540,10 @@ def body_head(e, epi, older_stores):
 
 
 def kernel(name, epi, diag=None):
+    global STORE_POLICY, STAGGER, SPLIT
+    STORE_POLICY = "" if diag == "l2store" else " nt"
+    STAGGER = diag != "nostagger"
+    SPLIT = diag != "nosplit"
     e = Emitter(name)
     # ---- arguments ----
     e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")          # A B C AUX0
@@ -413,53 +571,74 @@ def kernel(name, epi, diag=None):
     e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
     e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("end"))
-    udiv(e, S_TM, S_TILE, S_TN, S_TNI)
-    udiv(e, S_GDIV, S_GRID, S_TN, S_GMOD)
+    tile_order_setup(e)
+    stagger_setup(e)
+    emit_all(e, tile_coords())
     setup_operands(e)
-    setup_output(e)
     prologue_dma(e)
     e("s_waitcnt vmcnt(16)")                    # step 0 landed (this wave's part) ...
     e("s_barrier")                              # ... and every wave's
     # first tile of the workgroup: nothing older than its DMA prologue
     extra = body_head(e, epi, 0)
     iteration(e, "first", diag, extra)
-    e("s_branch " + e.L("steps"))
-    # later tiles: the previous tile's 32 epilogue stores were issued after this tile's DMA prologue
-    e.label(e.L("next"))
-    extra = body_head(e, epi, 32 if diag != "noepi" else 0)
-    iteration(e, "first", diag, extra)
-    e.label(e.L("steps"))
-    # K-steps: first (above), loop x (kt - 3), penult, last  (kt >= 4)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    # K-steps: first, loop x (kt - 3), penult, last  (kt >= 4, even)
     e.label(e.L("kloop"))
     iteration(e, "loop", diag)
     e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc0 " + e.L("kloop"))
-    # the last two K-steps: with a successor tile they load its steps 0 and 1 (next_tile + operand setup
-    # ride in penult's first MFMA gaps); the finished tile's C resource stays until its stores are out
+    e.label(e.L("tail"))
+    # the last two K-steps.  The C resource of this tile is set in penult's first MFMA gaps (the previous
+    # tile's deferred stores went out in steps 0..3); with a successor tile, the next_tile / operand setup
+    # follow it there and these two steps DMA the successor's steps 0 and 1
+    out = Emitter(e.prefix)
+    setup_output(out)
+    pre_out = [l.strip() for l in out.lines]
+    sub = Emitter(e.prefix)
+    setup_operands(sub)
+    pre_next = pre_out + next_tile() + [l.strip() for l in sub.lines]
     e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
     e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("final"))
-    pre = next_tile()
-    sub = Emitter(e.prefix)
-    setup_operands(sub)
-    pre += [l.strip() for l in sub.lines]
-    iteration(e, "penult", diag, prefetch=True, pre=pre)
+    e(f"s_cmp_lt_u32 s{S_KT}, {3 + len(DEFER_SPLIT) - 1}")   # steps 0..3 peeled, penult after them
+    e("s_cbranch_scc1 " + e.L("tail_imm"))
+    # ---- successor with deferred stores: 6 stores now, 26 packed into v[144:247] and issued under the
+    #      successor's K-steps 0..3 (the HBM write of a tile overlaps the next tile's MFMAs instead of all CUs
+    #      storing 128 KB at once) ----
+    iteration(e, "penult", diag, prefetch=True, pre=pre_next)
     iteration(e, "last", diag, prefetch=True)
-    for v in (V_RA0, V_RA1, V_RB0, V_RB1):       # fragment bases back at stage 0
-        e(f"v_and_b32 v{v}, 0xffff, v{v}")
-    for _ in range(3):                            # MFMA -> v_accvgpr_read wait states
-        e("s_nop 7")
+    tile_boundary(e)
+    groups = epilogue_stash(e, epi) if diag != "noepi" else []
+    n_imm = N_IMMEDIATE if groups else 0
+    e(f"s_waitcnt vmcnt({16 + n_imm})")         # the successor's step 0 landed (step 1 + the stores younger)
+    e("s_barrier")
+    extra = body_head(e, epi, n_imm)
+    k = 0
+    for n, cnt in enumerate(DEFER_SPLIT):
+        grp = groups[k:k + cnt] if groups else []
+        k += cnt
+        iteration(e, "first" if n == 0 else "loop", diag, (extra if n == 0 else 0) + len(grp), stores=grp)
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, {3 + len(DEFER_SPLIT) - 1}")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc1 " + e.L("tail"))
+    e("s_branch " + e.L("kloop"))
+    # ---- successor, 4 K-steps per tile: all 32 stores at the boundary ----
+    e.label(e.L("tail_imm"))
+    iteration(e, "penult", diag, prefetch=True, pre=pre_next)
+    iteration(e, "last", diag, prefetch=True)
+    tile_boundary(e)
     if diag != "noepi":
         epilogue_store(e, epi)
-    setup_output(e)
-    # the next tile's step 0 landed: its step 1 (16 DMA) and the 32 stores are younger
     e(f"s_waitcnt vmcnt({16 + (32 if diag != 'noepi' else 0)})")
     e("s_barrier")
-    e("s_branch " + e.L("next"))
+    extra = body_head(e, epi, 32 if diag != "noepi" else 0)
+    iteration(e, "first", diag, extra)
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    e("s_branch " + e.L("kloop"))
+    # ---- no successor ----
     e.label(e.L("final"))
-    iteration(e, "penult", diag)
+    iteration(e, "penult", diag, pre=pre_out)
     iteration(e, "last", diag)
     for _ in range(3):
         e("s_nop 7")
@@ -471,35 +650,65 @@ def kernel(name, epi, diag=None):
     return e.text()
 
 
+# deferred epilogue: stores issued at the tile boundary, then per successor K-step 0..3
+N_IMMEDIATE = 6
+DEFER_SPLIT = [7, 7, 6, 6]
+V_STASH = V_EPI                 # 26 packed stores x 4 VGPRs = v[144:247]
+V_ETMP = SET0_A                 # readout temps (the fragment sets are free until the successor's body_head)
+
+
+def tile_boundary(e):
+    for v in (V_RA0, V_RA1, V_RB0, V_RB1):       # fragment bases back at stage 0
+        e(f"v_and_b32 v{v}, 0xffff, v{v}")
+    for _ in range(3):                            # MFMA -> v_accvgpr_read wait states
+        e("s_nop 7")
+
+
+def pack_row(e, epi, i, r, t, dst):
+    """output row (i, r) of this wave: 8 accumulators -> (+ bias) -> 4 packed bf16 pairs in v[dst:dst+3]"""
+    for j in range(8):
+        e(f"v_accvgpr_read_b32 v{t + j}, a{(i * 8 + j) * 4 + r}")
+    if epi == "bias":
+        for j in range(8):
+            e(f"v_add_f32 v{t + j}, v{t + j}, v{V_BIAS + j}")
+    for p in range(4):
+        e(f"v_cvt_pk_bf16_f32 v{dst + p}, v{t + 2 * p}, v{t + 2 * p + 1}")
+
+
+STORE_POLICY = " nt"    # cache-policy modifier of the C stores: streaming (measured +1-2 % on wide N)
+
+
+def store_row(i, r, src):
+    return [f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}",
+            f"buffer_store_dwordx4 {vr(src)}, v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen{STORE_POLICY}"]
+
+
+def epilogue_stash(e, epi):
+    """the first N_IMMEDIATE output rows stored now, the rest packed into V_STASH; returns their store groups"""
+    assert N_IMMEDIATE + sum(DEFER_SPLIT) == 32 and V_STASH + 4 * sum(DEFER_SPLIT) <= V_BIAS
+    groups = []
+    for idx in range(32):
+        i, r = divmod(idx, 4)
+        t = V_ETMP + (idx % 4) * 12
+        if idx < N_IMMEDIATE:
+            pack_row(e, epi, i, r, t, t + 8)
+            for ins in store_row(i, r, t + 8):
+                e(ins)
+        else:
+            dst = V_STASH + 4 * (idx - N_IMMEDIATE)
+            pack_row(e, epi, i, r, t, dst)
+            groups.append(store_row(i, r, dst))
+    return groups
+
+
 def epilogue_store(e, epi):
-    rot = 0
-    for i in range(8):
-        for r in range(4):
-            t = V_EPI + (rot % 4) * 12
-            rot += 1
-            for j in range(8):
-                e(f"v_accvgpr_read_b32 v{t + j}, a{(i * 8 + j) * 4 + r}")
-            if epi == "bias":
-                for j in range(8):
-                    e(f"v_add_f32 v{t + j}, v{t + j}, v{V_BIAS + j}")
-            for p in range(4):
-                e(f"v_cvt_pk_bf16_f32 v{t + 8 + p}, v{t + 2 * p}, v{t + 2 * p + 1}")
-            e(f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}")
-            e(f"buffer_store_dwordx4 {vr(t + 8)}, v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen")
-
-
-def udiv(e, q, n, d, r):
-    """s[q] = s[n] / s[d], s[r] = s[n] % s[d] for s[n] < 2^20, s[d] <= 2^12 (shift-subtract, 20 steps)"""
-    e(f"s_mov_b32 s{q}, 0")
-    e(f"s_mov_b32 s{r}, s{n}")
-    for b in range(19, -1, -1):
-        lab = e.fresh("div")
-        e(f"s_lshl_b32 s{S_T3}, s{d}, {b}")
-        e(f"s_cmp_ge_u32 s{r}, s{S_T3}")
-        e(f"s_cbranch_scc0 {lab}")
-        e(f"s_sub_u32 s{r}, s{r}, s{S_T3}")
-        e(f"s_or_b32 s{q}, s{q}, {1 << b}")
-        e.label(lab)
+    """all 32 output rows of this wave stored at once"""
+    for idx in range(32):
+        i, r = divmod(idx, 4)
+        t = V_EPI + (idx % 4) * 12
+        pack_row(e, epi, i, r, t, t + 8)
+        for ins in store_row(i, r, t + 8):
+            e(ins)
 
 
 def set_srd(e, srd, ptr, row0, ld, nr):
@@ -576,7 +785,7 @@ def descriptor(name):
 
 
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None)]
-DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma")]
+DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")]
 
 
 def main(out, diag=False):

@@ -31,10 +31,12 @@ def test_asm_gemm_builds(tmp_path):
         assert f".name:           {name}" in notes
     assert notes.count(".vgpr_count:     512") == len(gen_gemm.KERNELS)
     assert notes.count(".group_segment_fixed_size: 131072") == len(gen_gemm.KERNELS)
-    # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads, 2 barriers in the loop body
+    # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads, 3 barriers in the loop body
+    # (A image released, B image released, next step landed)
     body = text.split("dalle_gemm_nt_plain_kloop:")[1].split("s_cbranch_scc0")[0]
     assert body.count("v_mfma_f32_16x16x32_bf16") == 128
-    assert body.count(" lds") == 16 and body.count("ds_read_b128") == 32 and body.count("s_barrier") == 2
+    assert body.count(" lds") == 16 and body.count("ds_read_b128") == 32 and body.count("s_barrier") == 3
+    assert "s_nop" not in body   # every wait state of the loop is an MFMA
 
 
 def test_fragment_reads_are_bank_conflict_free():

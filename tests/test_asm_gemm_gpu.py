@@ -1,6 +1,7 @@
 """The hand-scheduled assembly GEMM (csrc/asm/gen_gemm.py, ``_C.asm_gemm``) against an fp32 PyTorch product:
 plain and fp32-bias epilogues, several tile / K-step counts (the K-step schedule's first / loop / penultimate /
-last iterations, persistent workgroups walking several tiles), strided operand rows and an output view."""
+last iterations, persistent workgroups walking several tiles -- with a column-index carry when the grid is
+not a multiple of the tile columns -- with immediate (4 K-steps) and deferred epilogue stores), strided operand rows and an output view."""
 import pytest
 import torch
 
@@ -15,7 +16,8 @@ def C():
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 384), (2560, 1024, 1024), (4096, 3072, 1024),
-                                   (2560, 1024, 4096), (8192, 256, 512), (65536, 1024, 256)])
+                                   (2560, 1024, 4096), (8192, 256, 512), (65536, 1024, 256),
+                                   (25600, 768, 384), (25600, 768, 1024)])
 @pytest.mark.parametrize("bias", [False, True])
 def test_asm_gemm_matches_fp32(cuda, C, M, N, K, bias):
     torch.manual_seed(M + N + K)
