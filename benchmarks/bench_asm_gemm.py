@@ -68,6 +68,70 @@ def run(mod, name, A, B, C, aux0=None, grid=None):
     mod.launch(name, grid, gemm_args(A, B, C, aux0, grid))
 
 
+def tn_args(A, B, part, splits):
+    Ktot, M = A.shape
+    N = B.shape[1]
+    units = (M // 256) * (N // 256) * splits
+    ptrs = [A.data_ptr(), B.data_ptr(), part.data_ptr(), 0, 0, 0]
+    ints = [M, N, Ktot // splits, A.stride(0), B.stride(0), N, N // 256, units, units, 0, 0, 0]
+    return units, struct.pack("<6Q12i", *ptrs, *ints)
+
+
+def run_tn(mod, A, B, part, splits):
+    units, args = tn_args(A, B, part, splits)
+    mod.launch("dalle_gemm_tn_wgrad", units, args)
+
+
+def check_tn(mod, shapes):
+    ok = True
+    for (Ktot, M, N, splits) in shapes:
+        torch.manual_seed(Ktot + M + N)
+        A = torch.randn(Ktot, M, device="cuda").to(torch.bfloat16)
+        B = torch.randn(Ktot, N, device="cuda").to(torch.bfloat16)
+        part = torch.full((splits, M, N), float("nan"), device="cuda")
+        run_tn(mod, A, B, part, splits)
+        torch.cuda.synchronize()
+        ref = A.float().t() @ B.float()
+        got = part.sum(0)
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        nan = torch.isnan(got).sum().item()
+        good = err < 1e-3 and nan == 0
+        ok &= good
+        print(json.dumps({"check": "tn_wgrad", "Ktot": Ktot, "M": M, "N": N, "splits": splits, "max_rel_err": err,
+                          "nan": nan, "ok": good}), flush=True)
+    return ok
+
+
+def bench_tn(mod, shapes, iters=10, rounds=5):
+    for (Ktot, M, N, splits) in shapes:
+        A = torch.rand(Ktot, M, device="cuda").sub_(0.5).to(torch.bfloat16)
+        B = torch.rand(Ktot, N, device="cuda").sub_(0.5).to(torch.bfloat16)
+        part = torch.empty(splits, M, N, device="cuda")
+        out = torch.empty(M, N, device="cuda")
+        fns = {
+            "hipblaslt_tn": lambda: torch.mm(A.t(), B, out_dtype=torch.float32, out=out),
+            "asm_tn": lambda: run_tn(mod, A, B, part, splits),
+            "asm_tn+fold": lambda: (run_tn(mod, A, B, part, splits), torch.sum(part, 0, out=out)),
+        }
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        times = {k: [] for k in fns}
+        for _ in range(rounds):
+            for k, f in fns.items():
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(iters):
+                    f()
+                e.record()
+                e.synchronize()
+                times[k].append(s.elapsed_time(e) * 1000 / iters)
+        flop = 2.0 * M * N * Ktot
+        us = {k: round(sorted(v)[len(v) // 2], 1) for k, v in times.items()}
+        print(json.dumps({"shape": f"TN_K{Ktot}_M{M}_N{N}_s{splits}", "us": us,
+                          "TF": {k: round(flop / v / 1e6) for k, v in us.items()}}), flush=True)
+
+
 def check(mod, shapes):
     ok = True
     for (M, N, K) in shapes:
@@ -127,6 +191,7 @@ def main():
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--diag", action="store_true", help="also time the measurement-only variants")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tn", action="store_true", help="also time the weight-gradient (TN) kernel")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
@@ -134,10 +199,15 @@ def main():
     mod = Module(a.hsaco)
     ok = check(mod, [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (2560, 3072, 1024), (4096, 1024, 4096),
                      (25600, 768, 512), (9 * 256, 1024, 512), (17 * 256, 256, 512), (259 * 256, 3 * 256, 512)])
+    ok &= check_tn(mod, [(2048, 256, 256, 1), (4096, 512, 768, 2), (8192, 1024, 1024, 4), (16384, 3072, 1024, 16),
+                         (3 * 8192, 768, 512, 3)])
     if not ok:
         sys.exit(1)
     if a.check_only:
         return
+    if a.tn:
+        bench_tn(mod, [(163840, 1024, 1024, 16), (163840, 3072, 1024, 16), (163840, 8192, 1024, 2),
+                       (163840, 1024, 4096, 4)], rounds=a.rounds)
     shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]
     diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None
     bench(mod, shapes, iters=a.iters, diag=diag, rounds=a.rounds)

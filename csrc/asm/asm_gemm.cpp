@@ -86,4 +86,21 @@ bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, cons
   return hipModuleLaunchKernel(f, args.grid, 1, 1, 256, 1, 1, 0, st, nullptr, extra) == hipSuccess;
 }
 
+bool asm_gemm_tn(const void* A, const void* B, void* part, int M, int N, int Ktot, int lda, int ldb, int splits, hipStream_t st) {
+  if (M <= 0 || N <= 0 || M % 256 || N % 256 || splits <= 0 || Ktot % splits) return false;
+  const int Kc = Ktot / splits;
+  if (Kc % 128 || Kc < 256 || lda < M || ldb < N || lda >= (1 << 23) || ldb >= (1 << 23)) return false;
+  GemmArgs args;
+  std::memset(&args, 0, sizeof(args));
+  args.a = A; args.b = B; args.c = part;
+  args.m = M; args.n = N; args.k = Kc; args.lda = lda; args.ldb = ldb; args.ldc = N;
+  args.tiles_n = N / 256;
+  args.num_tiles = (M / 256) * (N / 256) * splits;  // work units (tile, split)
+  args.grid = args.num_tiles;                       // one unit per workgroup
+  size_t size = sizeof(args);
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  hipFunction_t f = get_function("dalle_gemm_tn_wgrad");
+  return hipModuleLaunchKernel(f, args.grid, 1, 1, 256, 1, 1, 0, st, nullptr, extra) == hipSuccess;
+}
+
 }  // namespace dalle

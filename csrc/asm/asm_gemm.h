@@ -9,5 +9,9 @@ namespace dalle {
 bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, const void* aux0, const void* aux1,
                  const void* aux2, int M, int N, int K, int lda, int ldb, int ldc, int ld_aux, int flags, hipStream_t st);
 int asm_gemm_grid(int num_tiles);
+// Weight-gradient form: part[s] (M x N fp32) = A[s Kc : (s + 1) Kc, :]^T . B[s Kc : (s + 1) Kc, :] for s < splits,
+// Kc = Ktot / splits; A (Ktot x M) and B (Ktot x N) bf16 token-major with row pitches lda / ldb. M, N multiples
+// of 256, Kc a multiple of 128 and >= 256. Returns false (launches nothing) for unsupported shapes.
+bool asm_gemm_tn(const void* A, const void* B, void* part, int M, int N, int Ktot, int lda, int ldb, int splits, hipStream_t st);
 
 }  // namespace dalle

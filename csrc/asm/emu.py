@@ -1,0 +1,444 @@
+#!/usr/bin/env python3
+"""Functional emulator of the generated gfx950 GEMM kernels (csrc/asm/gen_gemm.py) on the CPU.
+
+Runs one workgroup (4 waves) instruction by instruction -- SALU, the VALU subset the generator emits,
+LDS reads (ds_read_b128, ds_read_b64_tr_b16), LDS-DMA buffer loads, buffer stores, v_mfma_f32_16x16x32_bf16 --
+against numpy "global memory" whose every access is bounds-checked against the tensors that were passed
+in: a kernel that would fault on the GPU raises here with the instruction and the address instead.  Waves run
+in turn between barriers (a barrier is a rendezvous of all 4); memory operations complete at issue, so
+s_waitcnt is a no-op (the emulator checks addressing and data layout, not the timing of the schedule).
+
+    python csrc/asm/emu.py            # self-test: the NT and TN kernels on small shapes vs numpy
+"""
+import os
+import re
+import struct
+import sys
+
+import numpy as np
+
+M32 = 0xFFFFFFFF
+
+
+def bf16_to_f32(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def f32_to_bf16(f):
+    u = np.asarray(f, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r
+
+
+class Memory:
+    """global memory: named byte buffers at fake base addresses; every access is range-checked"""
+
+    def __init__(self):
+        self.bufs = []   # (base, bytearray-like np.uint8 array, name)
+        self.next = 0x1000_0000
+
+    def alloc(self, arr, name):
+        b = np.frombuffer(np.ascontiguousarray(arr).tobytes(), dtype=np.uint8).copy()
+        base = self.next
+        self.next += (len(b) + 0xFFFFF) & ~0xFFFFF
+        self.next += 0x100000
+        self.bufs.append((base, b, name))
+        return base
+
+    def find(self, addr, n):
+        for base, b, name in self.bufs:
+            if base <= addr and addr + n <= base + len(b):
+                return b, addr - base
+        raise RuntimeError(f"out-of-bounds global access at {addr:#x} (+{n})")
+
+    def read(self, addr, n):
+        b, o = self.find(addr, n)
+        return b[o:o + n]
+
+    def write(self, addr, data):
+        b, o = self.find(addr, len(data))
+        b[o:o + len(data)] = data
+
+    def get(self, base, dtype, shape):
+        for bb, b, name in self.bufs:
+            if bb == base:
+                return b.view(dtype).reshape(shape)
+        raise KeyError(base)
+
+
+def parse_kernel(asm_text, name):
+    lines = asm_text.split("\n")
+    start = lines.index(f"{name}:") + 1
+    code, labels = [], {}
+    for l in lines[start:]:
+        if l.startswith("\t.size"):
+            break
+        s = l.strip()
+        if not s or s.startswith(";"):
+            continue
+        if s.endswith(":"):
+            labels[s[:-1]] = len(code)
+            continue
+        code.append(s)
+    return code, labels
+
+
+def reg_range(tok):
+    """'v[16:19]' -> (16, 4); 'v5' -> (5, 1); 's[24:27]' -> (24, 4); 'a[0:3]' -> (0, 4)"""
+    m = re.match(r"^[vsa]\[(\d+):(\d+)\]$", tok)
+    if m:
+        return int(m.group(1)), int(m.group(2)) - int(m.group(1)) + 1
+    return int(tok[1:]), 1
+
+
+class Wave:
+    def __init__(self, wid):
+        self.v = np.zeros((256, 64), dtype=np.uint32)
+        self.a = np.zeros((256, 64), dtype=np.float32)
+        self.s = np.zeros(108, dtype=np.uint64)
+        self.m0 = 0
+        self.scc = 0
+        self.pc = 0
+        self.done = False
+        self.v[0] = np.arange(64) + 64 * wid
+
+
+class Workgroup:
+    def __init__(self, code, labels, mem, kernarg, wg_id, lds_bytes=160 * 1024):
+        self.code, self.labels, self.mem = code, labels, mem
+        self.lds = np.zeros(lds_bytes, dtype=np.uint8)
+        self.lds_alloc = 131072
+        self.waves = [Wave(w) for w in range(4)]
+        ka = mem.alloc(np.frombuffer(kernarg, dtype=np.uint8), "kernarg")
+        for w in self.waves:
+            w.s[0] = ka & M32
+            w.s[1] = ka >> 32
+            w.s[2] = wg_id
+
+    # ---- operand helpers ----
+    def sval(self, w, tok):
+        tok = tok.strip()
+        if tok == "m0":
+            return w.m0
+        if tok.startswith("s") and tok[1:].isdigit():
+            return int(w.s[int(tok[1:])]) & M32
+        if tok.startswith("0x"):
+            return int(tok, 16) & M32
+        return int(tok) & M32
+
+    def vval(self, w, tok):
+        """per-lane uint32 operand: VGPR, SGPR (broadcast) or constant"""
+        tok = tok.strip()
+        if tok.startswith("v") and tok[1:].isdigit():
+            return w.v[int(tok[1:])].astype(np.uint64)
+        return np.full(64, self.sval(w, tok), dtype=np.uint64)
+
+    def run_wave(self, w):
+        """run until a barrier or the end; returns 'barrier' or 'end'"""
+        code = self.code
+        while True:
+            if w.pc >= len(code):
+                w.done = True
+                return "end"
+            ins = code[w.pc]
+            w.pc += 1
+            r = self.step(w, ins)
+            if r:
+                return r
+
+    def run(self, max_rounds=10 ** 7):
+        for _ in range(max_rounds):
+            states = [self.run_wave(w) if not w.done else "end" for w in self.waves]
+            if all(s == "end" for s in states):
+                return
+            if any(s == "end" for s in states) and any(s == "barrier" for s in states):
+                raise RuntimeError("barrier mismatch: some waves ended while others wait")
+        raise RuntimeError("too many barrier rounds")
+
+    def step(self, w, ins):
+        op, _, rest = ins.partition(" ")
+        # split args but keep modifiers (offen, lds, offset:N, nt) separately
+        toks = [t.strip() for t in rest.split(",")] if rest else []
+        mods = []
+        if toks:
+            last = toks[-1].split()
+            toks[-1] = last[0]
+            mods = last[1:]
+        d = lambda i=0: int(toks[i][1:])
+        S = w.s
+        if op == "s_endpgm":
+            w.done = True
+            return "end"
+        if op == "s_barrier":
+            return "barrier"
+        if op in ("s_nop", "s_waitcnt"):
+            return None
+        if op == "s_load_dwordx8" or op == "s_load_dword":
+            base, n = reg_range(toks[0])
+            addr = (int(S[int(toks[1][2:].split(":")[0])]) | (int(S[int(toks[1][2:].split(":")[0]) + 1]) << 32)) + int(toks[2], 16)
+            data = self.mem.read(addr, 4 * n).view(np.uint32)
+            for i in range(n):
+                S[base + i] = int(data[i])
+            return None
+        if op.startswith("s_"):
+            return self.salu(w, op, toks)
+        if op.startswith("v_mfma"):
+            return self.mfma(w, toks)
+        if op.startswith("v_"):
+            return self.valu(w, op, toks)
+        if op.startswith("ds_read"):
+            return self.ds_read(w, op, toks, mods)
+        if op.startswith("buffer_"):
+            return self.buffer(w, op, toks, mods)
+        raise RuntimeError("unsupported: " + ins)
+
+    def salu(self, w, op, t):
+        S = w.s
+        val = lambda x: self.sval(w, x)
+
+        def setd(v):
+            if t[0] == "m0":
+                w.m0 = v & M32
+            else:
+                S[int(t[0][1:])] = v & M32
+        if op == "s_mov_b32":
+            setd(val(t[1]))
+        elif op == "s_add_u32":
+            r = val(t[1]) + val(t[2]); w.scc = r >> 32; setd(r)
+        elif op == "s_addc_u32":
+            r = val(t[1]) + val(t[2]) + w.scc; w.scc = r >> 32; setd(r)
+        elif op == "s_sub_u32":
+            r = val(t[1]) - val(t[2]); w.scc = 1 if r < 0 else 0; setd(r)
+        elif op == "s_mul_i32":
+            setd(val(t[1]) * val(t[2]))
+        elif op == "s_mul_hi_u32":
+            setd((val(t[1]) * val(t[2])) >> 32)
+        elif op in ("s_lshl_b32", "s_lshr_b32", "s_and_b32", "s_or_b32", "s_xor_b32", "s_andn2_b32"):
+            a, b = val(t[1]), val(t[2])
+            r = {"s_lshl_b32": (a << (b & 31)) & M32, "s_lshr_b32": a >> (b & 31), "s_and_b32": a & b,
+                 "s_or_b32": a | b, "s_xor_b32": a ^ b, "s_andn2_b32": a & ~b & M32}[op]
+            setd(r); w.scc = int(r != 0)
+        elif op == "s_lshl_b64":
+            lo = reg_range(t[0])[0]
+            src = reg_range(t[1])[0]
+            v = int(S[src]) | (int(S[src + 1]) << 32)
+            v = (v << val(t[2])) & ((1 << 64) - 1)
+            S[lo], S[lo + 1] = v & M32, v >> 32
+            w.scc = int(v != 0)
+        elif op == "s_cselect_b32":
+            setd(val(t[1]) if w.scc else val(t[2]))
+        elif op.startswith("s_cmp_"):
+            a, b = val(t[0]), val(t[1])
+            w.scc = int({"eq_u32": a == b, "lt_u32": a < b, "ge_u32": a >= b, "eq_i32": a == b, "lg_u32": a != b,
+                         "gt_u32": a > b}[op[6:]])
+        elif op == "s_bitcmp1_b32":
+            w.scc = (val(t[0]) >> val(t[1])) & 1
+        elif op == "s_cbranch_scc0":
+            if not w.scc:
+                w.pc = self.labels[t[0]]
+        elif op == "s_cbranch_scc1":
+            if w.scc:
+                w.pc = self.labels[t[0]]
+        elif op == "s_branch":
+            w.pc = self.labels[t[0]]
+        else:
+            raise RuntimeError("unsupported SALU " + op)
+        return None
+
+    def valu(self, w, op, t):
+        V = w.v
+        if op == "v_accvgpr_read_b32":
+            V[d0(t)] = w.a[int(t[1][1:])].view(np.uint32)
+            return None
+        if op == "v_readfirstlane_b32":
+            w.s[int(t[0][1:])] = int(V[int(t[1][1:])][0])
+            return None
+        x = lambda i: self.vval(w, t[i])
+        M = np.uint64(M32)
+        if op == "v_lshrrev_b32":
+            r = x(2) >> (x(1) & 31)
+        elif op == "v_lshlrev_b32":
+            r = (x(2) << (x(1) & 31)) & M
+        elif op == "v_and_b32":
+            r = x(1) & x(2)
+        elif op == "v_xor_b32":
+            r = x(1) ^ x(2)
+        elif op == "v_add_u32":
+            r = (x(1) + x(2)) & M
+        elif op == "v_mov_b32":
+            r = x(1)
+        elif op == "v_lshl_add_u32":
+            r = ((x(1) << (x(2) & 31)) + x(3)) & M
+        elif op == "v_mad_u32_u24":
+            r = ((x(1) & np.uint64(0xFFFFFF)) * (x(2) & np.uint64(0xFFFFFF)) + x(3)) & M
+        elif op == "v_mul_lo_u32":
+            r = (x(1) * x(2)) & M
+        elif op == "v_add_f32":
+            a = x(1).astype(np.uint32).view(np.float32)
+            b = x(2).astype(np.uint32).view(np.float32)
+            r = (a + b).view(np.uint32).astype(np.uint64)
+        elif op == "v_cvt_pk_bf16_f32":
+            a = x(1).astype(np.uint32).view(np.float32)
+            b = x(2).astype(np.uint32).view(np.float32)
+            r = f32_to_bf16(a).astype(np.uint64) | (f32_to_bf16(b).astype(np.uint64) << np.uint64(16))
+        else:
+            raise RuntimeError("unsupported VALU " + op)
+        V[int(t[0][1:])] = r.astype(np.uint32)
+        return None
+
+    def ds_read(self, w, op, t, mods):
+        off = 0
+        for m in mods:
+            if m.startswith("offset:"):
+                off = int(m[7:])
+        dst, n = reg_range(t[0])
+        addr = w.v[int(t[1][1:])].astype(np.int64) + off
+        if op == "ds_read_b128":
+            for l in range(64):
+                a = int(addr[l])
+                assert a % 16 == 0 and a + 16 <= self.lds_alloc, f"ds_read_b128 address {a}"
+                w.v[dst:dst + 4, l] = self.lds[a:a + 16].view(np.uint32)
+        elif op == "ds_read_b64_tr_b16":
+            out = np.zeros((64, 4), dtype=np.uint16)
+            for g in range(4):
+                # lane 4q + p of the group supplies the address of row q, columns 4p..4p+3
+                block = np.zeros((4, 16), dtype=np.uint16)
+                for q in range(4):
+                    for p in range(4):
+                        a = int(addr[16 * g + 4 * q + p])
+                        assert a % 8 == 0 and a + 8 <= self.lds_alloc, f"ds_read_b64_tr_b16 address {a}"
+                        block[q, 4 * p:4 * p + 4] = self.lds[a:a + 8].view(np.uint16)
+                for i in range(16):
+                    out[16 * g + i] = block[:, i]
+            w.v[dst:dst + 2] = out.view(np.uint32).reshape(64, 2).T
+        else:
+            raise RuntimeError("unsupported DS " + op)
+        return None
+
+    def srd(self, w, tok):
+        b = reg_range(tok)[0]
+        S = w.s
+        base = int(S[b]) | ((int(S[b + 1]) & 0xFFFF) << 32)
+        return base, int(S[b + 2])
+
+    def buffer(self, w, op, t, mods):
+        imm = 0
+        for m in mods:
+            if m.startswith("offset:"):
+                imm = int(m[7:])
+        assert "offen" in mods
+        if op == "buffer_load_dwordx4" and "lds" in mods:
+            voff = w.v[int(t[0][1:])].astype(np.int64)
+            base, nr = self.srd(w, t[1])
+            soff = self.sval(w, t[2])
+            for l in range(64):
+                o = int(voff[l]) + imm
+                assert o + 16 <= nr, "DMA offset beyond num_records"
+                data = self.mem.read(base + soff + o, 16)
+                la = w.m0 + 16 * l
+                assert la + 16 <= self.lds_alloc, f"LDS-DMA write at {la}"
+                self.lds[la:la + 16] = data
+            return None
+        if op in ("buffer_load_dwordx4",):
+            dst = reg_range(t[0])[0]
+            voff = w.v[int(t[1][1:])].astype(np.int64)
+            base, nr = self.srd(w, t[2])
+            soff = self.sval(w, t[3])
+            for l in range(64):
+                data = self.mem.read(base + soff + int(voff[l]) + imm, 16).view(np.uint32)
+                w.v[dst:dst + 4, l] = data
+            return None
+        if op in ("buffer_store_dword", "buffer_store_dwordx4"):
+            src, n = reg_range(t[0])
+            n = 4 if op.endswith("x4") else 1
+            voff = w.v[int(t[1][1:])].astype(np.int64)
+            base, nr = self.srd(w, t[2])
+            soff = self.sval(w, t[3])
+            for l in range(64):
+                o = int(voff[l]) + imm
+                assert o + 4 * n <= nr or nr == M32, "store beyond num_records"
+                self.mem.write(base + soff + o, w.v[src:src + n, l].astype(np.uint32).view(np.uint8))
+            return None
+        raise RuntimeError("unsupported buffer op " + op)
+
+    def mfma(self, w, t):
+        dst = reg_range(t[0])[0]
+        a0 = reg_range(t[1])[0]
+        b0 = reg_range(t[2])[0]
+        # A lane l: row l & 15, k 8 (l >> 4) + e (e = 0..7) in 4 VGPRs of 2 bf16
+        av = w.v[a0:a0 + 4].T.copy().view(np.uint16).reshape(64, 8)
+        bv = w.v[b0:b0 + 4].T.copy().view(np.uint16).reshape(64, 8)
+        A = np.zeros((16, 32), dtype=np.float32)
+        B = np.zeros((16, 32), dtype=np.float32)
+        for l in range(64):
+            A[l & 15, 8 * (l >> 4):8 * (l >> 4) + 8] = bf16_to_f32(av[l])
+            B[l & 15, 8 * (l >> 4):8 * (l >> 4) + 8] = bf16_to_f32(bv[l])
+        D = A @ B.T
+        if t[3].strip() != "0":
+            c0 = reg_range(t[3])[0]
+            C = np.zeros((16, 16), dtype=np.float32)
+            for l in range(64):
+                for r in range(4):
+                    C[4 * (l >> 4) + r, l & 15] = w.a[c0 + r, l]
+            D = D + C
+        for l in range(64):
+            for r in range(4):
+                w.a[dst + r, l] = D[4 * (l >> 4) + r, l & 15]
+        return None
+
+
+def d0(t):
+    return int(t[0][1:])
+
+
+def run_kernel(asm_text, name, mem, kernarg, grid):
+    code, labels = parse_kernel(asm_text, name)
+    for wg in range(grid):
+        Workgroup(code, labels, mem, kernarg, wg).run()
+
+
+def selftest(asm_path):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    text = open(asm_path).read()
+    rng = np.random.default_rng(0)
+    ok = True
+    # ---- TN weight-grad kernel ----
+    for (Ktot, M, N, splits) in [(512, 256, 256, 1), (1024, 512, 256, 2)]:
+        A = rng.standard_normal((Ktot, M)).astype(np.float32)
+        B = rng.standard_normal((Ktot, N)).astype(np.float32)
+        Ab, Bb = f32_to_bf16(A), f32_to_bf16(B)
+        mem = Memory()
+        pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
+        pc = mem.alloc(np.full((splits, M, N), np.nan, dtype=np.float32), "C")
+        units = (M // 256) * (N // 256) * splits
+        ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, Ktot // splits, M, N, N, N // 256, units, units, 0, 0, 0)
+        run_kernel(text, "dalle_gemm_tn_wgrad", mem, ka, units)
+        got = mem.get(pc, np.float32, (splits, M, N)).sum(0)
+        ref = bf16_to_f32(Ab).T @ bf16_to_f32(Bb)
+        err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        print(f"tn Ktot={Ktot} M={M} N={N} splits={splits}: max_rel_err {err:.2e}")
+        ok &= err < 1e-4
+    # ---- NT plain kernel (one tile per workgroup, grid = tiles) ----
+    for (M, N, K) in [(256, 256, 256), (512, 256, 512)]:
+        A = rng.standard_normal((M, K)).astype(np.float32)
+        B = rng.standard_normal((N, K)).astype(np.float32)
+        Ab, Bb = f32_to_bf16(A), f32_to_bf16(B)
+        mem = Memory()
+        pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
+        pc = mem.alloc(np.zeros((M, N), dtype=np.uint16), "C")
+        nt = (M // 256) * (N // 256)
+        grid = (nt + 7) // 8 * 8
+        ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, N // 256, nt, grid, 0, 0, 0)
+        run_kernel(text, "dalle_gemm_nt_plain", mem, ka, grid)
+        got = bf16_to_f32(mem.get(pc, np.uint16, (M, N)))
+        ref = bf16_to_f32(Ab) @ bf16_to_f32(Bb).T
+        err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        print(f"nt M={M} N={N} K={K}: max_rel_err {err:.2e}")
+        ok &= err < 1e-2
+    return ok
+
+
+if __name__ == "__main__":
+    path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "build", "asm",
+                                                              "gemm_gfx950.s")
+    sys.exit(0 if selftest(path) else 1)

@@ -143,6 +143,8 @@ def frag_reads(set_a, set_b, h):
     """16 ds_read_b128: the 8 A fragments and 8 B fragments of k-half h (fragment f = image rows 16 f..), in
     the order the i-major MFMAs consume them (A0, B0..B7, A1..A7) so that counted lgkmcnt waits release
     each MFMA as soon as its two operands are in"""
+    if TN:
+        return tn_frag_reads(set_a, set_b, h)
     ra, rb = (V_RA0, V_RB0) if h == 0 else (V_RA1, V_RB1)
     out = []
     for op, f in READ_ORDER:
@@ -174,12 +176,13 @@ def glds_list():
     then its B image rows (s = 0..7); M0 = S_MBASE (+ B_IMG) + s KB.  The M0 write needs one wait state
     before its DMA: in a slot schedule it goes one MFMA ahead (the MFMA is the wait state, no s_nop)."""
     out = []
+    par = (lambda s: (s >> 1) & 1) if TN else (lambda s: s & 1)   # which per-lane source offset
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {s * PIECE}",
-                    f"buffer_load_dwordx4 v{V_GA1 if s & 1 else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"))
+                    f"buffer_load_dwordx4 v{V_GA1 if par(s) else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"))
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}",
-                    f"buffer_load_dwordx4 v{V_GB1 if s & 1 else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
+                    f"buffer_load_dwordx4 v{V_GB1 if par(s) else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
     return out
 
 
@@ -189,6 +192,10 @@ STAGGER = True      # per-XCD K start (the diagnostic nostagger build turns it o
 def advance_k():
     """move both operand resources one K-slice (128 bytes) forward; with the staggered start a tile walks its
     slices s0, s0 + 1, .., kt - 1, 0, .., s0 - 1, so past the last slice the resources step back by 2 K - 128"""
+    if TN:
+        # the K-step is 64 ROWS of the token-major operands
+        return [f"s_add_u32 s{S_SRDA}, s{S_SRDA}, s{S_STEPA}", f"s_addc_u32 s{S_SRDA + 1}, s{S_SRDA + 1}, 0",
+                f"s_add_u32 s{S_SRDB}, s{S_SRDB}, s{S_STEPB}", f"s_addc_u32 s{S_SRDB + 1}, s{S_SRDB + 1}, 0"]
     if not STAGGER:
         return [
             f"s_add_u32 s{S_SRDA}, s{S_SRDA}, 128", f"s_addc_u32 s{S_SRDA + 1}, s{S_SRDA + 1}, 0",
@@ -226,7 +233,8 @@ def stagger_setup(e):
 
 def toggle_reads():
     """the fragment read bases move to the other stage (at B3: the next step's data)"""
-    return [f"v_xor_b32 v{v}, {STAGE}, v{v}" for v in (V_RA0, V_RA1, V_RB0, V_RB1)]
+    regs = list(range(V_TRA, V_TRA + 4)) + list(range(V_TRB, V_TRB + 4)) if TN else (V_RA0, V_RA1, V_RB0, V_RB1)
+    return [f"v_xor_b32 v{v}, {STAGE}, v{v}" for v in regs]
 
 
 # slot map of one K-step (instructions issued after MFMA n, n = 0..127), measured on the B128 shapes
@@ -264,7 +272,11 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     m1 = mfma_list(SET1_A, SET1_B, False)
     slots = [[] for _ in range(128)]  # instructions issued after MFMA n
     # k-half-1 fragments of this step (stage X) under MFMAs 0..31 (0..43 split: all A first)
-    if SPLIT:
+    if TN:
+        set1_slots = TN_SET1_SLOTS
+        reads = frag_reads(SET1_A, SET1_B, 1)      # 16 A then 16 B transposed reads
+        dma_slots = TN_DMA_SLOTS
+    elif SPLIT:
         set1_slots = SPLIT_SET1_SLOTS
         reads = frag_reads(SET1_A, SET1_B, 1)
         reads = [r for r in reads if f", v{V_RA1} " in r] + [r for r in reads if f", v{V_RB1} " in r]
@@ -277,8 +289,9 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     for n, ins in zip(set1_slots, reads):
         slots[n].append(ins)
     # the k-half-0 fragments still in flight from the previous step: wait for each as its MFMA comes up
-    for n, cnt in set0_waits(sorted(set1_slots)).items():
-        slots[n - 1].append(f"s_waitcnt lgkmcnt({cnt})")
+    if not TN:
+        for n, cnt in set0_waits(sorted(set1_slots)).items():
+            slots[n - 1].append(f"s_waitcnt lgkmcnt({cnt})")
     # pre: before the first M0 write (an SALU add: it rewrites SCC, which the pre sequences use)
     pre_end = BA_SLOT if SPLIT else 34
     for n, ins in enumerate(pre):
@@ -287,13 +300,16 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     for n, grp in enumerate(stores):
         slots[STORE_SLOTS[n]].extend(grp)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
-    if dma and SPLIT:
+    if dma and (SPLIT or TN):
         # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
         # BB after the B reads: its B image.  Each refilled with step t + 2's piece.
-        slots[BA_SLOT].append("s_waitcnt lgkmcnt(0)")
-        slots[BA_SLOT].append("s_barrier")
-        slots[BB_SLOT].append("s_waitcnt lgkmcnt(0)")
-        slots[BB_SLOT].append("s_barrier")
+        ba, bb = (TN_BA_SLOT, TN_BB_SLOT) if TN else (BA_SLOT, BB_SLOT)
+        # BA waits for the A reads only: the B reads issued since are younger (LDS returns in order)
+        n_b = sum(1 for sl in set1_slots[len(set1_slots) // 2:] if sl <= ba)
+        slots[ba].append(f"s_waitcnt lgkmcnt({n_b})")
+        slots[ba].append("s_barrier")
+        slots[bb].append("s_waitcnt lgkmcnt(0)")
+        slots[bb].append("s_barrier")
     elif dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
         slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
@@ -316,12 +332,13 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
         slots[B3_SLOT].append("s_barrier")
         slots[B3_SLOT].extend(toggle_reads())
         busy = set(dma_slots) if dma else set()
-        free = [n for n in range(B3_SLOT + 2, 124) if n not in busy]
-        pick = [free[round(i * (len(free) - 1) / 15)] for i in range(16)]
-        for n, ins in zip(pick, frag_reads(SET0_A, SET0_B, 0)):
+        free = [n for n in range(B3_SLOT + 2, 126 if TN else 124) if n not in busy]
+        reads0 = frag_reads(SET0_A, SET0_B, 0)
+        pick = [free[round(i * (len(free) - 1) / (len(reads0) - 1))] for i in range(len(reads0))]
+        for n, ins in zip(pick, reads0):
             slots[n].append(ins)
         # MFMA 0 of the next step needs A0 / B0 (the first two of these 16 reads)
-        slots[127].append(f"s_waitcnt lgkmcnt({16 - 2})")
+        slots[127].append("s_waitcnt lgkmcnt(0)" if TN else f"s_waitcnt lgkmcnt({16 - 2})")
     mf = m0 + m1
     for n in range(128):
         e(mf[n])
@@ -784,7 +801,252 @@ def descriptor(name):
 """
 
 
-KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None)]
+
+# ----------------------------------------------------------------------------------------------------
+# weight-gradient form (TN): dW partials.  C[s] (M x N fp32) = A[k, :]^T B[k, :] summed over the split's K
+# rows, A (Ktot x M) and B (Ktot x N) TOKEN-major (the activations and output grads exactly as the forward
+# and backward hold them: no transposed copies).  One workgroup per (tile, split) unit.
+#
+# The operand image of a K-step is [64 k-rows][256 columns] in the 8-row x 32-column subtile layout
+# (cdna_hip_programming.md T10 (a)):  off(row, ch) = 2048 (row >> 3) + 512 (ch >> 2) + 64 (row & 7)
+# + 16 ((ch & 3) ^ ((row >> 2) & 3))  per 128-column half (16 KB), so one LDS-DMA instruction (1 KB, lane-
+# linear) fills 8 rows x 64 columns from whole 128-B lines, and an MFMA fragment (16 columns x 8 k) is two
+# ds_read_b64_tr_b16 (rows 8g..8g+3 / +4..7 of the k-group g, delivered column-major = the operand layout),
+# conflict-free.  The fragment's read address is base(rd, i & 1) + 512 (i >> 1) + 8192 h: 4 bases per
+# operand.  Output: the standard 16x16 accumulator layout (lane holds column 16 j + c of rows 16 i + 4 g + r),
+# stored as fp32 dwords into the split's partial slab; csrc/kernels/elementwise.hip splitk_accum folds the
+# slabs into the fp32 weight grad (deterministic).
+# ----------------------------------------------------------------------------------------------------
+TN = False
+V_TRA = 5            # A transposed-read bases (rd, i parity): v5..v8
+V_TRB = 144          # B bases: v144..v147
+V_TNT = 148          # TN temps v148..v159
+S_STEPA, S_STEPB, S_SPLIT = 79, 80, 81
+TN_SET1_SLOTS = list(range(16)) + [18 + 2 * n for n in range(16)]     # 16 A reads, then 16 B reads
+TN_BA_SLOT, TN_BB_SLOT = 21, 52
+TN_DMA_SLOTS = [23 + 4 * n for n in range(8)] + [56 + round(9.7 * n) for n in range(8)]   # 23..51, 56..124
+
+
+def tn_frag_reads(set_a, set_b, h):
+    out = []
+    for base, dst in ((V_TRA, set_a), (V_TRB, set_b)):
+        for i in range(8):
+            for rd in range(2):
+                out.append(f"ds_read_b64_tr_b16 v[{dst + 4 * i + 2 * rd}:{dst + 4 * i + 2 * rd + 1}], "
+                           f"v{base + 2 * rd + (i & 1)} offset:{8192 * h + 512 * (i >> 1)}")
+    return out
+
+
+def tn_lane_setup(e):
+    T = V_TNT
+    # ---- transposed-read bases: lane l = 16 g + 4 q + p:
+    #      2048 g + 64 (q + 4 rd) + 16 ((2 ipar + (p >> 1)) ^ ((2 g + rd) & 3)) + 8 (p & 1) + 16 KB (wave half)
+    # (v0 is the workgroup-wide thread id: every lane field is masked to the wave's 64)
+    e(f"v_lshrrev_b32 v{T}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T}, 3, v{T}")                            # g
+    e(f"v_lshrrev_b32 v{T + 1}, 2, v{V_TID}")
+    e(f"v_and_b32 v{T + 1}, 3, v{T + 1}")                    # q
+    e(f"v_lshrrev_b32 v{T + 2}, 1, v{V_TID}")
+    e(f"v_and_b32 v{T + 2}, 1, v{T + 2}")                    # p >> 1
+    e(f"v_and_b32 v{T + 3}, 1, v{V_TID}")                    # p & 1
+    e(f"v_lshlrev_b32 v{T + 4}, 11, v{T}")                   # 2048 g
+    e(f"v_lshl_add_u32 v{T + 4}, v{T + 1}, 6, v{T + 4}")      # + 64 q
+    e(f"v_lshl_add_u32 v{T + 4}, v{T + 3}, 3, v{T + 4}")      # + 8 (p & 1)
+    e(f"v_lshlrev_b32 v{T + 5}, 1, v{T}")                    # 2 g
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 14")                    # A half: 16 KB wm
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 14")
+    e(f"s_add_u32 s{S_T1}, s{S_T1}, {B_IMG}")                # B half: B_IMG + 16 KB wn
+    for rd in range(2):
+        for ipar in range(2):
+            k = 2 * rd + ipar
+            e(f"v_add_u32 v{T + 6}, {rd}, v{T + 5}")
+            e(f"v_and_b32 v{T + 6}, 3, v{T + 6}")            # (2 g + rd) & 3
+            e(f"v_add_u32 v{T + 7}, {2 * ipar}, v{T + 2}")    # 2 ipar + (p >> 1)
+            e(f"v_xor_b32 v{T + 6}, v{T + 6}, v{T + 7}")
+            e(f"v_lshl_add_u32 v{T + 6}, v{T + 6}, 4, v{T + 4}")
+            if rd:
+                e(f"v_add_u32 v{T + 6}, 256, v{T + 6}")      # rows + 4: 64 * 4
+            e(f"v_add_u32 v{V_TRA + k}, s{S_T0}, v{T + 6}")
+            e(f"v_add_u32 v{V_TRB + k}, s{S_T1}, v{T + 6}")
+    # ---- DMA sources: lane t -> row r = (t >> 2) & 7, subtile t >> 5, slot t & 3, b = (t >> 4) & 1:
+    #      r ld2 + 64 (t >> 5) + 16 (slot ^ (2 Rpar + b)) + wave part 32 (q & 1) ld2 + 256 (q >> 1)
+    e(f"v_lshrrev_b32 v{T}, 2, v{V_TID}")
+    e(f"v_and_b32 v{T}, 7, v{T}")                            # r
+    e(f"v_lshrrev_b32 v{T + 1}, 5, v{V_TID}")
+    e(f"v_and_b32 v{T + 1}, 1, v{T + 1}")
+    e(f"v_lshlrev_b32 v{T + 1}, 6, v{T + 1}")                # 64 sub
+    e(f"v_and_b32 v{T + 2}, 3, v{V_TID}")                    # slot
+    e(f"v_lshrrev_b32 v{T + 3}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T + 3}, 1, v{T + 3}")                    # b
+    for par, (ga, gb) in enumerate(((V_GA0, V_GB0), (V_GA1, V_GB1))):
+        e(f"v_add_u32 v{T + 4}, {2 * par}, v{T + 3}")
+        e(f"v_xor_b32 v{T + 4}, v{T + 2}, v{T + 4}")
+        e(f"v_lshl_add_u32 v{T + 4}, v{T + 4}, 4, v{T + 1}")  # 64 sub + 16 chunk
+        e(f"v_mov_b32 v{ga}, v{T + 4}")
+        e(f"v_mov_b32 v{gb}, v{T + 4}")
+    for g_regs, ld, offs in (((V_GA0, V_GA1), S_LDA, S_OFFA), ((V_GB0, V_GB1), S_LDB, S_OFFB)):
+        e(f"s_lshl_b32 s{S_T2}, s{ld}, 1")                   # ld2
+        e(f"s_and_b32 s{S_T0}, s{S_WAVE}, 1")
+        e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T2}")
+        e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 5")                 # 32 (q & 1) ld2
+        e(f"s_lshr_b32 s{S_T1}, s{S_WAVE}, 1")
+        e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 8")
+        e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_T1}")             # + 256 (q >> 1)
+        for gr in g_regs:
+            e(f"v_mad_u32_u24 v{gr}, v{T}, s{S_T2}, v{gr}")
+            e(f"v_add_u32 v{gr}, s{S_T0}, v{gr}")
+        for s_ in range(8):
+            e(f"s_mul_i32 s{offs + s_}, s{S_T2}, {8 * (s_ >> 1)}")
+            if s_ & 1:
+                e(f"s_add_u32 s{offs + s_}, s{offs + s_}, 128")
+    # ---- epilogue: (128 wm + 4 g) ldc4 + (128 wn + c) 4
+    e(f"v_lshrrev_b32 v{T}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T}, 3, v{T}")
+    e(f"v_lshlrev_b32 v{T}, 2, v{T}")                        # 4 g
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"v_add_u32 v{T}, s{S_T0}, v{T}")
+    e(f"v_mul_lo_u32 v{V_CO}, v{T}, s{S_LDC2}")              # S_LDC2 holds ldc * 4 in this kernel
+    e(f"v_and_b32 v{T}, 15, v{V_TID}")
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 7")
+    e(f"v_add_u32 v{T}, s{S_T1}, v{T}")
+    e(f"v_lshl_add_u32 v{V_CO}, v{T}, 2, v{V_CO}")
+
+
+def div_const_free(e, q, r, n, d, mag):
+    """s[q] = s[n] / s[d], s[r] = s[n] % s[d] with s[mag] = magic(s[d]) (0 when s[d] == 1)"""
+    e(f"s_mul_hi_u32 s{q}, s{n}, s{mag}")
+    e(f"s_cmp_eq_u32 s{mag}, 0")
+    e(f"s_cselect_b32 s{q}, s{n}, s{q}")
+    e(f"s_mul_i32 s{r}, s{q}, s{d}")
+    e(f"s_sub_u32 s{r}, s{n}, s{r}")
+
+
+def add64(e, srd, lo, hi):
+    e(f"s_add_u32 s{srd}, s{srd}, s{lo}")
+    e(f"s_addc_u32 s{srd + 1}, s{srd + 1}, s{hi}")
+
+
+def mul64(e, a, b):
+    """s[T0:T1] = s[a] * s[b] (64-bit)"""
+    e(f"s_mul_i32 s{S_T0}, s{a}, s{b}")
+    e(f"s_mul_hi_u32 s{S_T1}, s{a}, s{b}")
+
+
+def kernel_tn(name):
+    global TN
+    TN = True
+    e = Emitter(name)
+    e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")          # A B C AUX0
+    e(f"s_load_dwordx8 {sr(S_M, 8)}, s[0:1], 0x30")         # M N K lda ldb ldc tiles_n units
+    e(f"s_load_dword s{S_GRID}, s[0:1], 0x50")
+    e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+    e("s_nop 1")
+    e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+    e("s_nop 1")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
+    e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 2")                 # fp32 output: ldc * 4
+    e(f"s_cmp_lt_u32 s{S_KT}, 4")
+    e("s_cbranch_scc1 " + e.L("end"))
+    e(f"s_bitcmp1_b32 s{S_KT}, 0")
+    e("s_cbranch_scc1 " + e.L("end"))
+    # ---- unit: XCD-major when the grid is a multiple of 8 (an XCD's CUs take consecutive units: the same
+    #      split's neighbouring tiles, whose operand slices they share in L2) ----
+    e(f"s_and_b32 s{S_T0}, s{S_GRID}, 7")
+    e(f"s_mov_b32 s{S_TILE}, s{S_WG}")
+    e(f"s_cmp_eq_u32 s{S_T0}, 0")
+    e("s_cbranch_scc0 " + e.L("unit"))
+    e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
+    e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
+    e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
+    e(f"s_lshr_b32 s{S_T1}, s{S_WG}, 3")
+    e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
+    e.label(e.L("unit"))
+    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("end"))
+    # tiles = (M / 256) tiles_n; split = unit / tiles, tile = unit % tiles; (tm, tni) = tile / tiles_n
+    e(f"s_lshr_b32 s{S_T3}, s{S_M}, 8")
+    e(f"s_mul_i32 s{S_G8}, s{S_T3}, s{S_TN}")                # tiles
+    magic(e, S_MAGG, S_G8)
+    e(f"s_cmp_lt_u32 s{S_G8}, 2")
+    e(f"s_cselect_b32 s{S_MAGG}, 0, s{S_MAGG}")
+    div_const_free(e, S_SPLIT, S_T2, S_TILE, S_G8, S_MAGG)
+    e(f"s_mov_b32 s{S_ROWREM}, s{S_T2}")                    # tile
+    magic(e, S_MAGR, S_TN)
+    e(f"s_cmp_lt_u32 s{S_TN}, 2")
+    e(f"s_cselect_b32 s{S_MAGR}, 0, s{S_MAGR}")
+    div_const_free(e, S_TM, S_TNI, S_ROWREM, S_TN, S_MAGR)
+    e(f"s_lshl_b32 s{S_ROW0}, s{S_TM}, 8")
+    e(f"s_lshl_b32 s{S_COL0}, s{S_TNI}, 8")
+    # ---- operand resources: base + split K rows + the tile's column block (no bounds: host-checked) ----
+    e(f"s_mul_i32 s{S_T3}, s{S_SPLIT}, s{S_K}")             # first K row of the split
+    for srd, ptr, ld, col, step in ((S_SRDA, S_A, S_LDA, S_ROW0, S_STEPA), (S_SRDB, S_B, S_LDB, S_COL0, S_STEPB)):
+        e(f"s_mov_b32 s{srd}, s{ptr}")
+        e(f"s_mov_b32 s{srd + 1}, s{ptr + 1}")
+        mul64(e, S_T3, ld)
+        e(f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 1")
+        add64(e, srd, S_T0, S_T1)
+        e(f"s_lshl_b32 s{S_T0}, s{col}, 1")
+        e(f"s_add_u32 s{srd}, s{srd}, s{S_T0}")
+        e(f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0")
+        e(f"s_mov_b32 s{srd + 2}, -1")
+        e(f"s_mov_b32 s{srd + 3}, 0x20000")
+        e(f"s_lshl_b32 s{step}, s{ld}, 7")                  # 64 rows * 2 bytes
+    # ---- partial slab: C + (split M N + row0 ldc + col0) * 4 ----
+    e(f"s_mov_b32 s{S_SRDC}, s{S_C}")
+    e(f"s_mov_b32 s{S_SRDC + 1}, s{S_C + 1}")
+    e(f"s_mul_i32 s{S_T3}, s{S_M}, s{S_N}")
+    mul64(e, S_SPLIT, S_T3)
+    e(f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 2")
+    add64(e, S_SRDC, S_T0, S_T1)
+    mul64(e, S_ROW0, S_LDC)
+    e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}")
+    e(f"s_addc_u32 s{S_T1}, s{S_T1}, 0")
+    e(f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 2")
+    add64(e, S_SRDC, S_T0, S_T1)
+    e(f"s_mov_b32 s{S_SRDC + 2}, -1")
+    e(f"s_mov_b32 s{S_SRDC + 3}, 0x20000")
+    e(f"s_lshl_b32 s{S_MBASE}, s{S_WAVE}, 13")
+    tn_lane_setup(e)
+    prologue_dma(e)
+    e("s_waitcnt vmcnt(16)")
+    e("s_barrier")
+    for ins in frag_reads(SET0_A, SET0_B, 0):
+        e(ins)
+    e("s_waitcnt lgkmcnt(0)")
+    iteration(e, "first")
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    e.label(e.L("kloop"))
+    iteration(e, "loop")
+    e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc0 " + e.L("kloop"))
+    iteration(e, "penult")
+    iteration(e, "last")
+    for _ in range(3):
+        e("s_nop 7")
+    # ---- fp32 partial tile: lane holds column 16 j + c of rows 16 i + 4 g + r ----
+    n = 0
+    for i in range(8):
+        for r in range(4):
+            e(f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}")
+            for j in range(8):
+                t = V_TNT + (n % 8)
+                n += 1
+                e(f"v_accvgpr_read_b32 v{t}, a{(i * 8 + j) * 4 + r}")
+                e(f"buffer_store_dword v{t}, v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen offset:{64 * j}")
+    e.label(e.L("end"))
+    e("s_waitcnt vmcnt(0)")
+    e("s_endpgm")
+    TN = False
+    return e.text()
+
+
+KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")]
 
 
@@ -793,7 +1055,7 @@ def main(out, diag=False):
     metas = []
     for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
-        parts.append(kernel(name, epi, dg))
+        parts.append(kernel_tn(name) if epi == "tn" else kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
         parts.append(descriptor(name))
         metas.append(metadata(name))

@@ -502,6 +502,26 @@ Tensor gemm_nt(Tensor A, Tensor B, c10::optional<Tensor> bias, int64_t variant) 
 
 // ---- hand-scheduled assembly GEMMs (csrc/asm/gen_gemm.py): C = A . B^T (+ fp32 bias) ----
 // A (M, K), B (N, K) bf16 (row strides free, K-contiguous); M, N multiples of 256, K of 128, K >= 256
+// out (M, N) fp32 (+)= A^T B: A (Ktot, M), B (Ktot, N) bf16 token-major (unit column stride); the reduction over
+// the Ktot tokens runs as `splits` K-ranges on the assembly TN kernel, whose fp32 partial slabs splitk_accum folds
+// into out in a fixed order (deterministic)
+void asm_wgrad_(Tensor out, Tensor A, Tensor B, int64_t splits, bool accumulate) {
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "asm_wgrad: bf16 cuda");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0), "asm_wgrad: A (Ktot, M), B (Ktot, N)");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "asm_wgrad: unit column stride");
+  CHECK_IN(out, torch::kFloat32);
+  const int Ktot = A.size(0), M = A.size(1), N = B.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N, "asm_wgrad: out (M, N)");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && splits > 0 && Ktot % splits == 0 && (Ktot / splits) % 128 == 0 &&
+                  Ktot / splits >= 256, "asm_wgrad: M, N multiples of 256, Ktot / splits a multiple of 128 (>= 256)");
+  TORCH_CHECK((int64_t)Ktot * A.stride(0) * 2 < (1ll << 40) && A.stride(0) < (1 << 23) && B.stride(0) < (1 << 23), "asm_wgrad: strides");
+  Tensor part = torch::empty({splits, M, N}, out.options());
+  TORCH_CHECK(dalle::asm_gemm_tn(A.data_ptr(), B.data_ptr(), part.data_ptr(), M, N, Ktot, (int)A.stride(0), (int)B.stride(0),
+                                 (int)splits, cur_stream()),
+              "asm_wgrad: launch failed");
+  dalle::splitk_accum(part.data_ptr<float>(), out.data_ptr<float>(), (long)M * N, (int)splits, accumulate ? 1 : 0, cur_stream());
+}
+
 Tensor asm_gemm(Tensor A, Tensor B, c10::optional<Tensor> bias, c10::optional<Tensor> out) {
   TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "asm_gemm: bf16 cuda");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "asm_gemm: A (M, K) and B (N, K)");
@@ -1229,6 +1249,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
   m.def("asm_gemm", &asm_gemm, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out") = py::none());
+  m.def("asm_wgrad_", &asm_wgrad_, py::arg("out"), py::arg("A"), py::arg("B"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
   m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),
         py::arg("n"), py::arg("col_major"), py::arg("qscale"), py::arg("persist") = -1);

@@ -104,7 +104,7 @@ def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
 # (csrc/asm/gen_gemm.py: hipBLASLt's own gfx950 structure -- 4 waves, 128x128 AGPR quadrants, LDS-DMA two
 # K-steps ahead -- with every instruction placed by the generator) wherever the shape tiles; hipBLASLt
 # otherwise. DALLE_AMD_ASM_GEMM=0 sends every plain product to hipBLASLt (A/B).
-ASM_GEMM = os.environ.get("DALLE_AMD_ASM_GEMM", "0") != "0"
+ASM_GEMM = os.environ.get("DALLE_AMD_ASM_GEMM", "1") != "0"
 
 
 def _asm_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -199,7 +199,7 @@ def wgrad_splits(M: int, N: int, K: int) -> int:
 # X^T (one bf16 transpose kernel, ~60 us per 168 MB) instead of X, and dW = g^T X runs on hipBLASLt with
 # a token-contiguous B operand: 3072x1024 1128 vs 847 TF/s, 8192x1024 1334 vs 1130 at M = 81920
 # (profiles/r3s5_wgrad_nt_vs_tn_m81920.txt).
-WGRAD_XT = True
+WGRAD_XT = not ASM_GEMM   # the assembly TN weight-grad kernel reads token-major inputs directly
 
 
 class XT:
@@ -219,7 +219,7 @@ class XT:
 # per 168 MB; the 1024x4096 product runs at 1265 vs 1106 TF/s in isolation): small but consistent in the full
 # step -- micro-batch 64 229.50 / 229.41 vs 229.54 / 229.63 ms, micro-batch 128 459.41 / 458.95 vs 460.09 /
 # 461.66 ms (same box each, profiles/r3s5_wgrad_xt_ab.txt)
-WGRAD_GT = True
+WGRAD_GT = not ASM_GEMM
 
 
 def saved_gemm_input(x2: torch.Tensor, enabled: Optional[bool] = None):
@@ -273,6 +273,33 @@ def _weight_grad_t(gw, fused: bool, g2, x2):
     return torch.mm(a[0], b[0], out_dtype=torch.float32)
 
 
+def asm_wgrad_splits(M: int, N: int, K: int) -> int:
+    """Split count of the assembly TN weight-grad kernel for an (N x K) weight over M tokens, or 0 when the
+    shape does not tile: the (tile, split) units should fill whole waves of the 256 CUs (then the fewest
+    splits: every split adds an fp32 partial slab to the fold).  Measured at M = 163840
+    (profiles/r5_asm_wgrad_tn.jsonl): 1024x1024 s16 1439 TF/s, 3072x1024 s16 1441, 8192x1024 s2 1535,
+    1024x4096 s4 1493 (hipBLASLt on the same token-major operands: 496 / 742 / 1130 / 992)."""
+    if N % 256 or K % 256:
+        return 0
+    tiles = (N // 256) * (K // 256)
+    best = None
+    for s in (1, 2, 4, 5, 8, 10, 16, 20, 32):
+        if M % (128 * s) or M // s < 256:
+            continue
+        units = tiles * s
+        util = units / (-(-units // 256) * 256)
+        key = (round(util, 2), -s)
+        if best is None or key > best[0]:
+            best = (key, s)
+    return best[1] if best else 0
+
+
+def _asm_wgrad_ok(g2, x2) -> bool:
+    return (ASM_GEMM and isinstance(g2, torch.Tensor) and isinstance(x2, torch.Tensor) and g2.is_cuda
+            and g2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and g2.dim() == 2 and x2.dim() == 2
+            and g2.stride(1) == 1 and x2.stride(1) == 1 and g2.shape[0] == x2.shape[0])
+
+
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2):
     """dW = g2^T x2 in fp32. When ``w.grad`` already exists (the flat grad arena), accumulate into it
     and return None: no temporary dW and no autograd add kernel, and the shared blocks' grads (one per
@@ -284,6 +311,13 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2):
     if isinstance(x2, XT) or isinstance(g2, XT):
         return _weight_grad_t(gw, fused, g2, x2)
     M, N, K = g2.shape[0], g2.shape[1], x2.shape[1]
+    if _asm_wgrad_ok(g2, x2):
+        s = asm_wgrad_splits(M, N, K)
+        if s:
+            _count("asm_wgrad")
+            out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)
+            C().asm_wgrad_(out, g2, x2, s, fused)
+            return None if fused else out
     s = wgrad_splits(M, N, K)
     if s > 1:
         out = gw if fused else torch.empty(N, K, dtype=torch.float32, device=g2.device)

@@ -62,3 +62,44 @@ def test_fragment_reads_are_bank_conflict_free():
             r_img, pos = 8 * d + (t >> 3), t & 7
             chunk = pos ^ (4 * (d & 1) + ((t >> 3) >> 1))
             assert pos == chunk ^ ((r_img >> 1) & 7)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(LLVM, "clang")), reason="ROCm LLVM not installed")
+def test_kernels_on_the_emulator(tmp_path):
+    """csrc/asm/emu.py runs the generated NT and TN kernels instruction by instruction on one small shape each,
+    bounds-checking every global / LDS access, and compares with numpy (it caught the TN kernel's unmasked
+    lane fields -- an out-of-range store -- before a second GPU run)."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import struct
+
+    import numpy as np
+
+    import emu
+    import gen_gemm
+
+    s = tmp_path / "g.s"
+    gen_gemm.main(str(s))
+    text = s.read_text()
+    rng = np.random.default_rng(0)
+    Ktot, M, N = 512, 256, 256
+    Ab = emu.f32_to_bf16(rng.standard_normal((Ktot, M)).astype(np.float32))
+    Bb = emu.f32_to_bf16(rng.standard_normal((Ktot, N)).astype(np.float32))
+    mem = emu.Memory()
+    pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
+    pc = mem.alloc(np.zeros((M, N), dtype=np.float32), "C")
+    ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, Ktot, M, N, N, 1, 1, 1, 0, 0, 0)
+    emu.run_kernel(text, "dalle_gemm_tn_wgrad", mem, ka, 1)
+    ref = emu.bf16_to_f32(Ab).T @ emu.bf16_to_f32(Bb)
+    got = mem.get(pc, np.float32, (M, N))
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-4
+    K = 256
+    Ab = emu.f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
+    Bb = emu.f32_to_bf16(rng.standard_normal((N, K)).astype(np.float32))
+    mem = emu.Memory()
+    pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
+    pc = mem.alloc(np.zeros((M, N), dtype=np.uint16), "C")
+    ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, 1, 1, 8, 0, 0, 0)
+    emu.run_kernel(text, "dalle_gemm_nt_plain", mem, ka, 8)
+    ref = emu.bf16_to_f32(Ab) @ emu.bf16_to_f32(Bb).T
+    got = emu.bf16_to_f32(mem.get(pc, np.uint16, (M, N)))
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-2

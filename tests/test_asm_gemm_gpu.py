@@ -50,3 +50,36 @@ def test_asm_gemm_rejects_untiled(cuda, C):
     B = torch.randn(256, 256, device=cuda).to(torch.bfloat16)
     with pytest.raises(RuntimeError):
         C.asm_gemm(A, B, None, None)
+
+
+@pytest.mark.parametrize("Ktot,M,N,splits", [(2048, 256, 256, 1), (4096, 512, 768, 2), (16384, 1024, 1024, 16),
+                                             (24576, 768, 512, 3), (32768, 3072, 1024, 16)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_asm_wgrad_matches_fp32(cuda, C, Ktot, M, N, splits, accumulate):
+    """dW (+)= G^T X on the assembly TN kernel (token-major operands, split-K partial slabs + fold)"""
+    torch.manual_seed(Ktot + M + N)
+    G = torch.randn(Ktot, M, device=cuda).to(torch.bfloat16)
+    X = torch.randn(Ktot, N, device=cuda).to(torch.bfloat16)
+    out = torch.randn(M, N, device=cuda)
+    init = out.clone()
+    C.asm_wgrad_(out, G, X, splits, accumulate)
+    ref = G.float().t() @ X.float() + (init if accumulate else 0)
+    err = ((out - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-4, err
+
+
+def test_weight_grad_routes_to_asm(cuda, C):
+    from dalle_amd.ops import hip_ops
+
+    if not hip_ops.ASM_GEMM:
+        pytest.skip("assembly GEMM disabled")
+    torch.manual_seed(3)
+    w = torch.nn.Parameter(torch.randn(1024, 1024, device=cuda))
+    w.grad = torch.zeros_like(w)
+    g = torch.randn(8192, 1024, device=cuda).to(torch.bfloat16)
+    x = torch.randn(8192, 1024, device=cuda).to(torch.bfloat16)
+    before = hip_ops.PATH_COUNTS.get("asm_wgrad", 0)
+    assert hip_ops.weight_grad(w, g, x) is None
+    ref = g.float().t() @ x.float()
+    assert ((w.grad - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    assert hip_ops.PATH_COUNTS.get("asm_wgrad", 0) == before + 1

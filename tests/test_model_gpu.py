@@ -168,7 +168,7 @@ def test_reversible_stored_activations_match_recompute(cuda):
 def test_sequential_fused_stack_matches_per_sublayer(cuda, monkeypatch):
     """Non-reversible stack as one node with fused sublayer boundaries (ln_shift_fwd_res / ln_shift_bwd_sr)
     == the per-sublayer autograd nodes, with every gradient landing in the flat arena."""
-    from dalle_amd.ops import hip_ops
+    import dalle_amd.ops as ops_mod
 
     torch.manual_seed(0)
     cfg = _cfg(False)
@@ -177,8 +177,10 @@ def test_sequential_fused_stack_matches_per_sublayer(cuda, monkeypatch):
     text = torch.randint(1, cfg.num_text_tokens, (2, cfg.text_seq_len), device=cuda)
     img = torch.randint(0, cfg.num_image_tokens, (2, cfg.image_seq_len), device=cuda)
     grads, losses = [], []
+    fused_stack = ops_mod.sequential_stack
     for fused in (1, 0):
-        monkeypatch.setattr(hip_ops, "FUSED_SEQUENTIAL", fused)
+        # the unfused arm: the stack declines and the model runs the per-sublayer nodes
+        monkeypatch.setattr(ops_mod, "sequential_stack", fused_stack if fused else (lambda x, subs: None))
         arena.zero_grad()
         loss = m(text, img, return_loss=True)
         loss.backward()
@@ -274,8 +276,8 @@ def test_fused_lamb_restore_before_first_step(cuda):
     assert torch.equal(arena2.data, ref)
 
 
-@pytest.mark.parametrize("reversible,own", [(False, False), (True, False), (False, True)])
-def test_reference_geometry_end_to_end(cuda, reversible, own, monkeypatch):
+@pytest.mark.parametrize("reversible,asm", [(False, False), (True, False), (False, True), (True, True)])
+def test_reference_geometry_end_to_end(cuda, reversible, asm, monkeypatch):
     """The bench / reference geometry (d=1024, 16 heads, 256 text + 32x32 image tokens, the attention /
     sharing cycle of the recipe) with the flat arena attached, B=2 (M = 2560 = 10 x 256), so every fused
     path runs: QKV GEMM + rotary epilogue, FF dgrad + GEGLU-backward epilogue, the fused sequential /
@@ -284,9 +286,11 @@ def test_reference_geometry_end_to_end(cuda, reversible, own, monkeypatch):
     from dalle_amd.data.synthetic import synthetic_batch
     from dalle_amd.ops import hip_ops
 
-    if own:  # every projection GEMM on the hand-written kernels, FF-in with the GEGLU epilogue
-        monkeypatch.setattr(hip_ops, "OWN_GEMM", 2)
-        monkeypatch.setattr(hip_ops, "FUSED_FF_IN", 1)
+    # asm: the plain projections and the weight grads on the assembly GEMMs (token-major weight-grad inputs);
+    # otherwise hipBLASLt with the token-contiguous transposed weight-grad inputs
+    monkeypatch.setattr(hip_ops, "ASM_GEMM", asm)
+    monkeypatch.setattr(hip_ops, "WGRAD_XT", not asm)
+    monkeypatch.setattr(hip_ops, "WGRAD_GT", not asm)
     torch.manual_seed(0)
     cfg = DALLEConfig(depth=4, attn_types=reference_attn_types(4), shared_attn_ids=reference_shared_ids(4),
                       shared_ff_ids=reference_shared_ids(4), reversible=reversible)
@@ -301,7 +305,7 @@ def test_reference_geometry_end_to_end(cuda, reversible, own, monkeypatch):
     loss.backward()
     torch.cuda.synchronize()
     stack = "reversible_stack" if reversible else "sequential_stack"
-    for path in ("qkv_rope", "ff_dgrad_geglu", stack) + (("own_gemm", "ff_in_geglu") if own else ()):
+    for path in ("qkv_rope", "ff_dgrad_geglu", stack) + (("asm_gemm", "asm_wgrad") if asm else ("wgrad_xt",)):
         assert hip_ops.PATH_COUNTS.get(path, 0) > 0, (path, hip_ops.PATH_COUNTS)
     torch.set_num_threads(16)
     loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
