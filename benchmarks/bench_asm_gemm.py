@@ -132,6 +132,39 @@ def bench_tn(mod, shapes, iters=10, rounds=5):
                           "TF": {k: round(flop / v / 1e6) for k, v in us.items()}}), flush=True)
 
 
+def bench_geglu(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
+    """FF-in GEMM + fused GEGLU vs the same GEMM with the bias epilogue only (the fusion's extra cost)"""
+    x = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+    w = torch.rand(2 * F, K, device="cuda").sub_(0.5).mul_(0.06).to(torch.bfloat16)
+    b = torch.zeros(2 * F, device="cuda")
+    a = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    u = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    nt = (M // 256) * (2 * F // 256)
+    grid = min(256, (nt + 7) // 8 * 8)
+    ptrs = [x.data_ptr(), w.data_ptr(), a.data_ptr(), b.data_ptr(), u.data_ptr(), 0]
+    ints = [M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0]
+    args = struct.pack("<6Q12i", *ptrs, *ints)
+    fns = {"asm_bias": lambda: mod.launch("dalle_gemm_nt_bias", grid, args),
+           "asm_geglu": lambda: mod.launch("dalle_gemm_nt_geglu", grid, args)}
+    if diag is not None:
+        fns["asm_geglu_nowork"] = lambda: diag.launch("dalle_gemm_diag_geglu_nowork", grid, args)
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                f()
+            e.record()
+            e.synchronize()
+            times[k].append(s.elapsed_time(e) * 1000 / iters)
+    us = {k: round(sorted(v)[len(v) // 2], 1) for k, v in times.items()}
+    print(json.dumps({"shape": f"GEGLU_M{M}_F{F}_K{K}", "us": us}), flush=True)
+
+
 def check(mod, shapes):
     ok = True
     for (M, N, K) in shapes:
@@ -192,6 +225,7 @@ def main():
     ap.add_argument("--diag", action="store_true", help="also time the measurement-only variants")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tn", action="store_true", help="also time the weight-gradient (TN) kernel")
+    ap.add_argument("--geglu", action="store_true", help="also time the fused FF-in + GEGLU kernel")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
@@ -205,6 +239,9 @@ def main():
         sys.exit(1)
     if a.check_only:
         return
+    if a.geglu:
+        bench_geglu(mod, rounds=a.rounds,
+                    diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
     if a.tn:
         bench_tn(mod, [(163840, 1024, 1024, 16), (163840, 3072, 1024, 16), (163840, 8192, 1024, 2),
                        (163840, 1024, 4096, 4)], rounds=a.rounds)

@@ -127,11 +127,22 @@ class Workgroup:
         return int(tok) & M32
 
     def vval(self, w, tok):
-        """per-lane uint32 operand: VGPR, SGPR (broadcast) or constant"""
+        """per-lane uint32 operand: VGPR, SGPR (broadcast) or constant (integer, or an inline float like 0.5)"""
         tok = tok.strip()
         if tok.startswith("v") and tok[1:].isdigit():
             return w.v[int(tok[1:])].astype(np.uint64)
+        if re.match(r"^-?\d+\.\d+$", tok):
+            return np.full(64, int(np.float32(float(tok)).view(np.uint32)), dtype=np.uint64)
         return np.full(64, self.sval(w, tok), dtype=np.uint64)
+
+    def fval(self, w, tok):
+        """per-lane fp32 operand with an optional neg (-v) or abs (|v|) modifier"""
+        tok = tok.strip()
+        if tok.startswith("|") and tok.endswith("|"):
+            return np.abs(self.vval(w, tok[1:-1]).astype(np.uint32).view(np.float32))
+        neg = tok.startswith("-v")
+        r = self.vval(w, tok[1:] if neg else tok).astype(np.uint32).view(np.float32)
+        return -r if neg else r
 
     def run_wave(self, w):
         """run until a barrier or the end; returns 'barrier' or 'end'"""
@@ -173,7 +184,7 @@ class Workgroup:
             return "barrier"
         if op in ("s_nop", "s_waitcnt"):
             return None
-        if op == "s_load_dwordx8" or op == "s_load_dword":
+        if op in ("s_load_dwordx8", "s_load_dwordx2", "s_load_dword"):
             base, n = reg_range(toks[0])
             addr = (int(S[int(toks[1][2:].split(":")[0])]) | (int(S[int(toks[1][2:].split(":")[0]) + 1]) << 32)) + int(toks[2], 16)
             data = self.mem.read(addr, 4 * n).view(np.uint32)
@@ -247,6 +258,8 @@ class Workgroup:
 
     def valu(self, w, op, t):
         V = w.v
+        if op.endswith("_e64"):
+            op = op[:-4]
         if op == "v_accvgpr_read_b32":
             V[d0(t)] = w.a[int(t[1][1:])].view(np.uint32)
             return None
@@ -273,10 +286,24 @@ class Workgroup:
             r = ((x(1) & np.uint64(0xFFFFFF)) * (x(2) & np.uint64(0xFFFFFF)) + x(3)) & M
         elif op == "v_mul_lo_u32":
             r = (x(1) * x(2)) & M
-        elif op == "v_add_f32":
-            a = x(1).astype(np.uint32).view(np.float32)
-            b = x(2).astype(np.uint32).view(np.float32)
-            r = (a + b).view(np.uint32).astype(np.uint64)
+        elif op in ("v_add_f32", "v_mul_f32", "v_fma_f32", "v_fmaak_f32", "v_rcp_f32", "v_exp_f32"):
+            f = lambda i: self.fval(w, t[i])
+            with np.errstate(all="ignore"):
+                if op == "v_add_f32":
+                    rf = f(1) + f(2)
+                elif op == "v_mul_f32":
+                    rf = f(1) * f(2)
+                elif op == "v_fma_f32":
+                    rf = (f(1).astype(np.float64) * f(2) + f(3)).astype(np.float32)
+                elif op == "v_fmaak_f32":
+                    rf = (f(1).astype(np.float64) * f(2) + f(3)).astype(np.float32)
+                elif op == "v_rcp_f32":
+                    rf = (np.float32(1.0) / f(1)).astype(np.float32)
+                else:
+                    rf = np.exp2(f(1)).astype(np.float32)
+            r = rf.astype(np.float32).view(np.uint32).astype(np.uint64)
+        elif op == "v_bfi_b32":
+            r = (x(1) & x(2)) | (~x(1) & M & x(3))
         elif op == "v_cvt_pk_bf16_f32":
             a = x(1).astype(np.uint32).view(np.float32)
             b = x(2).astype(np.uint32).view(np.float32)
@@ -435,7 +462,47 @@ def selftest(asm_path):
         err = float(np.abs(got - ref).max() / np.abs(ref).max())
         print(f"nt M={M} N={N} K={K}: max_rel_err {err:.2e}")
         ok &= err < 1e-2
+    ok &= selftest_geglu(text)
     return ok
+
+
+def ff_in_perm(F):
+    """interleaved row order of W1 for the geglu kernel: [value 8 | gate 8] blocks"""
+    n = np.arange(2 * F)
+    b, e = n // 16, n % 16
+    return np.where(e < 8, 8 * b + e, F + 8 * b + e - 8)
+
+
+def gelu_ref(x):
+    from math import erf, sqrt
+    return np.array([0.5 * v * (1 + erf(v / sqrt(2))) for v in x.ravel()], dtype=np.float64).reshape(x.shape)
+
+
+def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):
+    rng = np.random.default_rng(1)
+    x = f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
+    w1 = (rng.standard_normal((2 * F, K)) * 0.03).astype(np.float32)
+    b1 = (rng.standard_normal(2 * F) * 0.1).astype(np.float32)
+    perm = ff_in_perm(F)
+    w1p = f32_to_bf16(w1[perm])
+    b1p = b1[perm].astype(np.float32)
+    mem = Memory()
+    pa, pb = mem.alloc(x, "x"), mem.alloc(w1p, "w1p")
+    pc = mem.alloc(np.zeros((M, 2 * F), dtype=np.uint16), "a")
+    pbias = mem.alloc(b1p, "b1p")
+    pu = mem.alloc(np.zeros((M, F), dtype=np.uint16), "u")
+    nt = (M // 256) * (2 * F // 256)
+    ka = struct.pack("<6Q12i", pa, pb, pc, pbias, pu, 0, M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0)
+    run_kernel(text, "dalle_gemm_nt_geglu", mem, ka, grid)
+    a = bf16_to_f32(mem.get(pc, np.uint16, (M, 2 * F)))
+    u = bf16_to_f32(mem.get(pu, np.uint16, (M, F)))
+    a_ref = bf16_to_f32(x) @ bf16_to_f32(f32_to_bf16(w1)).T + b1
+    err_a = float(np.abs(a - a_ref).max() / np.abs(a_ref).max())
+    ab = a.astype(np.float64)
+    u_ref = ab[:, :F] * gelu_ref(ab[:, F:])
+    err_u = float(np.abs(u - u_ref).max() / np.abs(u_ref).max())
+    print(f"geglu M={M} F={F} K={K}: a max_rel_err {err_a:.2e}, u (from the stored a) {err_u:.2e}")
+    return err_a < 1e-2 and err_u < 1e-2
 
 
 if __name__ == "__main__":

@@ -38,6 +38,7 @@ Diagnostic builds (``--diag``, measurement only, never loaded by the framework):
 
 Usage:  gen_gemm.py OUT.s [--diag]     (assemble with clang -target amdgcn-amd-amdhsa -mcpu=gfx950)
 """
+import re
 import sys
 
 # ----------------------------------------------------------------------------------------------------
@@ -67,7 +68,7 @@ S_TM, S_TNI = 67, 68  # tile row / column index
 S_G8, S_MAGG, S_FULL, S_TMFULL, S_ROWREM, S_MAGR = 69, 70, 71, 76, 77, 78
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
 S_KV, S_WRAP, S_S0B = 79, 80, 81   # K-slice of the next DMA, 128 - 2 K (the wrap step), first slice * 128
-S_LAST = 84
+S_LAST = 98
 
 # VGPRs
 V_TID = 0
@@ -258,7 +259,7 @@ SPLIT_DMA_SLOTS = [20 + 4 * n for n in range(8)] + [54 + 10 * n for n in range(8
 STORE_SLOTS = [3 + 4 * n for n in range(8)]                   # deferred epilogue stores: before B2
 
 
-def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
+def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), head=(), work=(), work_span=(40, 120)):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
     ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
@@ -266,7 +267,10 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     under these steps' MFMAs. ``pre``: scalar instructions spread in order over MFMAs 1..33 (next-tile setup).
     ``stores``: instruction groups (the previous tile's deferred epilogue stores) issued early in the step,
     older than this step's DMA; ``extra``: VMEM operations issued after the previous step's DMA and before
-    this step's B3 that B3 need not wait for (the stores here plus whatever the caller issued).
+    this step's B3 that B3 need not wait for (issued by the caller between the previous step and this one;
+    every VMEM instruction this step places before B3 is counted here).  ``head``: instructions before MFMA 0;
+    ``work``: instructions spread in order over the MFMA gaps of ``work_span`` (a fused epilogue's deferred
+    work; its VMEM must sit before the step's last DMA).  Returns this step's VMEM instructions in issue order.
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
@@ -299,6 +303,11 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     assert len(stores) <= len(STORE_SLOTS)
     for n, grp in enumerate(stores):
         slots[STORE_SLOTS[n]].extend(grp)
+    if work:
+        lo, hi = work_span
+        assert hi <= 120
+        for n, ins in enumerate(work):
+            slots[lo + n * (hi - lo) // len(work)].append(ins)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
     if dma and (SPLIT or TN):
         # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
@@ -326,7 +335,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
     if kind != "last":
         # B3: step t + 1's DMA (issued during the previous step) landed for every wave; the DMA of this
         # step issued so far may stay in flight. Then read step t + 1's k-half-0 fragments from stage Y.
-        younger = (sum(1 for sl in dma_slots if sl <= B3_SLOT) if dma else 0) + extra
+        younger = sum(1 for n in range(B3_SLOT + 1) for ins in slots[n] if ins.startswith("buffer_")) + extra
         assert younger < 64
         slots[B3_SLOT].append(f"s_waitcnt vmcnt({younger})")
         slots[B3_SLOT].append("s_barrier")
@@ -340,10 +349,13 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=()):
         # MFMA 0 of the next step needs A0 / B0 (the first two of these 16 reads)
         slots[127].append("s_waitcnt lgkmcnt(0)" if TN else f"s_waitcnt lgkmcnt({16 - 2})")
     mf = m0 + m1
+    for ins in head:
+        e(ins)
     for n in range(128):
         e(mf[n])
         for ins in slots[n]:
             e(ins)
+    return [ins for n in range(128) for ins in slots[n] if ins.startswith("buffer_")]
 
 
 # ----------------------------------------------------------------------------------------------------
@@ -635,7 +647,7 @@ def kernel(name, epi, diag=None):
     for n, cnt in enumerate(DEFER_SPLIT):
         grp = groups[k:k + cnt] if groups else []
         k += cnt
-        iteration(e, "first" if n == 0 else "loop", diag, (extra if n == 0 else 0) + len(grp), stores=grp)
+        iteration(e, "first" if n == 0 else "loop", diag, extra if n == 0 else 0, stores=grp)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, {3 + len(DEFER_SPLIT) - 1}")
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc1 " + e.L("tail"))
@@ -1046,8 +1058,269 @@ def kernel_tn(name):
     return e.text()
 
 
-KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None)]
-DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")]
+
+# ----------------------------------------------------------------------------------------------------
+# FF-in GEMM + GEGLU forward: a = x W1^T + b1 (M x 2F, [value | gate] column order) and u = value * gelu(gate)
+# (M x F).  The B operand is W1 with its rows interleaved in 8-row blocks [value j0..j0+7 | gate j0..j0+7 | ..]
+# (host: ff_in_perm), so lane c of a wave half holds a value block (c even) or the matching gate block (c odd);
+# the epilogue writes `a` back in the ORIGINAL column order (value j -> column j, gate j -> F + j: a per-lane
+# base, whole 16-byte chunks), deferred like the plain kernel.  u is computed from the stored (bf16) `a` --
+# the numbers the unfused geglu kernel reads -- during the NEXT tile's K-steps 3..13: each wave reloads the
+# value / gate chunks of its own rows and columns (L2-hot, written one to three steps earlier by the same
+# wave), one K-step ahead, and its gelu VALU fills the MFMA gaps.  Needs kt = 16 (K = 1024; the host checks):
+# the K-loop of a successor tile is fully unrolled so the deferred work can be placed statically.
+# ----------------------------------------------------------------------------------------------------
+S_SRDU = 84          # u resource (4)
+S_SOFFU, S_SOFFV, S_GP, S_MASK7, S_F2, S_LDU2 = 88, 89, 90, 91, 92, 93
+S_RSQ2, S_A5 = 94, 95
+GE_C4 = 10           # v10: the a4 coefficient (a lane constant; v10 is a setup temp only)
+S_AUX1, S_LDU = 22, 21
+V_RLA, V_CU, V_RLG = 13, 14, 15
+GE_BANK = (144, 160)     # reload banks (2 row-groups x [value 4 | gate 4] each)
+GE_T = 176               # gelu temps v176..v182
+# u row-groups computed per K-step (loaded one step earlier): row-group rg needs the `a` chunks 4 (rg >> 1) ..
+# +3, stored at the boundary (< 6) or in steps 0..3 (DEFER_SPLIT), and a store is complete two steps later
+GE_PLAN = {2: (0,), 3: (1, 2), 4: (3,), 5: (4,), 6: (5, 6), 7: (7,), 8: (8,), 9: (9, 10), 10: (11,), 11: (12,),
+           12: (13, 14), 13: (15,)}
+GE_CONSTS = {"c_rsqrt2": 0x3F3504F3, "a5": 0x3F87DC22, "a4": 0xBFBA00E3, "a3": 0x3FB5F0E3, "a2": 0xBE91A98E,
+             "a1": 0x3E827906, "nhl2e": 0xBF38AA3B}
+
+
+def ge_loads(rg, bank_base, slot):
+    """value / gate chunks of u row-group rg (rows 8 rg .. +7 of the wave, 8 j per lane) into a bank slot"""
+    va = bank_base + 8 * slot
+    return [f"s_mul_i32 s{S_SOFFU}, s{S_LDC2}, {8 * rg}",
+            f"buffer_load_dwordx4 {vr(va)}, v{V_RLA}, {sr(S_SRDC, 4)}, s{S_SOFFU} offen",
+            f"buffer_load_dwordx4 {vr(va + 4)}, v{V_RLG}, {sr(S_SRDC, 4)}, s{S_SOFFU} offen"]
+
+
+def ge_compute(rg, bank_base, slot):
+    """u = value * gelu(gate) for the 8 loaded elements (gelu_fast of csrc/kernels/common.h: A-S 7.1.26 erf),
+    packed over the value registers, then stored.  ~21 VALU per element; constants in s[S_GP..] / v[GE_C4]."""
+    va, ga = bank_base + 8 * slot, bank_base + 8 * slot + 4
+    g, v, t1, t2, t3, t4, ue = (GE_T + i for i in range(7))
+    c = GE_CONSTS
+    out = []
+    for k in range(8):
+        src_g, src_v = ga + (k >> 1), va + (k >> 1)
+        if k & 1:
+            out += [f"v_and_b32 v{g}, 0xffff0000, v{src_g}", f"v_and_b32 v{v}, 0xffff0000, v{src_v}"]
+        else:
+            out += [f"v_lshlrev_b32 v{g}, 16, v{src_g}", f"v_lshlrev_b32 v{v}, 16, v{src_v}"]
+        out += [f"v_mul_f32_e64 v{t1}, |v{g}|, s{S_RSQ2}",              # z = |x| / sqrt2
+                f"v_fma_f32 v{t1}, v{t1}, s{S_GP}, 1.0",
+                f"v_rcp_f32 v{t1}, v{t1}",                               # t
+                f"v_mul_f32 v{t3}, {c['nhl2e']:#x}, v{g}",
+                f"v_fma_f32 v{t2}, v{t1}, s{S_A5}, v{GE_C4}",            # (s_nop: t is a transcendental result)
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a3']:#x}",
+                f"v_mul_f32 v{t3}, v{t3}, v{g}",                         # -x^2 / 2 * log2 e
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a2']:#x}",
+                f"v_exp_f32 v{t3}, v{t3}",                               # exp(-x^2 / 2)
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a1']:#x}",
+                f"v_mul_f32 v{t2}, v{t2}, v{t1}",                        # poly
+                f"v_fma_f32 v{t4}, -v{t2}, v{t3}, 1.0",                  # |erf|
+                f"v_bfi_b32 v{t4}, s{S_MASK7}, v{t4}, v{g}",             # copysign(., x)
+                f"v_fma_f32 v{t4}, 0.5, v{t4}, 0.5",                     # cdf
+                f"v_mul_f32 v{t4}, v{g}, v{t4}",                         # gelu
+                f"v_mul_f32 v{t4}, v{v}, v{t4}"]                         # u
+        if k & 1:
+            out.append(f"v_cvt_pk_bf16_f32 v{va + (k >> 1)}, v{ue}, v{t4}")
+        else:
+            out.append(f"v_mov_b32 v{ue}, v{t4}")
+    out += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {8 * rg}",
+            f"buffer_store_dwordx4 {vr(va)}, v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
+    return fix_trans_hazards(out)
+
+
+def fix_trans_hazards(seq):
+    """gfx950: a VALU reading the result of a transcendental (v_rcp / v_exp) in the NEXT instruction needs one
+    wait state -- insert s_nop 0 only where the consumer immediately follows"""
+    out = []
+    for i, ins in enumerate(seq):
+        out.append(ins)
+        if ins.startswith(("v_rcp_f32", "v_exp_f32")) and i + 1 < len(seq):
+            dst = ins.split()[1].rstrip(",")
+            nxt = seq[i + 1]
+            if re.search(rf"\b{dst}\b", nxt.split(None, 1)[1] if " " in nxt else ""):
+                out.append("s_nop 0")
+    return out
+
+
+def geglu_lane_setup(e):
+    """per-lane bases of the geglu epilogue: `a` in the original column order, the u reload / store"""
+    T0, T1 = V_T, V_T + 1
+    # a: (128 wm + 4 g) ldc2 + (64 wn + 8 (c >> 1)) 2 + (c & 1) 2F
+    e(f"v_lshrrev_b32 v{T0}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 3, v{T0}")
+    e(f"v_lshlrev_b32 v{T0}, 2, v{T0}")
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")
+    e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
+    e(f"v_lshrrev_b32 v{T0}, 1, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 7, v{T0}")                      # c >> 1
+    e(f"v_lshlrev_b32 v{T0}, 4, v{T0}")                  # 8 (c >> 1) columns * 2 bytes
+    e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 7")                # 64 wn * 2 bytes
+    e(f"v_add_u32 v{T0}, s{S_T1}, v{T0}")
+    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T0}")
+    e(f"v_and_b32 v{T0}, 1, v{V_TID}")
+    e(f"v_mul_lo_u32 v{T0}, v{T0}, s{S_F2}")
+    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T0}")
+    # reload / u: lane (rr = (l >> 3) & 7, jc = l & 7): row 128 wm + rr, j 64 wn + 8 jc
+    e(f"v_lshrrev_b32 v{T0}, 3, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 7, v{T0}")
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")                # row
+    e(f"v_and_b32 v{T1}, 7, v{V_TID}")
+    e(f"v_lshlrev_b32 v{T1}, 4, v{T1}")                  # 8 jc * 2 bytes
+    e(f"v_add_u32 v{T1}, s{S_T1}, v{T1}")                # + 64 wn * 2
+    e(f"v_mul_lo_u32 v{V_RLA}, v{T0}, s{S_LDC2}")
+    e(f"v_add_u32 v{V_RLA}, v{V_RLA}, v{T1}")
+    e(f"v_add_u32 v{V_RLG}, s{S_F2}, v{V_RLA}")
+    e(f"v_mul_lo_u32 v{V_CU}, v{T0}, s{S_LDU2}")
+    e(f"v_add_u32 v{V_CU}, v{V_CU}, v{T1}")
+
+
+def setup_output_geglu(e):
+    """`a` resource of tile (S_ROW0, S_COL0): a + row0 ldc2 + col0 (the tile's F-columns start at col0 / 2);
+    u resource: u + row0 ldu2 + col0"""
+    for srd, ptr, ld2 in ((S_SRDC, S_C, S_LDC2), (S_SRDU, S_AUX1, S_LDU2)):
+        e(f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{ld2}")
+        e(f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{ld2}")
+        e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}")
+        e(f"s_addc_u32 s{S_T1}, s{S_T1}, 0")
+        e(f"s_add_u32 s{srd}, s{ptr}, s{S_T0}")
+        e(f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{S_T1}")
+        e(f"s_lshl_b32 s{srd + 2}, s{ld2}, 8")
+        e(f"s_mov_b32 s{srd + 3}, 0x20000")
+
+
+def ge_final_u(e):
+    """u of the last tile (no successor to hide it under): all 16 row-groups straight"""
+    e("s_waitcnt vmcnt(0)")
+    for rg in range(16):
+        bank = GE_BANK[rg & 1]
+        for ins in ge_loads(rg, bank, 0) + ["s_waitcnt vmcnt(0)"] + ge_compute(rg, bank, 0):
+            e(ins)
+
+
+def kernel_geglu(name, diag=None):
+    global STORE_POLICY
+    STORE_POLICY = ""          # `a` is re-read by the u pass: keep it in L2
+    e = Emitter(name)
+    e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")
+    e(f"s_load_dwordx2 {sr(S_AUX1, 2)}, s[0:1], 0x20")
+    e(f"s_load_dwordx8 {sr(S_M, 8)}, s[0:1], 0x30")
+    e(f"s_load_dword s{S_GRID}, s[0:1], 0x50")
+    e(f"s_load_dword s{S_LDU}, s[0:1], 0x54")
+    e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+    e("s_nop 1")
+    e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+    e("s_nop 1")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
+    e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
+    e(f"s_lshl_b32 s{S_LDU2}, s{S_LDU}, 1")
+    e(f"s_lshl_b32 s{S_F2}, s{S_LDU}, 1")               # 2 F bytes: the gate half of an `a` row (ld_aux = F)
+    e(f"s_mov_b32 s{S_GP}, 0x3ea7ba05")                  # 0.3275911
+    e(f"s_mov_b32 s{S_MASK7}, 0x7fffffff")
+    e(f"s_mov_b32 s{S_RSQ2}, {GE_CONSTS['c_rsqrt2']:#x}")
+    e(f"s_mov_b32 s{S_A5}, {GE_CONSTS['a5']:#x}")
+    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
+    e("s_cbranch_scc0 " + e.L("end"))
+    lane_setup(e, "bias")
+    geglu_lane_setup(e)
+    e(f"v_mov_b32 v{GE_C4}, {GE_CONSTS['a4']:#x}")
+    e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
+    e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
+    e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
+    e(f"s_lshr_b32 s{S_T1}, s{S_WG}, 3")
+    e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
+    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("end"))
+    tile_order_setup(e)
+    stagger_setup(e)
+    emit_all(e, tile_coords())
+    setup_operands(e)
+    prologue_dma(e)
+    e("s_waitcnt vmcnt(16)")
+    e("s_barrier")
+    extra = body_head(e, "bias", 0)
+    iteration(e, "first", None, extra)
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    e.label(e.L("kloop"))
+    iteration(e, "loop")
+    e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc0 " + e.L("kloop"))
+    e.label(e.L("tail"))
+    out = Emitter(e.prefix)
+    setup_output_geglu(out)
+    pre_out = [l.strip() for l in out.lines]
+    sub = Emitter(e.prefix)
+    setup_operands(sub)
+    pre_next = pre_out + next_tile() + [l.strip() for l in sub.lines]
+    e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
+    e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("final"))
+    iteration(e, "penult", None, prefetch=True, pre=pre_next)
+    iteration(e, "last", None, prefetch=True)
+    tile_boundary(e)
+    groups = epilogue_stash(e, "bias")
+    e(f"s_waitcnt vmcnt({16 + N_IMMEDIATE})")
+    e("s_barrier")
+    extra = body_head(e, "bias", N_IMMEDIATE)
+    # ---- the successor's K-steps 0 .. 13, unrolled: deferred `a` stores in 0..3, u of the finished tile in
+    #      3..13 (reloads one step ahead of their gelu) ----
+    k = 0
+    prev_vmem, prev_last_load = None, None
+    for t in range(14):
+        grp = []
+        if t < len(DEFER_SPLIT):
+            grp = groups[k:k + DEFER_SPLIT[t]]
+            k += DEFER_SPLIT[t]
+        work = []
+        load_rgs = GE_PLAN.get(t + 1, ()) if diag != "nowork" else ()
+        for slot_i, rg in enumerate(load_rgs):
+            work += ge_loads(rg, GE_BANK[(t + 1) % 2], slot_i)
+        for slot_i, rg in enumerate(GE_PLAN.get(t, ()) if diag != "nowork" else ()):
+            work += ge_compute(rg, GE_BANK[t % 2], slot_i)
+        head = []
+        if t in GE_PLAN and prev_vmem is not None and prev_last_load is not None:
+            # the loads issued in the previous step for this step's row-groups have landed
+            n_after = len(prev_vmem) - 1 - prev_last_load
+            head = [f"s_waitcnt vmcnt({n_after})"]
+        # step 1 only loads row-group 0, whose `a` chunks the boundary stored: complete once B3 of step 1 has
+        # waited for step 0's DMA (issued after them), so those loads go after B3
+        span = (B3_SLOT + 2, 118) if t == 1 else (36 if t < len(DEFER_SPLIT) else 1, 118)
+        vmem = iteration(e, "first" if t == 0 else "loop", None, extra if t == 0 else 0, stores=grp, head=head,
+                         work=work, work_span=span)
+        loads_idx = [i for i, ins in enumerate(vmem) if ins.startswith("buffer_load_dwordx4 v[")]
+        prev_vmem, prev_last_load = vmem, (loads_idx[-1] if loads_idx else None)
+        if load_rgs:
+            assert prev_last_load is not None
+    e("s_branch " + e.L("tail"))
+    e.label(e.L("final"))
+    iteration(e, "penult", None, pre=pre_out)
+    iteration(e, "last", None)
+    for _ in range(3):
+        e("s_nop 7")
+    epilogue_store(e, "bias")
+    if diag != "nowork":
+        ge_final_u(e)
+    e.label(e.L("end"))
+    e("s_waitcnt vmcnt(0)")
+    e("s_endpgm")
+    STORE_POLICY = " nt"
+    return e.text()
+
+
+KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None),
+           ("dalle_gemm_nt_geglu", "geglu", None)]
+DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")] + [
+    ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork")]
 
 
 def main(out, diag=False):
@@ -1055,7 +1328,7 @@ def main(out, diag=False):
     metas = []
     for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
-        parts.append(kernel_tn(name) if epi == "tn" else kernel(name, epi, dg))
+        parts.append(kernel_tn(name) if epi == "tn" else kernel_geglu(name, dg) if epi == "geglu" else kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
         parts.append(descriptor(name))
         metas.append(metadata(name))

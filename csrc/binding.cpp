@@ -522,6 +522,24 @@ void asm_wgrad_(Tensor out, Tensor A, Tensor B, int64_t splits, bool accumulate)
   dalle::splitk_accum(part.data_ptr<float>(), out.data_ptr<float>(), (long)M * N, (int)splits, accumulate ? 1 : 0, cur_stream());
 }
 
+// FF-in GEMM + GEGLU on the assembly kernel: x (M, 1024) bf16, w1p (2F, 1024) bf16 = W1 with its rows in the
+// interleaved [value 8 | gate 8] order (hip_ops.ff_in_perm), b1p (2F,) fp32 in the same order ->
+// a (M, 2F) bf16 pre-activation in the ORIGINAL [value | gate] order, u (M, F) = value * gelu(gate)
+std::vector<Tensor> asm_ff_in_geglu(Tensor x, Tensor w1p, Tensor b1p) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && w1p.scalar_type() == torch::kBFloat16, "asm_ff_in_geglu: bf16");
+  TORCH_CHECK(x.dim() == 2 && w1p.dim() == 2 && x.size(1) == w1p.size(1) && x.stride(1) == 1 && w1p.stride(1) == 1,
+              "asm_ff_in_geglu: x (M, K), w1p (2F, K), K-contiguous");
+  CHECK_IN(b1p, torch::kFloat32);
+  const int M = x.size(0), N = w1p.size(0), K = x.size(1);
+  TORCH_CHECK(K == 1024 && M % 256 == 0 && N % 256 == 0 && b1p.numel() == N, "asm_ff_in_geglu: K = 1024, M and 2F multiples of 256");
+  auto a = torch::empty({M, N}, x.options());
+  auto u = torch::empty({M, N / 2}, x.options());
+  TORCH_CHECK(dalle::asm_gemm_nt("dalle_gemm_nt_geglu", x.data_ptr(), w1p.data_ptr(), a.data_ptr(), b1p.data_ptr(), u.data_ptr(), nullptr,
+                                 M, N, K, (int)x.stride(0), (int)w1p.stride(0), N, N / 2, 0, cur_stream()),
+              "asm_ff_in_geglu: launch failed");
+  return {a, u};
+}
+
 Tensor asm_gemm(Tensor A, Tensor B, c10::optional<Tensor> bias, c10::optional<Tensor> out) {
   TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "asm_gemm: bf16 cuda");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "asm_gemm: A (M, K) and B (N, K)");
@@ -1249,6 +1267,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
   m.def("asm_gemm", &asm_gemm, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out") = py::none());
+  m.def("asm_ff_in_geglu", &asm_ff_in_geglu, py::arg("x"), py::arg("w1p"), py::arg("b1p"));
   m.def("asm_wgrad_", &asm_wgrad_, py::arg("out"), py::arg("A"), py::arg("B"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
   m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),

@@ -125,6 +125,38 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None)
     return torch.mm(a, b.t())
 
 
+_perms: Dict[tuple, torch.Tensor] = {}
+
+
+def ff_in_perm(F: int, device) -> torch.Tensor:
+    """Row order of W1 (and b1) for the fused FF-in + GEGLU kernel: 8-row blocks [value j..j+7 | gate j..j+7],
+    so each lane of the GEMM holds a value block or its gate block (csrc/asm/gen_gemm.py kernel_geglu)."""
+    key = (F, str(device))
+    p = _perms.get(key)
+    if p is None:
+        n = torch.arange(2 * F, device=device)
+        b, e = n // 16, n % 16
+        p = torch.where(e < 8, 8 * b + e, F + 8 * b + e - 8)
+        _perms[key] = p
+    return p
+
+
+def _ff_in_geglu_ok(h2: torch.Tensor, w1: torch.Tensor) -> bool:
+    return (ASM_GEMM and h2.is_cuda and h2.dtype == torch.bfloat16 and h2.dim() == 2 and h2.stride(1) == 1
+            and h2.shape[1] == 1024 and h2.shape[0] % 256 == 0 and w1.shape[0] % 256 == 0 and w1.shape[1] == 1024)
+
+
+def ff_in_geglu(h2: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
+    """(a, u) = (h2 W1^T + b1, GEGLU(a)) in one assembly kernel (u computed from the stored bf16 a, as the
+    separate geglu kernel would); W1 / b1 are permuted once per forward (cached like the bf16 casts)."""
+    F = w1.shape[0] // 2
+    perm = ff_in_perm(F, w1.device)
+    w1p = _cached(("ffw", id(w1)), w1, lambda: bf16_weight(w1).index_select(0, perm).contiguous())
+    b1p = _cached(("ffb", id(b1)), b1, lambda: b1.detach().float().index_select(0, perm).contiguous())
+    _count("asm_ff_in_geglu")
+    return C().asm_ff_in_geglu(h2, w1p, b1p)
+
+
 def input_grad(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = g W for a Linear weight W (out, in), computed as g . (W^T)^T from the cached transposed bf16
     copy: the NT form of the product (hipBLASLt also runs it 12-20 % faster than the NN form at every
@@ -617,8 +649,11 @@ def _ff_core_fwd(inp, h, mean, rstd, w1, b1, w2, b2, scale, meta, save: bool = T
     d = inp.shape[-1]
     h2 = h.view(-1, d)
     w1b, w2b = bf16_weight(w1), bf16_weight(w2)
-    a = mm_nt(h2, w1b, b1)
-    u = C().geglu_fwd(a)
+    if b1 is not None and _ff_in_geglu_ok(h2, w1):
+        a, u = ff_in_geglu(h2, w1, b1)
+    else:
+        a = mm_nt(h2, w1b, b1)
+        u = C().geglu_fwd(a)
     if not save:
         del a
     y = mm_nt(u, w2b, b2)

@@ -83,3 +83,22 @@ def test_weight_grad_routes_to_asm(cuda, C):
     ref = g.float().t() @ x.float()
     assert ((w.grad - ref).abs().max() / ref.abs().max()).item() < 1e-4
     assert hip_ops.PATH_COUNTS.get("asm_wgrad", 0) == before + 1
+
+
+@pytest.mark.parametrize("M,F", [(512, 1024), (10240, 4096), (2560, 512)])
+def test_asm_ff_in_geglu(cuda, C, M, F):
+    """FF-in GEMM + GEGLU in one assembly kernel (permuted W1 rows, u from the stored bf16 pre-activation,
+    deferred under the next tile's K-steps): a vs fp32 x W1^T + b1, u vs the unfused GEGLU of that a."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(M + F)
+    x = torch.randn(M, 1024, device=cuda).to(torch.bfloat16)
+    w1 = torch.randn(2 * F, 1024, device=cuda) * 0.03
+    b1 = torch.randn(2 * F, device=cuda) * 0.1
+    a, u = hip_ops.ff_in_geglu(x, w1, b1)
+    ref_a = x.float() @ w1.to(torch.bfloat16).float().t() + b1
+    assert ((a.float() - ref_a).abs().max() / ref_a.abs().max()).item() < 8e-3
+    af = a.float()
+    ref_u = af[:, :F] * torch.nn.functional.gelu(af[:, F:])
+    assert ((u.float() - ref_u).abs().max() / ref_u.abs().max()).item() < 8e-3
+    assert torch.equal(u, C.geglu_fwd(a)) or ((u.float() - C.geglu_fwd(a).float()).abs().max() <= 2 ** -6 * ref_u.abs().max())
