@@ -148,6 +148,7 @@ def bench_geglu(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
            "asm_geglu": lambda: mod.launch("dalle_gemm_nt_geglu", grid, args)}
     if diag is not None:
         fns["asm_geglu_nowork"] = lambda: diag.launch("dalle_gemm_diag_geglu_nowork", grid, args)
+
     for f in fns.values():
         f()
     torch.cuda.synchronize()

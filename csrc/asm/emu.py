@@ -375,9 +375,9 @@ class Workgroup:
                 data = self.mem.read(base + soff + int(voff[l]) + imm, 16).view(np.uint32)
                 w.v[dst:dst + 4, l] = data
             return None
-        if op in ("buffer_store_dword", "buffer_store_dwordx4"):
+        if op in ("buffer_store_dword", "buffer_store_dwordx2", "buffer_store_dwordx4"):
             src, n = reg_range(t[0])
-            n = 4 if op.endswith("x4") else 1
+            n = {"buffer_store_dword": 1, "buffer_store_dwordx2": 2, "buffer_store_dwordx4": 4}[op]
             voff = w.v[int(t[1][1:])].astype(np.int64)
             base, nr = self.srd(w, t[2])
             soff = self.sval(w, t[3])
@@ -467,10 +467,9 @@ def selftest(asm_path):
 
 
 def ff_in_perm(F):
-    """interleaved row order of W1 for the geglu kernel: [value 8 | gate 8] blocks"""
+    """interleaved row order of W1 for the geglu kernel: [value 4 | gate 4] blocks"""
     n = np.arange(2 * F)
-    b, e = n // 16, n % 16
-    return np.where(e < 8, 8 * b + e, F + 8 * b + e - 8)
+    return 4 * (n >> 3) + (n & 3) + ((n >> 2) & 1) * F
 
 
 def gelu_ref(x):

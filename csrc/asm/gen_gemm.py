@@ -68,7 +68,7 @@ S_TM, S_TNI = 67, 68  # tile row / column index
 S_G8, S_MAGG, S_FULL, S_TMFULL, S_ROWREM, S_MAGR = 69, 70, 71, 76, 77, 78
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
 S_KV, S_WRAP, S_S0B = 79, 80, 81   # K-slice of the next DMA, 128 - 2 K (the wrap step), first slice * 128
-S_LAST = 98
+S_LAST = 96
 
 # VGPRs
 V_TID = 0
@@ -1061,75 +1061,23 @@ def kernel_tn(name):
 
 # ----------------------------------------------------------------------------------------------------
 # FF-in GEMM + GEGLU forward: a = x W1^T + b1 (M x 2F, [value | gate] column order) and u = value * gelu(gate)
-# (M x F).  The B operand is W1 with its rows interleaved in 8-row blocks [value j0..j0+7 | gate j0..j0+7 | ..]
-# (host: ff_in_perm), so lane c of a wave half holds a value block (c even) or the matching gate block (c odd);
-# the epilogue writes `a` back in the ORIGINAL column order (value j -> column j, gate j -> F + j: a per-lane
-# base, whole 16-byte chunks), deferred like the plain kernel.  u is computed from the stored (bf16) `a` --
-# the numbers the unfused geglu kernel reads -- during the NEXT tile's K-steps 3..13: each wave reloads the
-# value / gate chunks of its own rows and columns (L2-hot, written one to three steps earlier by the same
-# wave), one K-step ahead, and its gelu VALU fills the MFMA gaps.  Needs kt = 16 (K = 1024; the host checks):
-# the K-loop of a successor tile is fully unrolled so the deferred work can be placed statically.
+# (M x F).  The B operand is W1 with its rows interleaved in 4-row blocks [value j..j+3 | gate j..j+3] (host:
+# ff_in_perm), so each lane's 8 columns of a row are the values AND the gates of 4 consecutive j: the lane
+# writes `a` back in the ORIGINAL column order as two 8-byte chunks (value j / gate F + j: 16 lanes = one whole
+# 128-byte line each) and computes its 4 u from the same registers -- no exchange, no reload.  Both are deferred
+# like the plain kernel's stores: the packed bf16 row-groups (the numbers the unfused geglu kernel would read)
+# wait in v[144:247] while the successor tile's K-steps 0..13 (unrolled: needs kt = 16, K = 1024; the host
+# checks) store them and spread the gelu VALU over their MFMA gaps.  The tile's bias is loaded during its last
+# K-step, so v[248:255] serve as the gelu temps meanwhile.
 # ----------------------------------------------------------------------------------------------------
 S_SRDU = 84          # u resource (4)
-S_SOFFU, S_SOFFV, S_GP, S_MASK7, S_F2, S_LDU2 = 88, 89, 90, 91, 92, 93
-S_RSQ2, S_A5 = 94, 95
-GE_C4 = 10           # v10: the a4 coefficient (a lane constant; v10 is a setup temp only)
+S_SOFFV, S_GP, S_MASK7, S_F2, S_LDU2, S_RSQ2 = 88, 89, 90, 91, 92, 93
 S_AUX1, S_LDU = 22, 21
-V_RLA, V_CU, V_RLG = 13, 14, 15
-GE_BANK = (144, 160)     # reload banks (2 row-groups x [value 4 | gate 4] each)
-GE_T = 176               # gelu temps v176..v182
-# u row-groups computed per K-step (loaded one step earlier): row-group rg needs the `a` chunks 4 (rg >> 1) ..
-# +3, stored at the boundary (< 6) or in steps 0..3 (DEFER_SPLIT), and a store is complete two steps later
-GE_PLAN = {2: (0,), 3: (1, 2), 4: (3,), 5: (4,), 6: (5, 6), 7: (7,), 8: (8,), 9: (9, 10), 10: (11,), 11: (12,),
-           12: (13, 14), 13: (15,)}
+V_CU, V_COG = 13, 14                 # u store base, `a` gate-chunk base (value base: V_CO)
+GE_T = V_BIAS                        # gelu temps v248..v254 (the packed u goes over the row-group's values)
+GE_SPLIT = [2] * 12 + [1, 1]         # deferred row-groups' u per successor K-step 0..13 (26)
 GE_CONSTS = {"c_rsqrt2": 0x3F3504F3, "a5": 0x3F87DC22, "a4": 0xBFBA00E3, "a3": 0x3FB5F0E3, "a2": 0xBE91A98E,
              "a1": 0x3E827906, "nhl2e": 0xBF38AA3B}
-
-
-def ge_loads(rg, bank_base, slot):
-    """value / gate chunks of u row-group rg (rows 8 rg .. +7 of the wave, 8 j per lane) into a bank slot"""
-    va = bank_base + 8 * slot
-    return [f"s_mul_i32 s{S_SOFFU}, s{S_LDC2}, {8 * rg}",
-            f"buffer_load_dwordx4 {vr(va)}, v{V_RLA}, {sr(S_SRDC, 4)}, s{S_SOFFU} offen",
-            f"buffer_load_dwordx4 {vr(va + 4)}, v{V_RLG}, {sr(S_SRDC, 4)}, s{S_SOFFU} offen"]
-
-
-def ge_compute(rg, bank_base, slot):
-    """u = value * gelu(gate) for the 8 loaded elements (gelu_fast of csrc/kernels/common.h: A-S 7.1.26 erf),
-    packed over the value registers, then stored.  ~21 VALU per element; constants in s[S_GP..] / v[GE_C4]."""
-    va, ga = bank_base + 8 * slot, bank_base + 8 * slot + 4
-    g, v, t1, t2, t3, t4, ue = (GE_T + i for i in range(7))
-    c = GE_CONSTS
-    out = []
-    for k in range(8):
-        src_g, src_v = ga + (k >> 1), va + (k >> 1)
-        if k & 1:
-            out += [f"v_and_b32 v{g}, 0xffff0000, v{src_g}", f"v_and_b32 v{v}, 0xffff0000, v{src_v}"]
-        else:
-            out += [f"v_lshlrev_b32 v{g}, 16, v{src_g}", f"v_lshlrev_b32 v{v}, 16, v{src_v}"]
-        out += [f"v_mul_f32_e64 v{t1}, |v{g}|, s{S_RSQ2}",              # z = |x| / sqrt2
-                f"v_fma_f32 v{t1}, v{t1}, s{S_GP}, 1.0",
-                f"v_rcp_f32 v{t1}, v{t1}",                               # t
-                f"v_mul_f32 v{t3}, {c['nhl2e']:#x}, v{g}",
-                f"v_fma_f32 v{t2}, v{t1}, s{S_A5}, v{GE_C4}",            # (s_nop: t is a transcendental result)
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a3']:#x}",
-                f"v_mul_f32 v{t3}, v{t3}, v{g}",                         # -x^2 / 2 * log2 e
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a2']:#x}",
-                f"v_exp_f32 v{t3}, v{t3}",                               # exp(-x^2 / 2)
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a1']:#x}",
-                f"v_mul_f32 v{t2}, v{t2}, v{t1}",                        # poly
-                f"v_fma_f32 v{t4}, -v{t2}, v{t3}, 1.0",                  # |erf|
-                f"v_bfi_b32 v{t4}, s{S_MASK7}, v{t4}, v{g}",             # copysign(., x)
-                f"v_fma_f32 v{t4}, 0.5, v{t4}, 0.5",                     # cdf
-                f"v_mul_f32 v{t4}, v{g}, v{t4}",                         # gelu
-                f"v_mul_f32 v{t4}, v{v}, v{t4}"]                         # u
-        if k & 1:
-            out.append(f"v_cvt_pk_bf16_f32 v{va + (k >> 1)}, v{ue}, v{t4}")
-        else:
-            out.append(f"v_mov_b32 v{ue}, v{t4}")
-    out += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {8 * rg}",
-            f"buffer_store_dwordx4 {vr(va)}, v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
-    return fix_trans_hazards(out)
 
 
 def fix_trans_hazards(seq):
@@ -1146,69 +1094,93 @@ def fix_trans_hazards(seq):
     return out
 
 
-def geglu_lane_setup(e):
-    """per-lane bases of the geglu epilogue: `a` in the original column order, the u reload / store"""
+def ge_u(src, temps, uout):
+    """u for the lane's 4 j from the packed row-group v[src..src+3] = [v0v1, v2v3, g0g1, g2g3]:
+    value * gelu(gate) (gelu_fast of csrc/kernels/common.h: A-S 7.1.26 erf), packed into uout[0], uout[1]"""
+    g, v, t1, t2, t3, t4, ue = temps
+    c = GE_CONSTS
+    out = []
+    for k in range(4):
+        rv, rg_ = src + (k >> 1), src + 2 + (k >> 1)
+        if k & 1:
+            out += [f"v_and_b32 v{g}, 0xffff0000, v{rg_}", f"v_and_b32 v{v}, 0xffff0000, v{rv}"]
+        else:
+            out += [f"v_lshlrev_b32 v{g}, 16, v{rg_}", f"v_lshlrev_b32 v{v}, 16, v{rv}"]
+        out += [f"v_mul_f32_e64 v{t1}, |v{g}|, s{S_RSQ2}",              # z = |x| / sqrt2
+                f"v_fma_f32 v{t1}, v{t1}, s{S_GP}, 1.0",
+                f"v_rcp_f32 v{t1}, v{t1}",                               # t
+                f"v_mul_f32 v{t3}, {c['nhl2e']:#x}, v{g}",
+                f"v_mul_f32 v{t2}, {c['a5']:#x}, v{t1}",
+                f"v_add_f32 v{t2}, {c['a4']:#x}, v{t2}",
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a3']:#x}",
+                f"v_mul_f32 v{t3}, v{t3}, v{g}",                         # -x^2 / 2 * log2 e
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a2']:#x}",
+                f"v_exp_f32 v{t3}, v{t3}",                               # exp(-x^2 / 2)
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a1']:#x}",
+                f"v_mul_f32 v{t2}, v{t2}, v{t1}",                        # poly
+                f"v_fma_f32 v{t4}, -v{t2}, v{t3}, 1.0",                  # |erf|
+                f"v_bfi_b32 v{t4}, s{S_MASK7}, v{t4}, v{g}",             # copysign(., x)
+                f"v_fma_f32 v{t4}, 0.5, v{t4}, 0.5",                     # cdf
+                f"v_mul_f32 v{t4}, v{g}, v{t4}",                         # gelu
+                f"v_mul_f32 v{t4}, v{v}, v{t4}"]                         # u
+        if k & 1:
+            out.append(f"v_cvt_pk_bf16_f32 v{uout[k >> 1]}, v{ue}, v{t4}")
+        else:
+            out.append(f"v_mov_b32 v{ue}, v{t4}")
+    return fix_trans_hazards(out)
+
+
+def ge_stores_a(i, r, src):
+    """the row-group's value chunk (v[src:src+1]) and gate chunk (v[src+2:src+3]) of `a`"""
+    return [f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}",
+            f"buffer_store_dwordx2 v[{src}:{src + 1}], v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen",
+            f"buffer_store_dwordx2 v[{src + 2}:{src + 3}], v{V_COG}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen"]
+
+
+def geglu_lane_setup(e, diag=None):
+    """per-lane bases of the geglu epilogue: `a` value / gate chunks in the original column order, u"""
     T0, T1 = V_T, V_T + 1
-    # a: (128 wm + 4 g) ldc2 + (64 wn + 8 (c >> 1)) 2 + (c & 1) 2F
+    # rows 128 wm + 4 g; value j = 64 wn + 4 c  (c = lane & 15)
     e(f"v_lshrrev_b32 v{T0}, 4, v{V_TID}")
     e(f"v_and_b32 v{T0}, 3, v{T0}")
     e(f"v_lshlrev_b32 v{T0}, 2, v{T0}")
     e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
     e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
-    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")
-    e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
-    e(f"v_lshrrev_b32 v{T0}, 1, v{V_TID}")
-    e(f"v_and_b32 v{T0}, 7, v{T0}")                      # c >> 1
-    e(f"v_lshlrev_b32 v{T0}, 4, v{T0}")                  # 8 (c >> 1) columns * 2 bytes
+    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")                # row
+    e(f"v_and_b32 v{T1}, 15, v{V_TID}")
+    e(f"v_lshlrev_b32 v{T1}, 3, v{T1}")                  # 4 c columns * 2 bytes
     e(f"s_and_b32 s{S_T1}, s{S_WAVE}, 1")
     e(f"s_lshl_b32 s{S_T1}, s{S_T1}, 7")                # 64 wn * 2 bytes
-    e(f"v_add_u32 v{T0}, s{S_T1}, v{T0}")
-    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T0}")
-    e(f"v_and_b32 v{T0}, 1, v{V_TID}")
-    e(f"v_mul_lo_u32 v{T0}, v{T0}, s{S_F2}")
-    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T0}")
-    # reload / u: lane (rr = (l >> 3) & 7, jc = l & 7): row 128 wm + rr, j 64 wn + 8 jc
-    e(f"v_lshrrev_b32 v{T0}, 3, v{V_TID}")
-    e(f"v_and_b32 v{T0}, 7, v{T0}")
-    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
-    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
-    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")                # row
-    e(f"v_and_b32 v{T1}, 7, v{V_TID}")
-    e(f"v_lshlrev_b32 v{T1}, 4, v{T1}")                  # 8 jc * 2 bytes
-    e(f"v_add_u32 v{T1}, s{S_T1}, v{T1}")                # + 64 wn * 2
-    e(f"v_mul_lo_u32 v{V_RLA}, v{T0}, s{S_LDC2}")
-    e(f"v_add_u32 v{V_RLA}, v{V_RLA}, v{T1}")
-    e(f"v_add_u32 v{V_RLG}, s{S_F2}, v{V_RLA}")
+    e(f"v_add_u32 v{T1}, s{S_T1}, v{T1}")
+    e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
+    e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T1}")
+    e(f"v_add_u32 v{V_COG}, s{S_F2}, v{V_CO}")
     e(f"v_mul_lo_u32 v{V_CU}, v{T0}, s{S_LDU2}")
     e(f"v_add_u32 v{V_CU}, v{V_CU}, v{T1}")
 
 
-def setup_output_geglu(e):
-    """`a` resource of tile (S_ROW0, S_COL0): a + row0 ldc2 + col0 (the tile's F-columns start at col0 / 2);
-    u resource: u + row0 ldu2 + col0"""
+def setup_output_geglu():
+    """(in penult's MFMA gaps) `a` resource of the finishing tile (S_ROW0, S_COL0): a + row0 ldc2 + col0 (its
+    F-columns start at col0 / 2), u resource u + row0 ldu2 + col0, bias resource aux0 + col0 * 4"""
+    out = []
     for srd, ptr, ld2 in ((S_SRDC, S_C, S_LDC2), (S_SRDU, S_AUX1, S_LDU2)):
-        e(f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{ld2}")
-        e(f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{ld2}")
-        e(f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}")
-        e(f"s_addc_u32 s{S_T1}, s{S_T1}, 0")
-        e(f"s_add_u32 s{srd}, s{ptr}, s{S_T0}")
-        e(f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{S_T1}")
-        e(f"s_lshl_b32 s{srd + 2}, s{ld2}, 8")
-        e(f"s_mov_b32 s{srd + 3}, 0x20000")
+        out += [f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{ld2}", f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{ld2}",
+                f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}", f"s_addc_u32 s{S_T1}, s{S_T1}, 0",
+                f"s_add_u32 s{srd}, s{ptr}, s{S_T0}", f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{S_T1}",
+                f"s_lshl_b32 s{srd + 2}, s{ld2}, 8", f"s_mov_b32 s{srd + 3}, 0x20000"]
+    out += [f"s_lshl_b32 s{S_T0}, s{S_COL0}, 2", f"s_add_u32 s{S_SRDX}, s{S_AUX0}, s{S_T0}",
+            f"s_addc_u32 s{S_SRDX + 1}, s{S_AUX0 + 1}, 0", f"s_mov_b32 s{S_SRDX + 2}, 1024",
+            f"s_mov_b32 s{S_SRDX + 3}, 0x20000"]
+    return out
 
 
-def ge_final_u(e):
-    """u of the last tile (no successor to hide it under): all 16 row-groups straight"""
-    e("s_waitcnt vmcnt(0)")
-    for rg in range(16):
-        bank = GE_BANK[rg & 1]
-        for ins in ge_loads(rg, bank, 0) + ["s_waitcnt vmcnt(0)"] + ge_compute(rg, bank, 0):
-            e(ins)
+BIAS_LOADS = [f"buffer_load_dwordx4 {vr(V_BIAS)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen",
+              f"buffer_load_dwordx4 {vr(V_BIAS + 4)}, v{V_BOFF}, {sr(S_SRDX, 4)}, 0 offen offset:16"]
 
 
 def kernel_geglu(name, diag=None):
     global STORE_POLICY
-    STORE_POLICY = ""          # `a` is re-read by the u pass: keep it in L2
+    STORE_POLICY = ""
     e = Emitter(name)
     e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")
     e(f"s_load_dwordx2 {sr(S_AUX1, 2)}, s[0:1], 0x20")
@@ -1227,12 +1199,10 @@ def kernel_geglu(name, diag=None):
     e(f"s_mov_b32 s{S_GP}, 0x3ea7ba05")                  # 0.3275911
     e(f"s_mov_b32 s{S_MASK7}, 0x7fffffff")
     e(f"s_mov_b32 s{S_RSQ2}, {GE_CONSTS['c_rsqrt2']:#x}")
-    e(f"s_mov_b32 s{S_A5}, {GE_CONSTS['a5']:#x}")
     e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
     e("s_cbranch_scc0 " + e.L("end"))
     lane_setup(e, "bias")
-    geglu_lane_setup(e)
-    e(f"v_mov_b32 v{GE_C4}, {GE_CONSTS['a4']:#x}")
+    geglu_lane_setup(e, diag)
     e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
     e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
     e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
@@ -1247,8 +1217,8 @@ def kernel_geglu(name, diag=None):
     prologue_dma(e)
     e("s_waitcnt vmcnt(16)")
     e("s_barrier")
-    extra = body_head(e, "bias", 0)
-    iteration(e, "first", None, extra)
+    body_head(e, "plain", 0)
+    iteration(e, "first", None, 0)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
     e.label(e.L("kloop"))
     iteration(e, "loop")
@@ -1256,9 +1226,7 @@ def kernel_geglu(name, diag=None):
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc0 " + e.L("kloop"))
     e.label(e.L("tail"))
-    out = Emitter(e.prefix)
-    setup_output_geglu(out)
-    pre_out = [l.strip() for l in out.lines]
+    pre_out = setup_output_geglu()
     sub = Emitter(e.prefix)
     setup_operands(sub)
     pre_next = pre_out + next_tile() + [l.strip() for l in sub.lines]
@@ -1266,50 +1234,69 @@ def kernel_geglu(name, diag=None):
     e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("final"))
     iteration(e, "penult", None, prefetch=True, pre=pre_next)
-    iteration(e, "last", None, prefetch=True)
+    vm = iteration(e, "last", None, prefetch=True, work=BIAS_LOADS, work_span=(1, 4))
+    after_bias = len(vm) - 1 - max(i for i, ins in enumerate(vm) if ins in BIAS_LOADS)
+    e(f"s_waitcnt vmcnt({after_bias})")                  # this tile's bias is in
     tile_boundary(e)
-    groups = epilogue_stash(e, "bias")
-    e(f"s_waitcnt vmcnt({16 + N_IMMEDIATE})")
+    # ---- boundary: pack every row-group (+ bias); the first N_IMMEDIATE stored and their u computed now ----
+    stash = []
+    n_imm_vmem = 0
+    for idx in range(32):
+        i, r = divmod(idx, 4)
+        t = V_ETMP + (idx % 4) * 12
+        if idx < N_IMMEDIATE:
+            pack_row(e, "bias", i, r, t, t + 8)
+            seq = ge_stores_a(i, r, t + 8)
+            if diag != "nowork":
+                seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
+                seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
+                        f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
+            emit_all(e, seq)
+            n_imm_vmem += sum(1 for x in seq if x.startswith("buffer_"))
+        else:
+            dst = V_STASH + 4 * (idx - N_IMMEDIATE)
+            pack_row(e, "bias", i, r, t, dst)
+            stash.append((i, r, dst))
+    e(f"s_waitcnt vmcnt({16 + n_imm_vmem})")             # the successor's step 0 landed
     e("s_barrier")
-    extra = body_head(e, "bias", N_IMMEDIATE)
-    # ---- the successor's K-steps 0 .. 13, unrolled: deferred `a` stores in 0..3, u of the finished tile in
-    #      3..13 (reloads one step ahead of their gelu) ----
-    k = 0
-    prev_vmem, prev_last_load = None, None
+    body_head(e, "plain", 0)
+    # ---- successor K-steps 0 .. 13, unrolled: `a` stores of the stashed row-groups in steps 0..3, their u
+    #      (gelu VALU + store) in steps 0..13 ----
+    ui = 0
+    per_step_a = [7, 7, 6, 6]
+    ai = 0
     for t in range(14):
-        grp = []
-        if t < len(DEFER_SPLIT):
-            grp = groups[k:k + DEFER_SPLIT[t]]
-            k += DEFER_SPLIT[t]
         work = []
-        load_rgs = GE_PLAN.get(t + 1, ()) if diag != "nowork" else ()
-        for slot_i, rg in enumerate(load_rgs):
-            work += ge_loads(rg, GE_BANK[(t + 1) % 2], slot_i)
-        for slot_i, rg in enumerate(GE_PLAN.get(t, ()) if diag != "nowork" else ()):
-            work += ge_compute(rg, GE_BANK[t % 2], slot_i)
-        head = []
-        if t in GE_PLAN and prev_vmem is not None and prev_last_load is not None:
-            # the loads issued in the previous step for this step's row-groups have landed
-            n_after = len(prev_vmem) - 1 - prev_last_load
-            head = [f"s_waitcnt vmcnt({n_after})"]
-        # step 1 only loads row-group 0, whose `a` chunks the boundary stored: complete once B3 of step 1 has
-        # waited for step 0's DMA (issued after them), so those loads go after B3
-        span = (B3_SLOT + 2, 118) if t == 1 else (36 if t < len(DEFER_SPLIT) else 1, 118)
-        vmem = iteration(e, "first" if t == 0 else "loop", None, extra if t == 0 else 0, stores=grp, head=head,
-                         work=work, work_span=span)
-        loads_idx = [i for i, ins in enumerate(vmem) if ins.startswith("buffer_load_dwordx4 v[")]
-        prev_vmem, prev_last_load = vmem, (loads_idx[-1] if loads_idx else None)
-        if load_rgs:
-            assert prev_last_load is not None
+        if t < 4:
+            for (i, r, src) in stash[ai:ai + per_step_a[t]]:
+                work += ge_stores_a(i, r, src)
+            ai += per_step_a[t]
+        if diag != "nowork":
+            for (i, r, src) in stash[ui:ui + GE_SPLIT[t]]:
+                # (its `a` chunks were stored in this or an earlier step: the values may be overwritten)
+                work += ge_u(src, tuple(GE_T + q for q in range(7)), (src, src + 1))
+                work += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
+                         f"buffer_store_dwordx2 v[{src}:{src + 1}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
+            ui += GE_SPLIT[t]
+        iteration(e, "first" if t == 0 else "loop", None, n_imm_vmem if t == 0 else 0, work=work,
+                  work_span=(1, 118))
     e("s_branch " + e.L("tail"))
     e.label(e.L("final"))
     iteration(e, "penult", None, pre=pre_out)
-    iteration(e, "last", None)
+    vm = iteration(e, "last", None, work=BIAS_LOADS, work_span=(1, 4))
+    e("s_waitcnt vmcnt(0)")
     for _ in range(3):
         e("s_nop 7")
-    epilogue_store(e, "bias")
-    if diag != "nowork":
-        ge_final_u(e)
+    for idx in range(32):
+        i, r = divmod(idx, 4)
+        t = V_EPI + (idx % 4) * 12
+        pack_row(e, "bias", i, r, t, t + 8)
+        seq = ge_stores_a(i, r, t + 8)
+        if diag != "nowork":
+            seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
+            seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
+                    f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
+        emit_all(e, seq)
     e.label(e.L("end"))
     e("s_waitcnt vmcnt(0)")
     e("s_endpgm")

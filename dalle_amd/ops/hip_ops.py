@@ -129,14 +129,13 @@ _perms: Dict[tuple, torch.Tensor] = {}
 
 
 def ff_in_perm(F: int, device) -> torch.Tensor:
-    """Row order of W1 (and b1) for the fused FF-in + GEGLU kernel: 8-row blocks [value j..j+7 | gate j..j+7],
-    so each lane of the GEMM holds a value block or its gate block (csrc/asm/gen_gemm.py kernel_geglu)."""
+    """Row order of W1 (and b1) for the fused FF-in + GEGLU kernel: 4-row blocks [value j..j+3 | gate j..j+3],
+    so each lane's 8 output columns are the values and gates of 4 j (csrc/asm/gen_gemm.py kernel_geglu)."""
     key = (F, str(device))
     p = _perms.get(key)
     if p is None:
         n = torch.arange(2 * F, device=device)
-        b, e = n // 16, n % 16
-        p = torch.where(e < 8, 8 * b + e, F + 8 * b + e - 8)
+        p = 4 * (n >> 3) + (n & 3) + ((n >> 2) & 1) * F
         _perms[key] = p
     return p
 
