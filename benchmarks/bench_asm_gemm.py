@@ -57,7 +57,7 @@ def gemm_args(A, B, C, aux0=None, grid=256):
     nt = (M // 256) * tiles_n
     ptrs = [A.data_ptr(), B.data_ptr(), C.data_ptr(), aux0.data_ptr() if aux0 is not None else 0, 0, 0]
     ints = [M, N, K, A.stride(0), B.stride(0), C.stride(0), tiles_n, nt, grid, 0, 0, 0]
-    return struct.pack("<6Q12i", *ptrs, *ints)
+    return struct.pack("<6Q16i", *ptrs, *ints, 0, 0, 0, 0)
 
 
 def run(mod, name, A, B, C, aux0=None, grid=None):
@@ -74,7 +74,7 @@ def tn_args(A, B, part, splits):
     units = (M // 256) * (N // 256) * splits
     ptrs = [A.data_ptr(), B.data_ptr(), part.data_ptr(), 0, 0, 0]
     ints = [M, N, Ktot // splits, A.stride(0), B.stride(0), N, N // 256, units, units, 0, 0, 0]
-    return units, struct.pack("<6Q12i", *ptrs, *ints)
+    return units, struct.pack("<6Q16i", *ptrs, *ints, 0, 0, 0, 0)
 
 
 def run_tn(mod, A, B, part, splits):
@@ -143,11 +143,12 @@ def bench_geglu(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
     grid = min(256, (nt + 7) // 8 * 8)
     ptrs = [x.data_ptr(), w.data_ptr(), a.data_ptr(), b.data_ptr(), u.data_ptr(), 0]
     ints = [M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0]
-    args = struct.pack("<6Q12i", *ptrs, *ints)
+    args = struct.pack("<6Q16i", *ptrs, *ints, 0, 0, 0, 0)
     fns = {"asm_bias": lambda: mod.launch("dalle_gemm_nt_bias", grid, args),
            "asm_geglu": lambda: mod.launch("dalle_gemm_nt_geglu", grid, args)}
     if diag is not None:
         fns["asm_geglu_nowork"] = lambda: diag.launch("dalle_gemm_diag_geglu_nowork", grid, args)
+        fns["asm_geglu_adjacent"] = lambda: diag.launch("dalle_gemm_diag_geglu_adjacent", grid, args)
 
     for f in fns.values():
         f()

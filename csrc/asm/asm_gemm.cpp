@@ -43,7 +43,7 @@ hipFunction_t get_function(const char* name) {
   return f;
 }
 
-// kernel argument block (must match gen_gemm.py: 6 pointers then 12 int32)
+// kernel argument block (must match gen_gemm.py: 6 pointers then 16 int32)
 struct alignas(8) GemmArgs {
   const void* a;
   const void* b;
@@ -52,8 +52,9 @@ struct alignas(8) GemmArgs {
   const void* aux1;
   const void* aux2;
   int32_t m, n, k, lda, ldb, ldc, tiles_n, num_tiles, grid, ld_aux, flags, pad;
+  int32_t e0, e1, e2, e3;  // kernel-specific (the QKV + rotary kernel's attention geometry)
 };
-static_assert(sizeof(GemmArgs) == 96, "kernarg block size");
+static_assert(sizeof(GemmArgs) == 112, "kernarg block size");
 
 int g_num_cus = 0;
 
@@ -83,6 +84,23 @@ bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, cons
   size_t size = sizeof(args);
   void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
   hipFunction_t f = get_function(kernel);
+  return hipModuleLaunchKernel(f, args.grid, 1, 1, 256, 1, 1, 0, st, nullptr, extra) == hipSuccess;
+}
+
+bool asm_qkv_rope(bool col, const void* h, const void* w, void* qkv, const float* cs3, int M, int N, int K, int lda, int ldb,
+                  int n, int T, int Tp, int Np, int H, int logS, hipStream_t st) {
+  if (M <= 0 || M % 256 || N % 256 || K != 1024 || n % 256 || M % n || (H * 64) % 256 || N != 3 * H * 64) return false;
+  GemmArgs args;
+  std::memset(&args, 0, sizeof(args));
+  args.a = h; args.b = w; args.c = qkv; args.aux0 = cs3;
+  args.m = M; args.n = N; args.k = K; args.lda = lda; args.ldb = ldb;
+  args.tiles_n = N / 256;
+  args.num_tiles = (M / 256) * (N / 256);
+  args.grid = asm_gemm_grid(args.num_tiles);
+  args.ld_aux = n; args.flags = T; args.pad = Tp; args.e0 = Np; args.e1 = H; args.e2 = logS;
+  size_t size = sizeof(args);
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  hipFunction_t f = get_function(col ? "dalle_gemm_nt_qkv_col" : "dalle_gemm_nt_qkv_row");
   return hipModuleLaunchKernel(f, args.grid, 1, 1, 256, 1, 1, 0, st, nullptr, extra) == hipSuccess;
 }
 

@@ -98,6 +98,7 @@ class Wave:
         self.s = np.zeros(108, dtype=np.uint64)
         self.m0 = 0
         self.scc = 0
+        self.vcc = np.zeros(64, dtype=bool)
         self.pc = 0
         self.done = False
         self.v[0] = np.arange(64) + 64 * wid
@@ -304,6 +305,19 @@ class Workgroup:
             r = rf.astype(np.float32).view(np.uint32).astype(np.uint64)
         elif op == "v_bfi_b32":
             r = (x(1) & x(2)) | (~x(1) & M & x(3))
+        elif op == "v_subrev_u32":
+            r = (x(2) - x(1)) & M
+        elif op == "v_add3_u32":
+            r = (x(1) + x(2) + x(3)) & M
+        elif op == "v_bfe_u32":
+            r = (x(1) >> (x(2) & 31)) & ((np.uint64(1) << (x(3) & 31)) - np.uint64(1))
+        elif op == "v_cmp_gt_u32":
+            assert t[0] == "vcc"
+            w.vcc = x(1) > x(2)
+            return None
+        elif op == "v_cndmask_b32":
+            assert t[3] == "vcc"
+            r = np.where(w.vcc, x(2), x(1))
         elif op == "v_cvt_pk_bf16_f32":
             a = x(1).astype(np.uint32).view(np.float32)
             b = x(2).astype(np.uint32).view(np.float32)
@@ -418,9 +432,9 @@ def d0(t):
     return int(t[0][1:])
 
 
-def run_kernel(asm_text, name, mem, kernarg, grid):
+def run_kernel(asm_text, name, mem, kernarg, grid, wgs=None):
     code, labels = parse_kernel(asm_text, name)
-    for wg in range(grid):
+    for wg in (range(grid) if wgs is None else wgs):
         Workgroup(code, labels, mem, kernarg, wg).run()
 
 
@@ -438,7 +452,7 @@ def selftest(asm_path):
         pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
         pc = mem.alloc(np.full((splits, M, N), np.nan, dtype=np.float32), "C")
         units = (M // 256) * (N // 256) * splits
-        ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, Ktot // splits, M, N, N, N // 256, units, units, 0, 0, 0)
+        ka = struct.pack("<6Q16i", pa, pb, pc, 0, 0, 0, M, N, Ktot // splits, M, N, N, N // 256, units, units, 0, 0, 0, 0, 0, 0, 0)
         run_kernel(text, "dalle_gemm_tn_wgrad", mem, ka, units)
         got = mem.get(pc, np.float32, (splits, M, N)).sum(0)
         ref = bf16_to_f32(Ab).T @ bf16_to_f32(Bb)
@@ -455,7 +469,7 @@ def selftest(asm_path):
         pc = mem.alloc(np.zeros((M, N), dtype=np.uint16), "C")
         nt = (M // 256) * (N // 256)
         grid = (nt + 7) // 8 * 8
-        ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, N // 256, nt, grid, 0, 0, 0)
+        ka = struct.pack("<6Q16i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, N // 256, nt, grid, 0, 0, 0, 0, 0, 0, 0)
         run_kernel(text, "dalle_gemm_nt_plain", mem, ka, grid)
         got = bf16_to_f32(mem.get(pc, np.uint16, (M, N)))
         ref = bf16_to_f32(Ab) @ bf16_to_f32(Bb).T
@@ -463,6 +477,7 @@ def selftest(asm_path):
         print(f"nt M={M} N={N} K={K}: max_rel_err {err:.2e}")
         ok &= err < 1e-2
     ok &= selftest_geglu(text)
+    ok &= selftest_qkv(text, col=True) and selftest_qkv(text, col=False)
     return ok
 
 
@@ -475,6 +490,70 @@ def ff_in_perm(F):
 def gelu_ref(x):
     from math import erf, sqrt
     return np.array([0.5 * v * (1 + erf(v / sqrt(2))) for v in x.ravel()], dtype=np.float64).reshape(x.shape)
+
+
+def tile_of_wg(wg, grid, tiles_m, tiles_n):
+    """(tm, tn) of the first tile of workgroup wg: the kernels' XCD map (grid a multiple of 8) and the grouped
+    tile order of gen_gemm.tile_coords (8 tile rows per group, column-major inside)"""
+    tile = (wg % 8) * (grid // 8) + wg // 8
+    full = (tiles_m & ~7) * tiles_n
+    if tile < full:
+        g, w = divmod(tile, 8 * tiles_n)
+        return 8 * g + w % 8, w // 8
+    rem = tiles_m & 7
+    w = tile - full
+    return (tiles_m & ~7) + w % rem, w // rem
+
+
+def selftest_qkv(text, col=True, T=257, S=16, H=4, B=2, K=1024, grid=8, wgs=None):
+    rng = np.random.default_rng(2)
+    I = S * S
+    n = T + I - 1
+    Tp = (T + 31) // 32 * 32
+    Np = Tp + I
+    M, N = B * n, 3 * H * 64
+    h = f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
+    w = f32_to_bf16((rng.standard_normal((N, K)) * 0.03).astype(np.float32))
+    cs = rng.uniform(-1, 1, (3, n + 1, 32, 2)).astype(np.float32)
+    mem = Memory()
+    ph, pw = mem.alloc(h, "h"), mem.alloc(w, "w")
+    pq = mem.alloc(np.zeros((3, B * H, Np, 64), dtype=np.uint16), "qkv")
+    pcs = mem.alloc(cs, "cs3")
+    nt = (M // 256) * (N // 256)
+    logS = S.bit_length() - 1
+    ka = struct.pack("<6Q16i", ph, pw, pq, pcs, 0, 0, M, N, K, K, K, 0, N // 256, nt, grid, n, T, Tp, Np, H, logS, 0)
+    run_kernel(text, "dalle_gemm_nt_qkv_col" if col else "dalle_gemm_nt_qkv_row", mem, ka, grid, wgs)
+    got = mem.get(pq, np.uint16, (3, B * H, Np, 64))
+    qkv = bf16_to_f32(f32_to_bf16(bf16_to_f32(h) @ bf16_to_f32(w).T)).reshape(B, n, 3, H, 32, 2)
+    c, s_ = cs[:, :n, None, :, 0], cs[:, :n, None, :, 1]          # (3, n, 1, 32)
+    x0, x1 = qkv[..., 0].transpose(2, 0, 1, 3, 4), qkv[..., 1].transpose(2, 0, 1, 3, 4)   # (3, B, n, H, 32)
+    y0 = x0 * c[:, None] - x1 * s_[:, None]
+    y1 = x1 * c[:, None] + x0 * s_[:, None]
+    ref = np.zeros((3, B, H, Np, 64), dtype=np.float32)
+    p = np.arange(n)
+    k = p - T
+    st = np.where(p < T, p, Tp + (((k % S) * S + k // S) if col else k))
+    y = np.stack([y0, y1], -1).reshape(3, B, n, H, 64).transpose(0, 1, 3, 2, 4)   # (3, B, H, n, 64)
+    ref[:, :, :, st] = y
+    ref = ref.reshape(3, B * H, Np, 64)
+    gotf = bf16_to_f32(got)
+    if wgs is not None:     # only the tiles the chosen workgroups own (one tile each: grid >= tiles)
+        errs = []
+        for wg in wgs:
+            tm, tn = tile_of_wg(wg, grid, M // 256, N // 256)
+            rows = np.arange(tm * 256, tm * 256 + 256)
+            b, pp = rows // n, rows % n
+            for cc in range(tn * 256, tn * 256 + 256, 64):
+                part, hh = cc // (H * 64), (cc % (H * 64)) // 64
+                g_ = gotf[part, b * H + hh, st[pp]]
+                r_ = ref[part, b * H + hh, st[pp]]
+                errs.append(np.abs(g_ - r_).max())
+        err = float(max(errs) / np.abs(ref).max())
+        print(f"qkv col={col} wgs={wgs}: max_rel_err {err:.2e}")
+        return err < 1.5e-2
+    err = float(np.abs(gotf[:, :, st] - ref[:, :, st]).max() / np.abs(ref).max())
+    print(f"qkv col={col} T={T} S={S} H={H} B={B}: max_rel_err {err:.2e}")
+    return err < 1.5e-2
 
 
 def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):
@@ -491,7 +570,7 @@ def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):
     pbias = mem.alloc(b1p, "b1p")
     pu = mem.alloc(np.zeros((M, F), dtype=np.uint16), "u")
     nt = (M // 256) * (2 * F // 256)
-    ka = struct.pack("<6Q12i", pa, pb, pc, pbias, pu, 0, M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0)
+    ka = struct.pack("<6Q16i", pa, pb, pc, pbias, pu, 0, M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
     run_kernel(text, "dalle_gemm_nt_geglu", mem, ka, grid)
     a = bf16_to_f32(mem.get(pc, np.uint16, (M, 2 * F)))
     u = bf16_to_f32(mem.get(pu, np.uint16, (M, F)))

@@ -68,7 +68,7 @@ S_TM, S_TNI = 67, 68  # tile row / column index
 S_G8, S_MAGG, S_FULL, S_TMFULL, S_ROWREM, S_MAGR = 69, 70, 71, 76, 77, 78
 S_SRDX = 72         # s[72:75] a spare resource (epilogue operands)
 S_KV, S_WRAP, S_S0B = 79, 80, 81   # K-slice of the next DMA, 128 - 2 K (the wrap step), first slice * 128
-S_LAST = 96
+S_LAST = 100
 
 # VGPRs
 V_TID = 0
@@ -259,7 +259,8 @@ SPLIT_DMA_SLOTS = [20 + 4 * n for n in range(8)] + [54 + 10 * n for n in range(8
 STORE_SLOTS = [3 + 4 * n for n in range(8)]                   # deferred epilogue stores: before B2
 
 
-def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), head=(), work=(), work_span=(40, 120)):
+def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), head=(), work=(), work_span=(40, 120),
+              work2=(), work2_span=(60, 118)):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
     ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
@@ -303,11 +304,11 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     assert len(stores) <= len(STORE_SLOTS)
     for n, grp in enumerate(stores):
         slots[STORE_SLOTS[n]].extend(grp)
-    if work:
-        lo, hi = work_span
-        assert hi <= 120
-        for n, ins in enumerate(work):
-            slots[lo + n * (hi - lo) // len(work)].append(ins)
+    for wk, (lo, hi) in ((work, work_span), (work2, work2_span)):
+        if wk:
+            assert hi <= 120
+            for n, ins in enumerate(wk):
+                slots[lo + n * (hi - lo) // len(wk)].append(ins)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
     if dma and (SPLIT or TN):
         # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
@@ -348,6 +349,18 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
             slots[n].append(ins)
         # MFMA 0 of the next step needs A0 / B0 (the first two of these 16 reads)
         slots[127].append("s_waitcnt lgkmcnt(0)" if TN else f"s_waitcnt lgkmcnt({16 - 2})")
+    # deferred-work markers "@vmwait:TAG": wait until the VMEM instruction(s) tagged "; @TAG" (placed
+    # earlier in this step) have completed -- vmcnt(number of VMEM instructions issued after the last one)
+    order = [(n, k) for n in range(128) for k in range(len(slots[n]))]
+    vm_seen = []
+    for n, k in order:
+        ins = slots[n][k]
+        if ins.startswith("@vmwait:"):
+            tag = ins.split(":", 1)[1]
+            last = max(i for i, x in enumerate(vm_seen) if x.endswith("; @" + tag))
+            slots[n][k] = f"s_waitcnt vmcnt({len(vm_seen) - 1 - last})"
+        elif ins.startswith("buffer_"):
+            vm_seen.append(ins)
     mf = m0 + m1
     for ins in head:
         e(ins)
@@ -751,7 +764,7 @@ def set_srd(e, srd, ptr, row0, ld, nr):
     e(f"s_mov_b32 s{srd + 3}, 0x20000")
 
 
-KERNARG_SIZE = 96
+KERNARG_SIZE = 112
 
 
 def metadata(name):
@@ -763,7 +776,7 @@ def metadata(name):
         .size:           8
         .value_kind:     global_buffer""")
         off += 8
-    for _ in range(12):
+    for _ in range(16):
         args.append(f"""      - .offset:         {off}
         .size:           4
         .value_kind:     by_value""")
@@ -1154,7 +1167,13 @@ def geglu_lane_setup(e, diag=None):
     e(f"v_add_u32 v{T1}, s{S_T1}, v{T1}")
     e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
     e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T1}")
-    e(f"v_add_u32 v{V_COG}, s{S_F2}, v{V_CO}")
+    if diag == "adjacent":      # measurement: gate chunk stored right after the value chunk (wrong layout)
+        e(f"v_lshlrev_b32 v{T1}, 1, v{T1}")
+        e(f"v_mul_lo_u32 v{V_CO}, v{T0}, s{S_LDC2}")
+        e(f"v_add_u32 v{V_CO}, v{V_CO}, v{T1}")
+        e(f"v_add_u32 v{V_COG}, 8, v{V_CO}")
+    else:
+        e(f"v_add_u32 v{V_COG}, s{S_F2}, v{V_CO}")
     e(f"v_mul_lo_u32 v{V_CU}, v{T0}, s{S_LDU2}")
     e(f"v_add_u32 v{V_CU}, v{V_CU}, v{T1}")
 
@@ -1247,7 +1266,7 @@ def kernel_geglu(name, diag=None):
         if idx < N_IMMEDIATE:
             pack_row(e, "bias", i, r, t, t + 8)
             seq = ge_stores_a(i, r, t + 8)
-            if diag != "nowork":
+            if diag not in ("nowork", "adjacent"):
                 seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
                 seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
                         f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
@@ -1271,7 +1290,7 @@ def kernel_geglu(name, diag=None):
             for (i, r, src) in stash[ai:ai + per_step_a[t]]:
                 work += ge_stores_a(i, r, src)
             ai += per_step_a[t]
-        if diag != "nowork":
+        if diag not in ("nowork", "adjacent"):
             for (i, r, src) in stash[ui:ui + GE_SPLIT[t]]:
                 # (its `a` chunks were stored in this or an earlier step: the values may be overwritten)
                 work += ge_u(src, tuple(GE_T + q for q in range(7)), (src, src + 1))
@@ -1292,7 +1311,7 @@ def kernel_geglu(name, diag=None):
         t = V_EPI + (idx % 4) * 12
         pack_row(e, "bias", i, r, t, t + 8)
         seq = ge_stores_a(i, r, t + 8)
-        if diag != "nowork":
+        if diag not in ("nowork", "adjacent"):
             seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
             seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
                     f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
@@ -1304,10 +1323,239 @@ def kernel_geglu(name, diag=None):
     return e.text()
 
 
+
+# ----------------------------------------------------------------------------------------------------
+# QKV projection + 3-axis rotary written straight into the attention storage (q pre-scaled): qkv = h Wqkv^T
+# (M x 3 H 64), each 64-column head block rotated pairwise by the (cos, sin) of its sequence position and stored
+# as row st(p) of head (part, b, h) of the (3, B H, Np, 64) storage -- st(p) = p for text, Tp + the image
+# position (transposed for the axial-column pattern, variant _col) otherwise.  A tile is 256 positions of ONE
+# sample (host: n % 256 == 0) and 4 heads of one part.  The rotation runs on the stored bf16 values, as the
+# unfused path (GEMM, then rope_fwd) does, so it is deferred like the plain stores: 8 row-groups rotated and
+# stored at the tile boundary with (cos, sin) prefetched during the last K-step, 24 packed in v[144:239] and
+# rotated / stored under the successor's K-steps 0..11 (their (cos, sin) loaded early in the same step).
+# cs3 = (3, n + 1, 32, 2) fp32 (cos, sin) per rotary pair of q (scaled by 1/8), k and v (all three rotated).
+# ----------------------------------------------------------------------------------------------------
+S_SRDQ, S_SRDCS = 84, 88
+S_QN, S_QT, S_QTP, S_QNP, S_QH, S_QLOGS, S_QP0, S_QMAGN = 92, 93, 94, 95, 96, 97, 98, 99
+S_QBT, S_QHD = 82, 83
+V_QLC, V_QPL, V_QCS = 13, 14, 15
+QX = (9, 10, 11, 12)                 # rotation temps
+Q_IMM = 8                            # row-groups rotated at the boundary
+Q_BANKS = (240, 248)                 # (cos, sin) of the two row-groups of a successor step
+Q_IMM_BANK = 176                     # the boundary row-groups' (cos, sin), prefetched in the last K-step
+
+
+def qkv_setup_tile():
+    """(penult's MFMA gaps) the finishing tile's sample b, first position p0, part / first head, and the
+    storage and (cos, sin) resources"""
+    T0, T1, T2, T3 = S_T0, S_T1, S_T2, S_T3
+    return [f"s_mul_hi_u32 s{T0}, s{S_ROW0}, s{S_QMAGN}",          # b
+            f"s_mul_i32 s{T1}, s{T0}, s{S_QN}",
+            f"s_sub_u32 s{S_QP0}, s{S_ROW0}, s{T1}",                # p0
+            f"s_cmp_ge_u32 s{S_COL0}, s{S_QHD}",
+            f"s_cselect_b32 s{T1}, 1, 0",
+            f"s_lshl_b32 s{T2}, s{S_QHD}, 1",
+            f"s_cmp_ge_u32 s{S_COL0}, s{T2}",
+            f"s_cselect_b32 s{T2}, 1, 0",
+            f"s_add_u32 s{T1}, s{T1}, s{T2}",                       # part
+            f"s_mul_i32 s{T2}, s{T1}, s{S_QHD}",
+            f"s_sub_u32 s{T2}, s{S_COL0}, s{T2}",
+            f"s_lshr_b32 s{T2}, s{T2}, 6",                          # first head of the tile
+            f"s_mul_i32 s{T3}, s{T1}, s{S_QBT}",
+            f"s_add_u32 s{T3}, s{T3}, s{T0}",
+            f"s_mul_i32 s{T3}, s{T3}, s{S_QH}",
+            f"s_add_u32 s{T3}, s{T3}, s{T2}",                       # global head index
+            f"s_add_u32 s{T0}, s{S_QN}, 1",
+            f"s_mul_i32 s{T0}, s{T0}, s{T1}",
+            f"s_lshl_b32 s{T0}, s{T0}, 8",                          # part (n + 1) 256
+            f"s_add_u32 s{S_SRDCS}, s{S_AUX0}, s{T0}",
+            f"s_addc_u32 s{S_SRDCS + 1}, s{S_AUX0 + 1}, 0",
+            f"s_mov_b32 s{S_SRDCS + 2}, -1",
+            f"s_mov_b32 s{S_SRDCS + 3}, 0x20000",
+            f"s_mul_i32 s{T2}, s{T3}, s{S_QNP}",
+            f"s_mov_b32 s{T3}, 0",
+            f"s_lshl_b64 s[{T2}:{T3}], s[{T2}:{T3}], 7",            # head * Np * 128 bytes
+            f"s_add_u32 s{S_SRDQ}, s{S_C}, s{T2}",
+            f"s_addc_u32 s{S_SRDQ + 1}, s{S_C + 1}, s{T3}",
+            f"s_mov_b32 s{S_SRDQ + 2}, -1",
+            f"s_mov_b32 s{S_SRDQ + 3}, 0x20000"]
+
+
+def qkv_load(i, r, bank, tag):
+    """(cos, sin) of the row-group's 4 pairs: v[bank:bank+7] (the byte offset goes through v[bank+4])"""
+    return [f"v_add_u32 v{bank + 4}, s{S_QP0}, v{V_QPL}",
+            f"v_add_u32 v{bank + 4}, {16 * i + r}, v{bank + 4}",          # position p
+            f"v_lshl_add_u32 v{bank + 4}, v{bank + 4}, 8, v{V_QCS}",
+            f"buffer_load_dwordx4 v[{bank}:{bank + 3}], v{bank + 4}, {sr(S_SRDCS, 4)}, 0 offen ; @{tag}",
+            f"buffer_load_dwordx4 v[{bank + 4}:{bank + 7}], v{bank + 4}, {sr(S_SRDCS, 4)}, 0 offen offset:16 ; @{tag}"]
+
+
+def qkv_rotate_store(i, r, src, bank, col):
+    """rotate the packed row-group v[src:src+3] by v[bank:bank+7], then store it at its storage row"""
+    x0, x1, ta, tb = QX
+    out = []
+    for k in range(4):
+        cs_, sn = bank + 2 * k, bank + 2 * k + 1
+        out += [f"v_lshlrev_b32 v{x0}, 16, v{src + k}",
+                f"v_and_b32 v{x1}, 0xffff0000, v{src + k}",
+                f"v_mul_f32 v{ta}, v{x1}, v{sn}",
+                f"v_fma_f32 v{ta}, v{x0}, v{cs_}, -v{ta}",                  # x0 c - x1 s
+                f"v_mul_f32 v{tb}, v{x0}, v{sn}",
+                f"v_fma_f32 v{tb}, v{x1}, v{cs_}, v{tb}",                   # x1 c + x0 s
+                f"v_cvt_pk_bf16_f32 v{src + k}, v{ta}, v{tb}"]
+    p, st, t = bank, bank + 1, bank + 2
+    out += [f"v_add_u32 v{p}, s{S_QP0}, v{V_QPL}",
+            f"v_add_u32 v{p}, {16 * i + r}, v{p}",
+            f"v_subrev_u32 v{st}, s{S_QT}, v{p}"]                           # image position k = p - T
+    if col:
+        out += [f"v_bfe_u32 v{t}, v{st}, 0, s{S_QLOGS}",
+                f"v_lshlrev_b32 v{t}, s{S_QLOGS}, v{t}",
+                f"v_lshrrev_b32 v{st}, s{S_QLOGS}, v{st}",
+                f"v_add3_u32 v{st}, v{t}, v{st}, s{S_QTP}"]                 # Tp + (k % S) S + k / S
+    else:
+        out += [f"v_add_u32 v{st}, s{S_QTP}, v{st}"]                        # Tp + k
+    out += [f"v_cmp_gt_u32 vcc, s{S_QT}, v{p}",
+            f"v_cndmask_b32 v{st}, v{st}, v{p}, vcc",                       # text: row p
+            f"v_lshl_add_u32 v{st}, v{st}, 7, v{V_QLC}",
+            f"buffer_store_dwordx4 {vr(src)}, v{st}, {sr(S_SRDQ, 4)}, 0 offen"]
+    return out
+
+
+def qkv_lane_setup(e):
+    T0, T1 = V_T, V_T + 1
+    # V_QLC = (2 wn + (c >> 3)) Np 128 + 16 (c & 7);  V_QPL = 128 wm + 4 g;  V_QCS = 32 (c & 7)
+    e(f"v_and_b32 v{T0}, 15, v{V_TID}")
+    e(f"v_lshrrev_b32 v{T0}, 3, v{T0}")                  # c >> 3
+    e(f"s_and_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 1")
+    e(f"v_add_u32 v{T0}, s{S_T0}, v{T0}")                # head within the tile
+    e(f"s_lshl_b32 s{S_T1}, s{S_QNP}, 7")
+    e(f"v_mul_lo_u32 v{V_QLC}, v{T0}, s{S_T1}")
+    e(f"v_and_b32 v{T1}, 7, v{V_TID}")
+    e(f"v_lshlrev_b32 v{V_QCS}, 5, v{T1}")
+    e(f"v_lshl_add_u32 v{V_QLC}, v{T1}, 4, v{V_QLC}")
+    e(f"v_lshrrev_b32 v{T0}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 3, v{T0}")
+    e(f"v_lshlrev_b32 v{T0}, 2, v{T0}")
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 7")
+    e(f"v_add_u32 v{V_QPL}, s{S_T0}, v{T0}")
+
+
+def kernel_qkv(name, col):
+    e = Emitter(name)
+    e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")
+    e(f"s_load_dwordx8 {sr(S_M, 8)}, s[0:1], 0x30")
+    e(f"s_load_dword s{S_GRID}, s[0:1], 0x50")
+    e(f"s_load_dwordx2 s[{S_QN}:{S_QT}], s[0:1], 0x54")     # n, T
+    e(f"s_load_dwordx2 s[{S_QTP}:{S_QNP}], s[0:1], 0x5c")   # Tp, Np
+    e(f"s_load_dwordx2 s[{S_QH}:{S_QLOGS}], s[0:1], 0x64")  # H, log2 S
+    e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+    e("s_nop 1")
+    e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+    e("s_nop 1")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
+    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
+    e("s_cbranch_scc0 " + e.L("end"))
+    e(f"s_lshl_b32 s{S_QHD}, s{S_QH}, 6")                # H * 64 columns per part
+    magic(e, S_QMAGN, S_QN)
+    e(f"s_mul_hi_u32 s{S_QBT}, s{S_M}, s{S_QMAGN}")      # batch = M / n
+    lane_setup(e, "plain")
+    qkv_lane_setup(e)
+    e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
+    e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
+    e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
+    e(f"s_lshr_b32 s{S_T1}, s{S_WG}, 3")
+    e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
+    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("end"))
+    tile_order_setup(e)
+    stagger_setup(e)
+    emit_all(e, tile_coords())
+    setup_operands(e)
+    prologue_dma(e)
+    e("s_waitcnt vmcnt(16)")
+    e("s_barrier")
+    body_head(e, "plain", 0)
+    iteration(e, "first", None, 0)
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    e.label(e.L("kloop"))
+    iteration(e, "loop")
+    e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc0 " + e.L("kloop"))
+    e.label(e.L("tail"))
+    pre_out = qkv_setup_tile()
+    sub = Emitter(e.prefix)
+    setup_operands(sub)
+    pre_next = pre_out + next_tile() + [l.strip() for l in sub.lines]
+    imm_loads = []
+    for idx in range(Q_IMM):
+        i, r = divmod(idx, 4)
+        imm_loads += qkv_load(i, r, Q_IMM_BANK + 8 * idx, "imm")
+
+    def boundary(final):
+        vm = iteration(e, "last", None, prefetch=not final, work=imm_loads, work_span=(1, 17))
+        last_ld = max(k for k, ins in enumerate(vm) if ins.endswith("; @imm"))
+        e(f"s_waitcnt vmcnt({len(vm) - 1 - last_ld})")
+        if not final:
+            tile_boundary(e)
+        else:
+            for _ in range(3):
+                e("s_nop 7")
+        n_vm = 0
+        for idx in range(Q_IMM):
+            i, r = divmod(idx, 4)
+            t = V_ETMP + (idx % 4) * 12
+            pack_row(e, "plain", i, r, t, t + 8)
+            seq = qkv_rotate_store(i, r, t + 8, Q_IMM_BANK + 8 * idx, col)
+            emit_all(e, seq)
+            n_vm += 1
+        return n_vm
+
+    e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
+    e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("final"))
+    iteration(e, "penult", None, prefetch=True, pre=pre_next)
+    n_vm = boundary(False)
+    stash = []
+    for idx in range(Q_IMM, 32):
+        i, r = divmod(idx, 4)
+        dst = V_STASH + 4 * (idx - Q_IMM)
+        pack_row(e, "plain", i, r, V_ETMP, dst)
+        stash.append((i, r, dst))
+    e(f"s_waitcnt vmcnt({16 + n_vm})")                   # the successor's step 0 landed
+    e("s_barrier")
+    body_head(e, "plain", 0)
+    for t in range(14):
+        loads, comp = [], []
+        for b_, (i, r, src) in enumerate(stash[2 * t:2 * t + 2] if t < 12 else []):
+            tag = f"q{b_}"
+            loads += qkv_load(i, r, Q_BANKS[b_], tag)
+            comp += [f"@vmwait:{tag}"] + qkv_rotate_store(i, r, src, Q_BANKS[b_], col)
+        iteration(e, "first" if t == 0 else "loop", None, n_vm if t == 0 else 0, work=loads, work_span=(1, 4),
+                  work2=comp, work2_span=(60, 118))
+    e("s_branch " + e.L("tail"))
+    e.label(e.L("final"))
+    iteration(e, "penult", None, pre=pre_out)
+    boundary(True)
+    for idx in range(Q_IMM, 32):
+        i, r = divmod(idx, 4)
+        t = V_EPI + (idx % 4) * 12
+        pack_row(e, "plain", i, r, t, t + 8)
+        emit_all(e, qkv_load(i, r, Q_BANKS[0], "f") + ["s_waitcnt vmcnt(0)"] +
+                 qkv_rotate_store(i, r, t + 8, Q_BANKS[0], col))
+    e.label(e.L("end"))
+    e("s_waitcnt vmcnt(0)")
+    e("s_endpgm")
+    return e.text()
+
+
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None),
-           ("dalle_gemm_nt_geglu", "geglu", None)]
+           ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")] + [
-    ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork")]
+    ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent")]
 
 
 def main(out, diag=False):
@@ -1315,7 +1563,14 @@ def main(out, diag=False):
     metas = []
     for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
-        parts.append(kernel_tn(name) if epi == "tn" else kernel_geglu(name, dg) if epi == "geglu" else kernel(name, epi, dg))
+        if epi == "tn":
+            parts.append(kernel_tn(name))
+        elif epi == "geglu":
+            parts.append(kernel_geglu(name, dg))
+        elif epi == "qkv":
+            parts.append(kernel_qkv(name, dg))
+        else:
+            parts.append(kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
         parts.append(descriptor(name))
         metas.append(metadata(name))

@@ -522,6 +522,25 @@ void asm_wgrad_(Tensor out, Tensor A, Tensor B, int64_t splits, bool accumulate)
   dalle::splitk_accum(part.data_ptr<float>(), out.data_ptr<float>(), (long)M * N, (int)splits, accumulate ? 1 : 0, cur_stream());
 }
 
+// QKV + rotary on the assembly kernel: h (M, 1024) bf16, w (3 H 64, 1024) bf16, cs3 (3, n + 1, 32, 2) fp32 (q's
+// (cos, sin) pre-scaled, k's and v's plain: all three rotated) -> q, k, v (B H, Np, 64) storage views (padding rows zeroed)
+std::vector<Tensor> asm_qkv_rope(Tensor h, Tensor w, Tensor cs3, int64_t T, int64_t S, int64_t H, int64_t n, bool col_major) {
+  CHECK_IN(h, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16); CHECK_IN(cs3, torch::kFloat32);
+  TORCH_CHECK(h.dim() == 2 && w.dim() == 2 && w.size(0) == 3 * H * 64 && w.size(1) == h.size(1), "asm_qkv_rope: shapes");
+  const int M = h.size(0), K = h.size(1);
+  TORCH_CHECK(cs3.dim() == 4 && cs3.size(0) == 3 && cs3.size(1) >= n + 1 && cs3.size(2) == 32 && cs3.size(3) == 2,
+              "asm_qkv_rope: cs3 (3, n + 1, 32, 2)");
+  auto g = make_attn_geom(T, S, n, 1, H, 0);
+  const int B = M / n;
+  auto qkv = torch::empty({3, B * H, g.Np, 64}, h.options());
+  TORCH_CHECK(dalle::asm_qkv_rope(col_major, h.data_ptr(), w.data_ptr(), qkv.data_ptr(), cs3.data_ptr<float>(), M, (int)w.size(0), K,
+                                  (int)h.stride(0), (int)w.stride(0), (int)n, (int)T, g.Tp, g.Np, (int)H, ilog2((int)S), cur_stream()),
+              "asm_qkv_rope: unsupported shape");
+  auto q = qkv[0], k = qkv[1], v = qkv[2];
+  dalle::rope_pad_zero(q.data_ptr(), k.data_ptr(), v.data_ptr(), g.Tp, T, g.Np, B * H, cur_stream());
+  return {q, k, v};
+}
+
 // FF-in GEMM + GEGLU on the assembly kernel: x (M, 1024) bf16, w1p (2F, 1024) bf16 = W1 with its rows in the
 // interleaved [value 8 | gate 8] order (hip_ops.ff_in_perm), b1p (2F,) fp32 in the same order ->
 // a (M, 2F) bf16 pre-activation in the ORIGINAL [value | gate] order, u (M, F) = value * gelu(gate)
@@ -1267,6 +1286,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1: hand-written GEMM workgroups wait for their output stores before ending");
   m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
   m.def("asm_gemm", &asm_gemm, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out") = py::none());
+  m.def("asm_qkv_rope", &asm_qkv_rope, py::arg("h"), py::arg("w"), py::arg("cs3"), py::arg("T"), py::arg("S"), py::arg("H"),
+        py::arg("n"), py::arg("col_major"));
   m.def("asm_ff_in_geglu", &asm_ff_in_geglu, py::arg("x"), py::arg("w1p"), py::arg("b1p"));
   m.def("asm_wgrad_", &asm_wgrad_, py::arg("out"), py::arg("A"), py::arg("B"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);

@@ -191,6 +191,18 @@ def rope_cs_table(geom: AttnGeometry, dim_head: int, device) -> torch.Tensor:
     return t
 
 
+def _cs3_from_tables(cos: torch.Tensor, sin: torch.Tensor, qscale: float) -> torch.Tensor:
+    """(3, n + 1, 32, 2) (cos, sin) per rotary pair for q (scaled by ``qscale``), k and v (all three are rotated,
+    as rope_fwd does): the table of the assembly QKV + rotary kernel (cached per table)."""
+    key = ("cs3", cos.data_ptr(), tuple(cos.shape), str(cos.device), qscale)
+    t = _cs_tables.get(key)
+    if t is None:
+        cs = _cs_from_tables(cos, sin)
+        t = torch.stack([cs * qscale, cs, cs]).contiguous()
+        _cs_tables[key] = t
+    return t
+
+
 def _cs_from_tables(cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     """rope_cs_table's packing from the (cos, sin) tables themselves (cached per table)."""
     key = ("tab", cos.data_ptr(), tuple(cos.shape), str(cos.device))
@@ -608,7 +620,12 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     h2 = h.view(-1, d)
     wq = bf16_weight(w_qkv)
     col = pattern == PATTERN_IDS["axial_col"]
-    if (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0 and d >= 128:
+    if ASM_GEMM and n % 256 == 0 and d == 1024 and wq.shape[0] == 3 * H * 64 and (H * 64) % 256 == 0 and h2.stride(1) == 1:
+        # QKV GEMM on the assembly kernel, the rotary applied to its stored bf16 values in the deferred epilogue
+        q, k, v = C().asm_qkv_rope(h2, wq, _cs3_from_tables(cos, sin, 0.125), T, S, H, n, col)
+        _count("qkv_rope")
+        _count("asm_qkv_rope")
+    elif (B * n) % 256 == 0 and wq.shape[0] % 256 == 0 and d % 64 == 0 and d >= 128:
         # QKV GEMM with the rotary fused into its epilogue: writes the attention storage directly
         q, k, v = C().qkv_rope_pt(h2, wq, _cs_from_tables(cos, sin), T, S, H, n, col, 0.125)
         _count("qkv_rope")

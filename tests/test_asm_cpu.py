@@ -87,7 +87,7 @@ def test_kernels_on_the_emulator(tmp_path):
     mem = emu.Memory()
     pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
     pc = mem.alloc(np.zeros((M, N), dtype=np.float32), "C")
-    ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, Ktot, M, N, N, 1, 1, 1, 0, 0, 0)
+    ka = struct.pack("<6Q16i", pa, pb, pc, 0, 0, 0, M, N, Ktot, M, N, N, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0)
     emu.run_kernel(text, "dalle_gemm_tn_wgrad", mem, ka, 1)
     ref = emu.bf16_to_f32(Ab).T @ emu.bf16_to_f32(Bb)
     got = mem.get(pc, np.float32, (M, N))
@@ -98,7 +98,7 @@ def test_kernels_on_the_emulator(tmp_path):
     mem = emu.Memory()
     pa, pb = mem.alloc(Ab, "A"), mem.alloc(Bb, "B")
     pc = mem.alloc(np.zeros((M, N), dtype=np.uint16), "C")
-    ka = struct.pack("<6Q12i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, 1, 1, 8, 0, 0, 0)
+    ka = struct.pack("<6Q16i", pa, pb, pc, 0, 0, 0, M, N, K, K, K, N, 1, 1, 8, 0, 0, 0, 0, 0, 0, 0)
     emu.run_kernel(text, "dalle_gemm_nt_plain", mem, ka, 8)
     ref = emu.bf16_to_f32(Ab) @ emu.bf16_to_f32(Bb).T
     got = emu.bf16_to_f32(mem.get(pc, np.uint16, (M, N)))

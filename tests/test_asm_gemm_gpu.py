@@ -102,3 +102,30 @@ def test_asm_ff_in_geglu(cuda, C, M, F):
     ref_u = af[:, :F] * torch.nn.functional.gelu(af[:, F:])
     assert ((u.float() - ref_u).abs().max() / ref_u.abs().max()).item() < 8e-3
     assert torch.equal(u, C.geglu_fwd(a)) or ((u.float() - C.geglu_fwd(a).float()).abs().max() <= 2 ** -6 * ref_u.abs().max())
+
+
+@pytest.mark.parametrize("B", [2, 8])
+@pytest.mark.parametrize("col", [False, True])
+def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B):
+    """QKV projection + 3-axis rotary on the assembly kernel (rotation deferred onto the stored bf16 values) ==
+    the unfused path (the projection, then rope_fwd on its bf16 output) on the reference geometry
+    (257 text + 32x32 image tokens, 16 heads: tiles straddle the text / image boundary). Two samples = 120
+    tiles, one per workgroup (the straight final path); eight = 480 tiles, so workgroups walk several tiles
+    and rotate / store under the successor tile's K-steps."""
+    from dalle_amd.models.patterns import AttnGeometry
+    from dalle_amd.ops.hip_ops import _cs3_from_tables, _rope_tables
+
+    torch.manual_seed(7)
+    T, S, H = 257, 32, 16
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    h = torch.randn(B * n, 1024, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(3 * H * 64, 1024, device=cuda) * 0.03).to(torch.bfloat16)
+    cos, sin = _rope_tables(geom, 64, cuda)
+    q, k, v = C.asm_qkv_rope(h, w, _cs3_from_tables(cos, sin, 0.125), T, S, H, n, col)
+    qkv = (h.float() @ w.float().t()).to(torch.bfloat16).view(B, n, -1)
+    q2, k2, v2 = C.rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+    for a, b in ((q, q2), (k, k2), (v, v2)):
+        assert a.shape == b.shape
+        err = ((a.float() - b.float()).abs().max() / b.float().abs().max()).item()
+        assert err < 1e-2, err
