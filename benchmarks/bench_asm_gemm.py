@@ -167,6 +167,48 @@ def bench_geglu(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
     print(json.dumps({"shape": f"GEGLU_M{M}_F{F}_K{K}", "us": us}), flush=True)
 
 
+def bench_geglu_bwd(mod, M=163840, F=4096, K=1024, iters=10, rounds=3):
+    """FF-out dgrad + GEGLU backward on the assembly kernel vs the plain GEMM of the same shape (the fused
+    backward's extra cost) and the HIP 8-phase kernel it replaces (extension)"""
+    dy = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+    w2t = torch.rand(F, K, device="cuda").sub_(0.5).mul_(0.06).to(torch.bfloat16)
+    h = torch.randn(M, 2 * F, device="cuda").to(torch.bfloat16)
+    dh = torch.empty_like(h)
+    du = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    part = torch.empty(M // 128, 2 * F, device="cuda")
+    nt = (M // 256) * (F // 256)
+    grid = min(256, (nt + 7) // 8 * 8)
+    ptrs = [dy.data_ptr(), w2t.data_ptr(), dh.data_ptr(), h.data_ptr(), part.data_ptr(), 0]
+    args = struct.pack("<6Q16i", *ptrs, M, F, K, K, K, 2 * F, F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
+    fns = {"asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", dy, w2t, du),
+           "asm_geglu_bwd": lambda: mod.launch("dalle_gemm_nt_geglu_bwd", grid, args)}
+    try:
+        sys.path.insert(0, os.path.join(HERE, ".."))
+        from dalle_amd.ops.ext import load_extension
+        C = load_extension(required=True)
+        fns["hip_8ph"] = lambda: C.ff_dgrad_geglu(dy, w2t, h, None)
+        fns["ext_asm"] = lambda: C.asm_ff_dgrad_geglu(dy, w2t, h, None)
+    except Exception as ex:   # extension not built: the code-object kernels only
+        print(json.dumps({"note": f"extension not loaded: {ex}"}))
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                f()
+            e.record()
+            e.synchronize()
+            times[k].append(s.elapsed_time(e) * 1000 / iters)
+    flop = 2.0 * M * F * K
+    us = {k: round(sorted(v)[len(v) // 2], 1) for k, v in times.items()}
+    print(json.dumps({"shape": f"GEGLU_BWD_M{M}_F{F}_K{K}", "us": us,
+                      "TF": {k: round(flop / v / 1e6) for k, v in us.items()}}), flush=True)
+
+
 def check(mod, shapes):
     ok = True
     for (M, N, K) in shapes:
@@ -228,6 +270,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tn", action="store_true", help="also time the weight-gradient (TN) kernel")
     ap.add_argument("--geglu", action="store_true", help="also time the fused FF-in + GEGLU kernel")
+    ap.add_argument("--geglu-bwd", action="store_true", help="also time the FF-out dgrad + GEGLU backward kernel")
+    ap.add_argument("--skip-plain", action="store_true", help="skip the plain-GEMM shape sweep")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="163840:1024:1024,163840:3072:1024,163840:4096:1024,163840:8192:1024,"
                                         "163840:1024:4096,163840:1024:8192,163840:1024:3072")
@@ -244,9 +288,13 @@ def main():
     if a.geglu:
         bench_geglu(mod, rounds=a.rounds,
                     diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
+    if a.geglu_bwd:
+        bench_geglu_bwd(mod, rounds=a.rounds)
     if a.tn:
         bench_tn(mod, [(163840, 1024, 1024, 16), (163840, 3072, 1024, 16), (163840, 8192, 1024, 2),
                        (163840, 1024, 4096, 4)], rounds=a.rounds)
+    if a.skip_plain:
+        return
     shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]
     diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None
     bench(mod, shapes, iters=a.iters, diag=diag, rounds=a.rounds)

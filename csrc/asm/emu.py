@@ -105,10 +105,10 @@ class Wave:
 
 
 class Workgroup:
-    def __init__(self, code, labels, mem, kernarg, wg_id, lds_bytes=160 * 1024):
+    def __init__(self, code, labels, mem, kernarg, wg_id, lds_bytes=160 * 1024, lds_alloc=131072):
         self.code, self.labels, self.mem = code, labels, mem
         self.lds = np.zeros(lds_bytes, dtype=np.uint8)
-        self.lds_alloc = 131072
+        self.lds_alloc = lds_alloc
         self.waves = [Wave(w) for w in range(4)]
         ka = mem.alloc(np.frombuffer(kernarg, dtype=np.uint8), "kernarg")
         for w in self.waves:
@@ -200,6 +200,18 @@ class Workgroup:
             return self.valu(w, op, toks)
         if op.startswith("ds_read"):
             return self.ds_read(w, op, toks, mods)
+        if op == "ds_write_b128":
+            off = 0
+            for m in mods:
+                if m.startswith("offset:"):
+                    off = int(m[7:])
+            src = reg_range(toks[1])[0]
+            addr = w.v[int(toks[0][1:])].astype(np.int64) + off
+            for l in range(64):
+                a = int(addr[l])
+                assert a % 16 == 0 and a + 16 <= self.lds_alloc, f"ds_write_b128 address {a}"
+                self.lds[a:a + 16] = w.v[src:src + 4, l].astype(np.uint32).view(np.uint8)
+            return None
         if op.startswith("buffer_"):
             return self.buffer(w, op, toks, mods)
         raise RuntimeError("unsupported: " + ins)
@@ -263,6 +275,17 @@ class Workgroup:
             op = op[:-4]
         if op == "v_accvgpr_read_b32":
             V[d0(t)] = w.a[int(t[1][1:])].view(np.uint32)
+            return None
+        if op in ("v_permlane16_swap_b32", "v_permlane32_swap_b32"):
+            # swap the odd rows (16 lanes) / upper half of vdst with the even rows / lower half of vsrc
+            a, b = int(t[0][1:]), int(t[1][1:])
+            va, vb = V[a].copy(), V[b].copy()
+            for l in range(64):
+                if op == "v_permlane32_swap_b32" and l >= 32:
+                    va[l], vb[l - 32] = V[b][l - 32], V[a][l]
+                elif op == "v_permlane16_swap_b32" and (l >> 4) & 1:
+                    va[l], vb[l - 16] = V[b][l - 16], V[a][l]
+            V[a], V[b] = va, vb
             return None
         if op == "v_readfirstlane_b32":
             w.s[int(t[0][1:])] = int(V[int(t[1][1:])][0])
@@ -432,10 +455,10 @@ def d0(t):
     return int(t[0][1:])
 
 
-def run_kernel(asm_text, name, mem, kernarg, grid, wgs=None):
+def run_kernel(asm_text, name, mem, kernarg, grid, wgs=None, lds_alloc=131072):
     code, labels = parse_kernel(asm_text, name)
     for wg in (range(grid) if wgs is None else wgs):
-        Workgroup(code, labels, mem, kernarg, wg).run()
+        Workgroup(code, labels, mem, kernarg, wg, lds_alloc=lds_alloc).run()
 
 
 def selftest(asm_path):
@@ -554,6 +577,66 @@ def selftest_qkv(text, col=True, T=257, S=16, H=4, B=2, K=1024, grid=8, wgs=None
     err = float(np.abs(gotf[:, :, st] - ref[:, :, st]).max() / np.abs(ref).max())
     print(f"qkv col={col} T={T} S={S} H={H} B={B}: max_rel_err {err:.2e}")
     return err < 1.5e-2
+
+
+def gelu_and_grad_ref(x):
+    from math import erf, exp, pi, sqrt
+    xf = x.ravel().astype(np.float64)
+    cdf = np.array([0.5 * (1 + erf(v / sqrt(2))) for v in xf])
+    pdf = np.exp(-0.5 * xf * xf) / sqrt(2 * pi)
+    return (xf * cdf).reshape(x.shape), (cdf + xf * pdf).reshape(x.shape)
+
+
+def selftest_geglu_bwd(text, M=2560, F=256, K=1024, grid=8, wgs=(0, 1, 2)):
+    """dh = GEGLU backward of du = bf16(dy W2) against the pre-activation a; part = 128-row column sums.
+    M = 2560, F = 256: 10 tiles on 8 workgroups -- workgroups 0 and 1 walk two (the deferred path), 2 one."""
+    rng = np.random.default_rng(3)
+    dy = f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
+    w2t = f32_to_bf16((rng.standard_normal((F, K)) * 0.03).astype(np.float32))
+    a = f32_to_bf16(rng.standard_normal((M, 2 * F)).astype(np.float32))
+    mem = Memory()
+    pa, pb = mem.alloc(dy, "dy"), mem.alloc(w2t, "w2t")
+    pc = mem.alloc(np.zeros((M, 2 * F), dtype=np.uint16), "dh")
+    ph = mem.alloc(a, "a")
+    pp = mem.alloc(np.full((M // 128, 2 * F), np.nan, dtype=np.float32), "part")
+    nt = (M // 256) * (F // 256)
+    ka = struct.pack("<6Q16i", pa, pb, pc, ph, pp, 0, M, F, K, K, K, 2 * F, F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
+    run_kernel(text, "dalle_gemm_nt_geglu_bwd", mem, ka, grid, list(wgs), lds_alloc=163840)
+    dh = bf16_to_f32(mem.get(pc, np.uint16, (M, 2 * F)))
+    part = mem.get(pp, np.float32, (M // 128, 2 * F))
+    du = bf16_to_f32(f32_to_bf16(bf16_to_f32(dy) @ bf16_to_f32(w2t).T)).astype(np.float64)
+    af = bf16_to_f32(a).astype(np.float64)
+    ge, gr = gelu_and_grad_ref(af[:, F:])
+    ref = np.concatenate([du * ge, du * af[:, :F] * gr], 1)
+    ok = True
+    errs, perrs = [], []
+    for wg in wgs:
+        tile = (wg % 8) * (grid // 8) + wg // 8
+        while tile < nt:
+            tm, tn = tile_of_wg_id(tile, M // 256, F // 256)
+            rows = slice(tm * 256, tm * 256 + 256)
+            for c0 in (tn * 256, F + tn * 256):
+                cols = slice(c0, c0 + 256)
+                errs.append(np.abs(dh[rows, cols] - ref[rows, cols]).max())
+                for blk in range(2):
+                    rb = slice(tm * 256 + 128 * blk, tm * 256 + 128 * blk + 128)
+                    psum = ref[rb, cols].sum(0)
+                    perrs.append(np.abs(part[tm * 2 + blk, cols] - psum).max() / (np.abs(psum).max() + 1e-6))
+            tile += grid
+    err = float(max(errs) / np.abs(ref).max())
+    perr = float(max(perrs))
+    print(f"geglu_bwd M={M} F={F} wgs={list(wgs)}: dh max_rel_err {err:.2e}, column sums {perr:.2e}")
+    return err < 1e-2 and perr < 2e-2
+
+
+def tile_of_wg_id(tile, tiles_m, tiles_n):
+    full = (tiles_m & ~7) * tiles_n
+    if tile < full:
+        g, w = divmod(tile, 8 * tiles_n)
+        return 8 * g + w % 8, w // 8
+    rem = tiles_m & 7
+    w = tile - full
+    return (tiles_m & ~7) + w % rem, w // rem
 
 
 def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):

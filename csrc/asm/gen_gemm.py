@@ -260,7 +260,7 @@ STORE_SLOTS = [3 + 4 * n for n in range(8)]                   # deferred epilogu
 
 
 def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), head=(), work=(), work_span=(40, 120),
-              work2=(), work2_span=(60, 118)):
+              work2=(), work2_span=(60, 118), at=()):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
     ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
@@ -271,7 +271,8 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     this step's B3 that B3 need not wait for (issued by the caller between the previous step and this one;
     every VMEM instruction this step places before B3 is counted here).  ``head``: instructions before MFMA 0;
     ``work``: instructions spread in order over the MFMA gaps of ``work_span`` (a fused epilogue's deferred
-    work; its VMEM must sit before the step's last DMA).  Returns this step's VMEM instructions in issue order.
+    work; its VMEM must sit before the step's last DMA); ``at``: (slot, instruction) pairs placed exactly.
+    Returns this step's VMEM instructions in issue order.
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
     m1 = mfma_list(SET1_A, SET1_B, False)
@@ -309,6 +310,8 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
             assert hi <= 120
             for n, ins in enumerate(wk):
                 slots[lo + n * (hi - lo) // len(wk)].append(ins)
+    for n, ins in at:
+        slots[n].append(ins)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
     if dma and (SPLIT or TN):
         # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
@@ -350,12 +353,17 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
         # MFMA 0 of the next step needs A0 / B0 (the first two of these 16 reads)
         slots[127].append("s_waitcnt lgkmcnt(0)" if TN else f"s_waitcnt lgkmcnt({16 - 2})")
     # deferred-work markers "@vmwait:TAG": wait until the VMEM instruction(s) tagged "; @TAG" (placed
-    # earlier in this step) have completed -- vmcnt(number of VMEM instructions issued after the last one)
+    # earlier in this step) have completed -- vmcnt(number of VMEM instructions issued after the last one);
+    # "@vmwait_prev:K": until a VMEM instruction of an EARLIER step followed by K others there has completed
     order = [(n, k) for n in range(128) for k in range(len(slots[n]))]
     vm_seen = []
     for n, k in order:
         ins = slots[n][k]
-        if ins.startswith("@vmwait:"):
+        if ins.startswith("@vmwait_prev:"):
+            cnt = int(ins.split(":", 1)[1]) + len(vm_seen)
+            assert cnt < 64
+            slots[n][k] = f"s_waitcnt vmcnt({cnt})"
+        elif ins.startswith("@vmwait:"):
             tag = ins.split(":", 1)[1]
             last = max(i for i, x in enumerate(vm_seen) if x.endswith("; @" + tag))
             slots[n][k] = f"s_waitcnt vmcnt({len(vm_seen) - 1 - last})"
@@ -765,6 +773,7 @@ def set_srd(e, srd, ptr, row0, ld, nr):
 
 
 KERNARG_SIZE = 112
+LDS_BYTES = {}          # kernels that use LDS beyond the two operand stages
 
 
 def metadata(name):
@@ -784,7 +793,7 @@ def metadata(name):
     return f"""  - .agpr_count:     256
     .args:
 {chr(10).join(args)}
-    .group_segment_fixed_size: {2 * STAGE}
+    .group_segment_fixed_size: {LDS_BYTES.get(name, 2 * STAGE)}
     .kernarg_segment_align: 8
     .kernarg_segment_size: {KERNARG_SIZE}
     .max_flat_workgroup_size: 256
@@ -805,7 +814,7 @@ def descriptor(name):
     return f"""	.section	.rodata,"a",@progbits
 	.p2align	6, 0x0
 	.amdhsa_kernel {name}
-		.amdhsa_group_segment_fixed_size {2 * STAGE}
+		.amdhsa_group_segment_fixed_size {LDS_BYTES.get(name, 2 * STAGE)}
 		.amdhsa_private_segment_fixed_size 0
 		.amdhsa_kernarg_size {KERNARG_SIZE}
 		.amdhsa_user_sgpr_count 2
@@ -1552,8 +1561,329 @@ def kernel_qkv(name, col):
     return e.text()
 
 
+# ----------------------------------------------------------------------------------------------------
+# FF-out dgrad + GEGLU backward: du = dy W2 (M x F; A = dy (M x K), B = W2^T (F x K), K = 1024), then with the
+# FF-in pre-activation a (M x 2F, [value | gate], aux0):  da_value = du gelu(gate), da_gate = du value gelu'(gate)
+# into dh (M x 2F, C; ldc = 2F, ld_aux = F), and the FF-in bias gradient's column sums per 128-row block into
+# part (M / 128 x 2F fp32, aux1; the host folds it).  du is rounded to bf16 first, as the unfused path stores
+# it.  Each lane's row-group (8 consecutive du columns of one row) needs the same 8 columns of a's value and
+# gate halves: two 16-byte loads, two 16-byte stores, no exchange.  The GEGLU backward is VALU-heavy (~27
+# instructions per element), so it runs under the successor tile's MFMAs: 7 row-groups at the tile boundary,
+# 17 with du packed in v[144:211] and 8 with du in the LDS above the two operand stages (32 KB), processed two
+# per successor K-step 0..13 (unrolled: K = 1024) with their `a` chunks loaded one K-step ahead (two banks of
+# 16 VGPRs).  Column sums: each element's (da, dg) pair is folded over lanes g, g + 2 by v_permlane32_swap into
+# 8 running sums; at the tile's end v_permlane16_swap folds g, g + 1 and each lane stores 4 of the 128-row
+# block's sums (16 bytes).
+# ----------------------------------------------------------------------------------------------------
+GB_STASH, GB_LDS = 17, 8
+GB_IMM = 32 - GB_STASH - GB_LDS                 # 7 row-groups processed at the tile boundary
+V_GBANK = 212                                   # a chunks of the next K-step's row-groups: 2 sets x 2 x 8 VGPRs
+V_GSUM = 244                                    # 8 fp32 column sums
+V_GDA = 252                                     # da0 da1 dg0 dg1
+V_GCOG, V_GPO, V_GLDS = 13, 14, 0               # gate chunk offset, part offset, LDS stash base (over v0)
+GX = (10, 11, 12, 15)                           # temps
+S_SRDAA, S_SRDP = S_SRDX, 84                    # a / part resources of the finishing tile
+S_GSOF = (88, 89)
+S_GMASK, S_GPR, S_GNH, S_GC2, S_GF = 90, 91, 92, 93, 94
+LDS_GB = 2 * STAGE
+LDS_BYTES["dalle_gemm_nt_geglu_bwd"] = LDS_GB + 256 * 16 * GB_LDS       # 160 KB: the whole LDS
+
+
+def fix_valu_hazards(seq):
+    """fix_trans_hazards, plus gfx950's two wait states between a VALU write and a v_permlane*_swap reading
+    (and rewriting) that VGPR"""
+    seq = fix_trans_hazards(seq)
+    out = []
+    for ins in seq:
+        if ins.startswith("v_permlane"):
+            regs = [x.strip() for x in ins.split(None, 1)[1].split(",")]
+            waits = 0
+            for prev in reversed(out):
+                if prev.startswith("s_nop"):
+                    waits += int(prev.split()[1]) + 1
+                    continue
+                if prev.startswith("v_") and prev.split(None, 1)[1].split(",")[0].strip() in regs:
+                    if waits < 2:
+                        out.append(f"s_nop {1 - waits}")
+                    break
+                waits += 1
+                if waits >= 2:
+                    break
+        out.append(ins)
+    return out
+
+
+def gb_load(idx, bank, sof, tag):
+    """the row-group's value / gate chunks of `a` into v[bank:bank+7]"""
+    i, r = divmod(idx, 4)
+    return [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}",
+            f"buffer_load_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDAA, 4)}, s{sof} offen ; @{tag}",
+            f"buffer_load_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDAA, 4)}, s{sof} offen ; @{tag}"]
+
+
+def gb_compute(idx, du, bank, sof):
+    """da / dg of the row-group (du packed bf16 in v[du:du+3], a's value / gate chunks in v[bank:bank+7]) into
+    v[bank:bank+7], stored; the pair-folded values added to the column sums"""
+    x, x1, x2, x3 = GX
+    c = GE_CONSTS
+    out = []
+    unpack = lambda dst, src, h: (f"v_and_b32 v{dst}, 0xffff0000, v{src}" if h else f"v_lshlrev_b32 v{dst}, 16, v{src}")
+    for k2 in range(4):
+        for h in range(2):
+            da, dg = V_GDA + h, V_GDA + 2 + h
+            out += [unpack(x, bank + 4 + k2, h),                               # gate
+                    f"v_fma_f32 v{x1}, |v{x}|, s{S_GPR}, 1.0",                  # 1 + p |x| / sqrt2
+                    f"v_rcp_f32 v{x1}, v{x1}",                                   # t
+                    f"v_mul_f32 v{x3}, s{S_GNH}, v{x}",
+                    f"v_mul_f32 v{x2}, {c['a5']:#x}, v{x1}",
+                    f"v_add_f32 v{x2}, {c['a4']:#x}, v{x2}",
+                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a3']:#x}",
+                    f"v_mul_f32 v{x3}, v{x3}, v{x}",                             # -x^2 / 2 * log2 e
+                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a2']:#x}",
+                    f"v_exp_f32 v{x3}, v{x3}",                                   # exp(-x^2 / 2)
+                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a1']:#x}",
+                    f"v_mul_f32 v{x2}, v{x2}, v{x1}",                            # poly
+                    f"v_fma_f32 v{x1}, -v{x2}, v{x3}, 1.0",                      # |erf|
+                    f"v_bfi_b32 v{x1}, s{S_GMASK}, v{x1}, v{x}",                  # copysign(., x)
+                    f"v_fma_f32 v{x1}, 0.5, v{x1}, 0.5",                          # cdf
+                    f"v_mul_f32 v{x2}, s{S_GC2}, v{x}",
+                    f"v_fma_f32 v{x2}, v{x2}, v{x3}, v{x1}",                      # gelu' = cdf + x pdf
+                    f"v_mul_f32 v{x1}, v{x}, v{x1}",                              # gelu
+                    unpack(x3, du + k2, h),                                       # du
+                    f"v_mul_f32 v{da}, v{x3}, v{x1}",
+                    unpack(x, bank + k2, h),                                      # value
+                    f"v_mul_f32 v{x2}, v{x2}, v{x}",
+                    f"v_mul_f32 v{dg}, v{x3}, v{x2}"]
+        out += [f"v_cvt_pk_bf16_f32 v{bank + k2}, v{V_GDA}, v{V_GDA + 1}",
+                f"v_cvt_pk_bf16_f32 v{bank + 4 + k2}, v{V_GDA + 2}, v{V_GDA + 3}"]
+        for h in range(2):
+            da, dg, sm = V_GDA + h, V_GDA + 2 + h, V_GSUM + 2 * k2 + h
+            out += [f"v_permlane32_swap_b32 v{da}, v{dg}",                        # lanes < 32: da (g, g + 2)
+                    f"v_add_f32 v{sm}, v{sm}, v{da}",                             # lanes >= 32: dg
+                    f"v_add_f32 v{sm}, v{sm}, v{dg}"]
+    i, r = divmod(idx, 4)
+    out += [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}",
+            f"buffer_store_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDC, 4)}, s{sof} offen",
+            f"buffer_store_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDC, 4)}, s{sof} offen"]
+    return fix_valu_hazards(out)
+
+
+def gb_finish():
+    """fold the sums over lanes g, g + 1 and store this lane's 4 of them; zero the sums for the next tile"""
+    out = ["s_nop 1"]
+    for k in range(4):
+        out += [f"v_permlane16_swap_b32 v{V_GSUM + k}, v{V_GSUM + 4 + k}",
+                f"v_add_f32 v{V_GSUM + k}, v{V_GSUM + k}, v{V_GSUM + 4 + k}"]
+    out.append(f"buffer_store_dwordx4 {vr(V_GSUM)}, v{V_GPO}, {sr(S_SRDP, 4)}, 0 offen")
+    out += [f"v_mov_b32 v{V_GSUM + 4 + k}, 0" for k in range(4)] + [f"v_mov_b32 v{V_GSUM + k}, 0" for k in range(4)]
+    return fix_valu_hazards(out)
+
+
+def gb_lane_setup(e):
+    """gate chunk offset, part offset, LDS stash base; zero sums.  The sums' lanes after both folds:
+    (lane >> 5) selects value / gate columns, (lane >> 4) & 1 the upper 4 of the lane's 8 columns."""
+    T0, T1 = V_T, V_T + 1
+    e(f"s_lshl_b32 s{S_T0}, s{S_GF}, 1")
+    e(f"v_add_u32 v{V_GCOG}, s{S_T0}, v{V_CO}")              # + F columns * 2 bytes
+    # part: wm ldc 4 + (lane >> 5) F 4 + (128 wn + 8 c + 4 ((lane >> 4) & 1)) 4
+    e(f"v_and_b32 v{T0}, 15, v{V_TID}")
+    e(f"v_lshlrev_b32 v{V_GPO}, 5, v{T0}")                    # 8 c * 4
+    e(f"v_lshrrev_b32 v{T0}, 4, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 1, v{T0}")
+    e(f"v_lshl_add_u32 v{V_GPO}, v{T0}, 4, v{V_GPO}")
+    e(f"v_lshrrev_b32 v{T0}, 5, v{V_TID}")
+    e(f"v_and_b32 v{T0}, 1, v{T0}")
+    e(f"s_lshl_b32 s{S_T0}, s{S_GF}, 2")
+    e(f"v_mul_lo_u32 v{T0}, v{T0}, s{S_T0}")
+    e(f"v_add_u32 v{V_GPO}, v{V_GPO}, v{T0}")
+    e(f"s_and_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 9")                     # 128 wn * 4
+    e(f"v_add_u32 v{V_GPO}, s{S_T0}, v{V_GPO}")
+    e(f"s_lshr_b32 s{S_T0}, s{S_WAVE}, 1")
+    e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_LDC}")
+    e(f"s_lshl_b32 s{S_T0}, s{S_T0}, 2")                     # wm ldc * 4
+    e(f"v_add_u32 v{V_GPO}, s{S_T0}, v{V_GPO}")
+    e(f"v_lshlrev_b32 v{V_GLDS}, 4, v{V_TID}")
+    e(f"v_add_u32 v{V_GLDS}, {LDS_GB}, v{V_GLDS}")           # + 16 tid (v0 is not needed past here)
+    for k in range(8):
+        e(f"v_mov_b32 v{V_GSUM + k}, 0")
+
+
+def gb_setup_tile():
+    """(penult's MFMA gaps) dh, a and part resources of the finishing tile"""
+    out = []
+    for srd, ptr in ((S_SRDC, S_C), (S_SRDAA, S_AUX0)):
+        out += [f"s_mul_i32 s{S_T0}, s{S_ROW0}, s{S_LDC}", f"s_mul_hi_u32 s{S_T1}, s{S_ROW0}, s{S_LDC}",
+                f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}", f"s_addc_u32 s{S_T1}, s{S_T1}, 0",
+                f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 1",
+                f"s_add_u32 s{srd}, s{ptr}, s{S_T0}", f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{S_T1}",
+                f"s_lshl_b32 s{srd + 2}, s{S_LDC2}, 8", f"s_mov_b32 s{srd + 3}, 0x20000"]
+    out += [f"s_lshr_b32 s{S_T0}, s{S_ROW0}, 7", f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_LDC}",
+            f"s_add_u32 s{S_T0}, s{S_T0}, s{S_COL0}", f"s_mov_b32 s{S_T1}, 0",
+            f"s_lshl_b64 s[{S_T0}:{S_T1}], s[{S_T0}:{S_T1}], 2",
+            f"s_add_u32 s{S_SRDP}, s{S_AUX1}, s{S_T0}", f"s_addc_u32 s{S_SRDP + 1}, s{S_AUX1 + 1}, s{S_T1}",
+            f"s_lshl_b32 s{S_SRDP + 2}, s{S_LDC}, 3", f"s_mov_b32 s{S_SRDP + 3}, 0x20000"]
+    return out
+
+
+def gb_plan():
+    """deferred row-groups per successor K-step: (idx, du location) with location ('v', reg) or ('l', k)"""
+    deferred = [(GB_IMM + s, ("v", V_STASH + 4 * s)) for s in range(GB_STASH)] + \
+               [(GB_IMM + GB_STASH + k, ("l", k)) for k in range(GB_LDS)]
+    per = [2] * 11 + [1] * 3
+    assert sum(per) == len(deferred)
+    plan, k = [], 0
+    for n in per:
+        plan.append(deferred[k:k + n])
+        k += n
+    return plan
+
+
+def kernel_geglu_bwd(name):
+    e = Emitter(name)
+    e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")
+    e(f"s_load_dwordx2 {sr(S_AUX1, 2)}, s[0:1], 0x20")
+    e(f"s_load_dwordx8 {sr(S_M, 8)}, s[0:1], 0x30")
+    e(f"s_load_dword s{S_GRID}, s[0:1], 0x50")
+    e(f"s_load_dword s{S_GF}, s[0:1], 0x54")
+    e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+    e("s_nop 1")
+    e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+    e("s_nop 1")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
+    e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
+    e(f"s_mov_b32 s{S_GMASK}, 0x7fffffff")
+    e(f"s_mov_b32 s{S_GPR}, 0x3e6d3388")                 # 0.3275911 / sqrt 2
+    e(f"s_mov_b32 s{S_GNH}, {GE_CONSTS['nhl2e']:#x}")     # -log2(e) / 2
+    e(f"s_mov_b32 s{S_GC2}, 0x3ecc422a")                 # 1 / sqrt(2 pi)
+    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
+    e("s_cbranch_scc0 " + e.L("end"))
+    lane_setup(e, "plain")
+    gb_lane_setup(e)
+    e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
+    e(f"s_lshr_b32 s{S_T1}, s{S_GRID}, 3")
+    e(f"s_mul_i32 s{S_T0}, s{S_T0}, s{S_T1}")
+    e(f"s_lshr_b32 s{S_T1}, s{S_WG}, 3")
+    e(f"s_add_u32 s{S_TILE}, s{S_T0}, s{S_T1}")
+    e(f"s_cmp_lt_u32 s{S_TILE}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("end"))
+    tile_order_setup(e)
+    stagger_setup(e)
+    emit_all(e, tile_coords())
+    setup_operands(e)
+    prologue_dma(e)
+    e("s_waitcnt vmcnt(16)")
+    e("s_barrier")
+    body_head(e, "plain", 0)
+    iteration(e, "first", None, 0)
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
+    e.label(e.L("kloop"))
+    iteration(e, "loop")
+    e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc0 " + e.L("kloop"))
+    e.label(e.L("tail"))
+    pre_out = gb_setup_tile()
+    sub = Emitter(e.prefix)
+    setup_operands(sub)
+    pre_next = pre_out + next_tile() + [l.strip() for l in sub.lines]
+    imm_loads = []
+    for idx in range(GB_IMM):
+        imm_loads += gb_load(idx, V_STASH + 8 * idx, S_GSOF[idx % 2], "imm")
+    plan = gb_plan()
+
+    def bank_of(t, b):
+        return V_GBANK + 16 * (t % 2) + 8 * b
+
+    def loads_for(t):
+        out = []
+        for b, (idx, _) in enumerate(plan[t]):
+            out += gb_load(idx, bank_of(t, b), S_GSOF[b], f"bk{t}")
+        return out
+
+    def after_last(vm, tag):
+        return len(vm) - 1 - max(k for k, ins in enumerate(vm) if ins.endswith("; @" + tag))
+
+    def boundary_imm(vm_pen, vm_last):
+        e(f"s_waitcnt vmcnt({after_last(vm_pen, 'imm') + len(vm_last)})")   # the immediate row-groups' a chunks
+        n = 0
+        for idx in range(GB_IMM):
+            i, r = divmod(idx, 4)
+            t = V_ETMP + (idx % 4) * 12
+            pack_row(e, "plain", i, r, t, t + 8)
+            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * idx, S_GSOF[idx % 2]))
+            n += 2
+        return n
+
+    e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
+    e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
+    e("s_cbranch_scc0 " + e.L("final"))
+    # ---- successor: 7 row-groups now, 25 under its K-steps 0..13 ----
+    vm_pen = iteration(e, "penult", None, prefetch=True, pre=pre_next, work=imm_loads, work_span=(20, 60))
+    vm_last = iteration(e, "last", None, prefetch=True, work=loads_for(0), work_span=(1, 8))
+    tile_boundary(e)
+    n_st = boundary_imm(vm_pen, vm_last)
+    for idx in range(GB_IMM, 32):
+        i, r = divmod(idx, 4)
+        t = V_ETMP + (idx % 4) * 12
+        if idx < GB_IMM + GB_STASH:
+            pack_row(e, "plain", i, r, t, V_STASH + 4 * (idx - GB_IMM))
+        else:
+            pack_row(e, "plain", i, r, t, t + 8)
+            e(f"ds_write_b128 v{V_GLDS}, {vr(t + 8)} offset:{4096 * (idx - GB_IMM - GB_STASH)}")
+    e(f"s_waitcnt vmcnt({len(vm_last) + n_st})")         # the successor's step 0 landed
+    e("s_barrier")
+    body_head(e, "plain", 0)
+    prev_wait = after_last(vm_last, "bk0") + n_st
+    for t in range(14):
+        work = loads_for(t + 1) if t + 1 < 14 else []
+        at = []
+        if t + 1 < 14:
+            lds_next = [(idx, loc) for idx, loc in plan[t + 1] if loc[0] == "l"]
+            for n, (idx, loc) in enumerate(lds_next):
+                # into the du registers of an already processed VGPR-stashed row-group
+                at.append((47 + n, f"ds_read_b128 {vr(V_STASH + 4 * loc[1])}, v{V_GLDS} offset:{4096 * loc[1]}"))
+            if lds_next:
+                at.append((62, "s_waitcnt lgkmcnt(0)"))
+        comp = [f"@vmwait_prev:{prev_wait}"]
+        for b, (idx, loc) in enumerate(plan[t]):
+            du = loc[1] if loc[0] == "v" else V_STASH + 4 * loc[1]
+            comp += gb_compute(idx, du, bank_of(t, b), S_GSOF[b])
+        if t == 13:
+            comp += gb_finish()
+        vm = iteration(e, "first" if t == 0 else "loop", None, n_st if t == 0 else 0, work=work, work_span=(1, 6),
+                       work2=comp, work2_span=(8, 120), at=at)
+        if work:
+            prev_wait = after_last(vm, f"bk{t + 1}")
+    e("s_branch " + e.L("tail"))
+    # ---- no successor: 7 row-groups, then the other 25 in three load batches ----
+    e.label(e.L("final"))
+    vm_pen = iteration(e, "penult", None, pre=pre_out, work=imm_loads, work_span=(20, 60))
+    vm_last = iteration(e, "last", None)
+    for _ in range(3):
+        e("s_nop 7")
+    boundary_imm(vm_pen, vm_last)
+    rest = list(range(GB_IMM, 32))
+    for batch in (rest[:9], rest[9:17], rest[17:]):
+        for n, idx in enumerate(batch):
+            emit_all(e, gb_load(idx, V_STASH + 8 * n, S_GSOF[n % 2], "f"))
+        e("s_waitcnt vmcnt(0)")
+        for n, idx in enumerate(batch):
+            i, r = divmod(idx, 4)
+            t = V_ETMP + (n % 4) * 12
+            pack_row(e, "plain", i, r, t, t + 8)
+            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * n, S_GSOF[n % 2]))
+    emit_all(e, gb_finish())
+    e.label(e.L("end"))
+    e("s_waitcnt vmcnt(0)")
+    e("s_endpgm")
+    return e.text()
+
+
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None),
-           ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1)]
+           ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
+           ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent")]
 
@@ -1569,6 +1899,8 @@ def main(out, diag=False):
             parts.append(kernel_geglu(name, dg))
         elif epi == "qkv":
             parts.append(kernel_qkv(name, dg))
+        elif epi == "geglu_bwd":
+            parts.append(kernel_geglu_bwd(name))
         else:
             parts.append(kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")

@@ -417,6 +417,30 @@ std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optiona
   return {dh, db};
 }
 
+// The same on the assembly kernel (csrc/asm/gen_gemm.py kernel_geglu_bwd): K = 1024, M and F multiples of 256
+std::vector<Tensor> asm_ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == torch::kBFloat16 && w2t.scalar_type() == torch::kBFloat16, "asm_ff_dgrad_geglu: bf16");
+  CHECK_IN(h, torch::kBFloat16);
+  TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2 && dy.stride(1) == 1 && w2t.stride(1) == 1, "asm_ff_dgrad_geglu: 2-D, K-contiguous");
+  const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
+  TORCH_CHECK(w2t.size(1) == K && h.size(0) == M && h.size(1) == 2 * F, "asm_ff_dgrad_geglu: shape mismatch");
+  TORCH_CHECK(K == 1024 && M % 256 == 0 && F % 256 == 0, "asm_ff_dgrad_geglu: K = 1024, M and F multiples of 256");
+  auto dh = torch::empty_like(h);
+  auto part = torch::empty({M / 128, 2 * F}, h.options().dtype(torch::kFloat32));
+  float* pb = sink_ptr(gb, 2 * F, "asm_ff_dgrad_geglu dbias");
+  Tensor db;
+  if (!pb) {
+    db = torch::empty({2 * F}, h.options().dtype(torch::kFloat32));
+    pb = db.data_ptr<float>();
+  }
+  TORCH_CHECK(dalle::asm_gemm_nt("dalle_gemm_nt_geglu_bwd", dy.data_ptr(), w2t.data_ptr(), dh.data_ptr(), h.data_ptr(), part.data_ptr(),
+                                 nullptr, (int)M, (int)F, (int)K, (int)dy.stride(0), (int)w2t.stride(0), (int)(2 * F), (int)F, 0,
+                                 cur_stream()), "asm_ff_dgrad_geglu: launch failed");
+  dalle::column_sum(part.data_ptr<float>(), M / 128, 2 * F, dalle::GradSink{pb, nullptr, nullptr, (int)(2 * F), db.defined() ? 0 : 1},
+                    cur_stream());
+  return {dh, db};
+}
+
 void scale_residual_(Tensor x, Tensor y, Tensor scale) {
   CHECK_IN(x, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
   const long D = x.size(-1);
@@ -1289,6 +1313,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("asm_qkv_rope", &asm_qkv_rope, py::arg("h"), py::arg("w"), py::arg("cs3"), py::arg("T"), py::arg("S"), py::arg("H"),
         py::arg("n"), py::arg("col_major"));
   m.def("asm_ff_in_geglu", &asm_ff_in_geglu, py::arg("x"), py::arg("w1p"), py::arg("b1p"));
+  m.def("asm_ff_dgrad_geglu", &asm_ff_dgrad_geglu, py::arg("dy"), py::arg("w2t"), py::arg("h"), py::arg("gb") = py::none());
   m.def("asm_wgrad_", &asm_wgrad_, py::arg("out"), py::arg("A"), py::arg("B"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_pt", &gemm_pt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0, py::arg("group") = 0);
   m.def("qkv_rope_pt", &qkv_rope_pt, py::arg("h"), py::arg("w"), py::arg("cs"), py::arg("T"), py::arg("S"), py::arg("H"),

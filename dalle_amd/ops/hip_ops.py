@@ -686,7 +686,13 @@ def _ff_core_bwd(saved, params, dy, sk):
     ln_w, ln_b, w1, b1, w2, b2, scale = params
     dy = dy.view(-1, dy.shape[-1])
     M, F = dy.shape[0], w2b.shape[1]
-    if M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
+    if ASM_GEMM and M % 256 == 0 and F % 256 == 0 and dy.shape[1] == 1024 and dy.stride(1) == 1:
+        # du = dy W2 on the assembly GEMM, the GEGLU backward + b1 column sums under the next tile's K-steps
+        da, db1 = C().asm_ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
+        _count("ff_dgrad_geglu")
+        _count("asm_ff_dgrad_geglu")
+        dw2 = weight_grad(w2, saved_gemm_input(dy, WGRAD_GT), u)
+    elif M % 256 == 0 and F % 256 == 0 and dy.shape[1] % 64 == 0:
         # du = dy W2 on the hand-written GEMM with the GEGLU backward + b1 grad in its epilogue
         da, db1 = C().ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
         _count("ff_dgrad_geglu")

@@ -30,7 +30,11 @@ def test_asm_gemm_builds(tmp_path):
     for name, _, _ in gen_gemm.KERNELS:
         assert f".name:           {name}" in notes
     assert notes.count(".vgpr_count:     512") == len(gen_gemm.KERNELS)
-    assert notes.count(".group_segment_fixed_size: 131072") == len(gen_gemm.KERNELS)
+    for name, _, _ in gen_gemm.KERNELS:   # two 64 KB operand stages; the GEGLU backward also its 32 KB stash
+        lds = gen_gemm.LDS_BYTES.get(name, 131072)
+        assert lds <= 160 * 1024
+    assert notes.count(".group_segment_fixed_size: 131072") == len(gen_gemm.KERNELS) - len(gen_gemm.LDS_BYTES)
+    assert notes.count(".group_segment_fixed_size: 163840") == len(gen_gemm.LDS_BYTES)
     # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads, 3 barriers in the loop body
     # (A image released, B image released, next step landed)
     body = text.split("dalle_gemm_nt_plain_kloop:")[1].split("s_cbranch_scc0")[0]
@@ -103,3 +107,18 @@ def test_kernels_on_the_emulator(tmp_path):
     ref = emu.bf16_to_f32(Ab) @ emu.bf16_to_f32(Bb).T
     got = emu.bf16_to_f32(mem.get(pc, np.uint16, (M, N)))
     assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-2
+
+
+def test_fused_epilogue_kernels_on_the_emulator(tmp_path):
+    """The FF-out dgrad + GEGLU backward kernel on the emulator: one workgroup walking two tiles, so both the
+    deferred path (row-groups at the boundary, in VGPRs and in LDS, processed under the successor's K-steps,
+    permlane-folded column sums) and the final path run; and the QKV + rotary kernel's first workgroup."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import emu
+    import gen_gemm
+
+    s = tmp_path / "g.s"
+    gen_gemm.main(str(s))
+    text = s.read_text()
+    assert emu.selftest_geglu_bwd(text, M=2560, F=256, grid=8, wgs=(0,))
+    assert emu.selftest_qkv(text, col=True, T=257, S=16, H=4, B=2, grid=8, wgs=[0])

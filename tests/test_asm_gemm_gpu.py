@@ -129,3 +129,25 @@ def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B):
         assert a.shape == b.shape
         err = ((a.float() - b.float()).abs().max() / b.float().abs().max()).item()
         assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("M,F", [(512, 256), (2560, 1024), (20480, 4096)])
+def test_asm_ff_dgrad_geglu(cuda, C, M, F):
+    """FF-out dgrad + GEGLU backward + FF-in bias column sums on the assembly kernel vs fp32: du = bf16(dy W2),
+    da_value = du gelu(gate), da_gate = du value gelu'(gate) (exact erf GELU), db = column sums of (da_value,
+    da_gate). 20480 x 4096 = 1280 tiles: workgroups walk several (the deferred path)."""
+    torch.manual_seed(M + F)
+    dy = torch.randn(M, 1024, device=cuda).to(torch.bfloat16)
+    w2t = (torch.randn(F, 1024, device=cuda) * 0.03).to(torch.bfloat16)
+    h = torch.randn(M, 2 * F, device=cuda).to(torch.bfloat16)
+    dh, db = C.asm_ff_dgrad_geglu(dy, w2t, h, None)
+    du = (dy.float() @ w2t.float().t()).to(torch.bfloat16).float()
+    v, g = h.float()[:, :F], h.float()[:, F:]
+    cdf = 0.5 * (1 + torch.erf(g * 0.7071067811865476))
+    pdf = torch.exp(-0.5 * g * g) * 0.3989422804014327
+    ref = torch.cat([du * g * cdf, du * v * (cdf + g * pdf)], 1)
+    assert ((dh.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    ref_db = ref.sum(0)
+    assert ((db - ref_db).abs().max() / ref_db.abs().max()).item() < 1e-2
+    dh2, db2 = C.ff_dgrad_geglu(dy, w2t, h, None)       # the HIP kernel it replaces
+    assert ((dh.float() - dh2.float()).abs().max() / ref.abs().max()).item() < 1e-2
