@@ -167,7 +167,7 @@ def bench_geglu(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
     print(json.dumps({"shape": f"GEGLU_M{M}_F{F}_K{K}", "us": us}), flush=True)
 
 
-def bench_geglu_bwd(mod, M=163840, F=4096, K=1024, iters=10, rounds=3):
+def bench_geglu_bwd(mod, M=163840, F=4096, K=1024, iters=10, rounds=3, diag=None):
     """FF-out dgrad + GEGLU backward on the assembly kernel vs the plain GEMM of the same shape (the fused
     backward's extra cost) and the HIP 8-phase kernel it replaces (extension)"""
     dy = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
@@ -182,6 +182,9 @@ def bench_geglu_bwd(mod, M=163840, F=4096, K=1024, iters=10, rounds=3):
     args = struct.pack("<6Q16i", *ptrs, M, F, K, K, K, 2 * F, F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
     fns = {"asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", dy, w2t, du),
            "asm_geglu_bwd": lambda: mod.launch("dalle_gemm_nt_geglu_bwd", grid, args)}
+    if diag is not None:
+        for v in ("novalu", "nomem"):
+            fns[f"asm_gbwd_{v}"] = (lambda v=v: diag.launch(f"dalle_gemm_diag_gbwd_{v}", grid, args))
     try:
         sys.path.insert(0, os.path.join(HERE, ".."))
         from dalle_amd.ops.ext import load_extension
@@ -289,7 +292,8 @@ def main():
         bench_geglu(mod, rounds=a.rounds,
                     diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
     if a.geglu_bwd:
-        bench_geglu_bwd(mod, rounds=a.rounds)
+        bench_geglu_bwd(mod, rounds=a.rounds,
+                        diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
     if a.tn:
         bench_tn(mod, [(163840, 1024, 1024, 16), (163840, 3072, 1024, 16), (163840, 8192, 1024, 2),
                        (163840, 1024, 4096, 4)], rounds=a.rounds)

@@ -260,7 +260,7 @@ STORE_SLOTS = [3 + 4 * n for n in range(8)]                   # deferred epilogu
 
 
 def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), head=(), work=(), work_span=(40, 120),
-              work2=(), work2_span=(60, 118), at=()):
+              work2=(), work2_span=(60, 118), at=(), more=()):
     """one K-step.  kind: 'first' (zero-init accumulators, DMA t+2), 'loop' (DMA t+2),
     'penult' (no DMA of this tile, wait all), 'last' (no DMA of this tile, no next reads).
     ``prefetch`` (penult / last of a tile that has a successor): the stage freed at B2 receives the NEXT
@@ -271,7 +271,8 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     this step's B3 that B3 need not wait for (issued by the caller between the previous step and this one;
     every VMEM instruction this step places before B3 is counted here).  ``head``: instructions before MFMA 0;
     ``work``: instructions spread in order over the MFMA gaps of ``work_span`` (a fused epilogue's deferred
-    work; its VMEM must sit before the step's last DMA); ``at``: (slot, instruction) pairs placed exactly.
+    work; its VMEM must sit before the step's last DMA); ``work2`` / ``more`` ((list, span) pairs): the same;
+    ``at``: (slot, instruction) pairs placed exactly.
     Returns this step's VMEM instructions in issue order.
     Entry: SET0 holds this step's k-half-0 fragments (waited); the read bases point at stage X."""
     m0 = mfma_list(SET0_A, SET0_B, kind == "first")
@@ -305,7 +306,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     assert len(stores) <= len(STORE_SLOTS)
     for n, grp in enumerate(stores):
         slots[STORE_SLOTS[n]].extend(grp)
-    for wk, (lo, hi) in ((work, work_span), (work2, work2_span)):
+    for wk, (lo, hi) in ((work, work_span), (work2, work2_span)) + tuple(more):
         if wk:
             assert hi <= 120
             for n, ins in enumerate(wk):
@@ -365,8 +366,9 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
             slots[n][k] = f"s_waitcnt vmcnt({cnt})"
         elif ins.startswith("@vmwait:"):
             tag = ins.split(":", 1)[1]
-            last = max(i for i, x in enumerate(vm_seen) if x.endswith("; @" + tag))
-            slots[n][k] = f"s_waitcnt vmcnt({len(vm_seen) - 1 - last})"
+            tagged = [i for i, x in enumerate(vm_seen) if x.endswith("; @" + tag)]
+            assert tagged or GB_DIAG == "nomem", f"no VMEM tagged {tag} before its wait"
+            slots[n][k] = f"s_waitcnt vmcnt({len(vm_seen) - 1 - max(tagged)})" if tagged else "s_nop 0"
         elif ins.startswith("buffer_"):
             vm_seen.append(ins)
     mf = m0 + m1
@@ -1575,18 +1577,21 @@ def kernel_qkv(name, col):
 # 8 running sums; at the tile's end v_permlane16_swap folds g, g + 1 and each lane stores 4 of the 128-row
 # block's sums (16 bytes).
 # ----------------------------------------------------------------------------------------------------
-GB_STASH, GB_LDS = 17, 8
-GB_IMM = 32 - GB_STASH - GB_LDS                 # 7 row-groups processed at the tile boundary
-V_GBANK = 212                                   # a chunks of the next K-step's row-groups: 2 sets x 2 x 8 VGPRs
-V_GSUM = 244                                    # 8 fp32 column sums
-V_GDA = 252                                     # da0 da1 dg0 dg1
+GB_STASH, GB_LDS = 20, 8
+GB_IMM = 32 - GB_STASH - GB_LDS                 # 4 row-groups processed at the tile boundary
+V_GBANK = 224                                   # a chunks of the two row-groups in flight (A, B): 2 x 8 VGPRs
+V_GSUM = 240                                    # 8 fp32 column sums
+V_GDA = 248                                     # da0 da1 dg0 dg1
+V_GA3 = 252                                     # the polynomial's leading coefficient (fmaak needs it in a VGPR)
+GX2 = (80, 81, 82, 83)                          # second chain's temps at the tile boundary (fragment set 1)
 V_GCOG, V_GPO, V_GLDS = 13, 14, 0               # gate chunk offset, part offset, LDS stash base (over v0)
 GX = (10, 11, 12, 15)                           # temps
 S_SRDAA, S_SRDP = S_SRDX, 84                    # a / part resources of the finishing tile
 S_GSOF = (88, 89)
 S_GMASK, S_GPR, S_GNH, S_GC2, S_GF = 90, 91, 92, 93, 94
 LDS_GB = 2 * STAGE
-LDS_BYTES["dalle_gemm_nt_geglu_bwd"] = LDS_GB + 256 * 16 * GB_LDS       # 160 KB: the whole LDS
+for _n in ("dalle_gemm_nt_geglu_bwd", "dalle_gemm_diag_gbwd_novalu", "dalle_gemm_diag_gbwd_nomem"):
+    LDS_BYTES[_n] = LDS_GB + 256 * 16 * GB_LDS       # 160 KB: the whole LDS
 
 
 def fix_valu_hazards(seq):
@@ -1613,47 +1618,62 @@ def fix_valu_hazards(seq):
     return out
 
 
+GB_A = (0x3F5F5377, 0xBE761A62, 0x3FEFF2C3)    # A-S 7.1.25 a1, a2, a3, each times sqrt(2 pi)
+GB_DIAG = None          # measurement builds: "novalu" (no GELU math), "nomem" (no `a` loads / dh stores)
+
+
 def gb_load(idx, bank, sof, tag):
     """the row-group's value / gate chunks of `a` into v[bank:bank+7]"""
     i, r = divmod(idx, 4)
+    if GB_DIAG == "nomem":
+        return [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}"]
     return [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}",
-            f"buffer_load_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDAA, 4)}, s{sof} offen ; @{tag}",
-            f"buffer_load_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDAA, 4)}, s{sof} offen ; @{tag}"]
+            f"buffer_load_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDAA, 4)}, s{sof} offen nt ; @{tag}",
+            f"buffer_load_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDAA, 4)}, s{sof} offen nt ; @{tag}"]
 
 
-def gb_compute(idx, du, bank, sof):
+def gb_compute(idx, du, bank, sof, temps2=None):
     """da / dg of the row-group (du packed bf16 in v[du:du+3], a's value / gate chunks in v[bank:bank+7]) into
-    v[bank:bank+7], stored; the pair-folded values added to the column sums"""
-    x, x1, x2, x3 = GX
-    c = GE_CONSTS
+    v[bank:bank+7], stored; the pair-folded values added to the column sums.  ``temps2``: four more temps --
+    the two columns of each pair then run as two interleaved dependency chains (the tile boundary, where no
+    MFMA gaps hide the chain latency)"""
     out = []
     unpack = lambda dst, src, h: (f"v_and_b32 v{dst}, 0xffff0000, v{src}" if h else f"v_lshlrev_b32 v{dst}, 16, v{src}")
+
+    def chain(k2, h, temps):
+        x, x1, x2, x3 = temps
+        da, dg = V_GDA + h, V_GDA + 2 + h
+        if GB_DIAG == "novalu":
+            return [unpack(x3, du + k2, h), unpack(x, bank + k2, h), f"v_mul_f32 v{da}, v{x3}, v{x}",
+                    unpack(x1, bank + 4 + k2, h), f"v_mul_f32 v{dg}, v{x3}, v{x1}"]
+        # erf(|x| / sqrt2) by Abramowitz-Stegun 7.1.25 (|error| <= 2.5e-5, far below bf16 resolution) with
+        # its coefficients scaled by sqrt(2 pi), so the exponential it multiplies is the normal pdf itself
+        return [unpack(x, bank + 4 + k2, h),                                   # gate
+                f"v_fma_f32 v{x1}, |v{x}|, s{S_GPR}, 1.0",                      # 1 + p |x| / sqrt2
+                f"v_rcp_f32 v{x1}, v{x1}",                                       # t
+                f"v_mul_f32 v{x3}, s{S_GNH}, v{x}",
+                f"v_fma_f32 v{x3}, v{x3}, v{x}, s{S_GC2}",                      # log2 pdf
+                f"v_fmaak_f32 v{x2}, v{x1}, v{V_GA3}, {GB_A[1]:#x}",
+                f"v_exp_f32 v{x3}, v{x3}",                                       # pdf
+                f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {GB_A[0]:#x}",
+                f"v_mul_f32 v{x2}, v{x2}, v{x1}",                                # poly sqrt(2 pi)
+                f"v_fma_f32 v{x1}, -v{x2}, v{x3}, 1.0",                          # |erf|
+                f"v_bfi_b32 v{x1}, s{S_GMASK}, v{x1}, v{x}",                      # copysign(., x)
+                f"v_fma_f32 v{x1}, 0.5, v{x1}, 0.5",                              # cdf
+                f"v_fma_f32 v{x2}, v{x}, v{x3}, v{x1}",                           # gelu' = cdf + x pdf
+                f"v_mul_f32 v{x1}, v{x}, v{x1}",                                  # gelu
+                unpack(x3, du + k2, h),                                           # du
+                f"v_mul_f32 v{da}, v{x3}, v{x1}",
+                unpack(x, bank + k2, h),                                          # value
+                f"v_mul_f32 v{x2}, v{x2}, v{x}",
+                f"v_mul_f32 v{dg}, v{x3}, v{x2}"]
+
     for k2 in range(4):
-        for h in range(2):
-            da, dg = V_GDA + h, V_GDA + 2 + h
-            out += [unpack(x, bank + 4 + k2, h),                               # gate
-                    f"v_fma_f32 v{x1}, |v{x}|, s{S_GPR}, 1.0",                  # 1 + p |x| / sqrt2
-                    f"v_rcp_f32 v{x1}, v{x1}",                                   # t
-                    f"v_mul_f32 v{x3}, s{S_GNH}, v{x}",
-                    f"v_mul_f32 v{x2}, {c['a5']:#x}, v{x1}",
-                    f"v_add_f32 v{x2}, {c['a4']:#x}, v{x2}",
-                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a3']:#x}",
-                    f"v_mul_f32 v{x3}, v{x3}, v{x}",                             # -x^2 / 2 * log2 e
-                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a2']:#x}",
-                    f"v_exp_f32 v{x3}, v{x3}",                                   # exp(-x^2 / 2)
-                    f"v_fmaak_f32 v{x2}, v{x2}, v{x1}, {c['a1']:#x}",
-                    f"v_mul_f32 v{x2}, v{x2}, v{x1}",                            # poly
-                    f"v_fma_f32 v{x1}, -v{x2}, v{x3}, 1.0",                      # |erf|
-                    f"v_bfi_b32 v{x1}, s{S_GMASK}, v{x1}, v{x}",                  # copysign(., x)
-                    f"v_fma_f32 v{x1}, 0.5, v{x1}, 0.5",                          # cdf
-                    f"v_mul_f32 v{x2}, s{S_GC2}, v{x}",
-                    f"v_fma_f32 v{x2}, v{x2}, v{x3}, v{x1}",                      # gelu' = cdf + x pdf
-                    f"v_mul_f32 v{x1}, v{x}, v{x1}",                              # gelu
-                    unpack(x3, du + k2, h),                                       # du
-                    f"v_mul_f32 v{da}, v{x3}, v{x1}",
-                    unpack(x, bank + k2, h),                                      # value
-                    f"v_mul_f32 v{x2}, v{x2}, v{x}",
-                    f"v_mul_f32 v{dg}, v{x3}, v{x2}"]
+        c0, c1 = chain(k2, 0, GX), chain(k2, 1, temps2 or GX)
+        if temps2:
+            out += [ins for pair in zip(c0, c1) for ins in pair]
+        else:
+            out += c0 + c1
         out += [f"v_cvt_pk_bf16_f32 v{bank + k2}, v{V_GDA}, v{V_GDA + 1}",
                 f"v_cvt_pk_bf16_f32 v{bank + 4 + k2}, v{V_GDA + 2}, v{V_GDA + 3}"]
         for h in range(2):
@@ -1662,9 +1682,10 @@ def gb_compute(idx, du, bank, sof):
                     f"v_add_f32 v{sm}, v{sm}, v{da}",                             # lanes >= 32: dg
                     f"v_add_f32 v{sm}, v{sm}, v{dg}"]
     i, r = divmod(idx, 4)
-    out += [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}",
-            f"buffer_store_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDC, 4)}, s{sof} offen",
-            f"buffer_store_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDC, 4)}, s{sof} offen"]
+    out += [f"s_mul_i32 s{sof}, s{S_LDC2}, {16 * i + r}"]
+    if GB_DIAG != "nomem":
+        out += [f"buffer_store_dwordx4 {vr(bank)}, v{V_CO}, {sr(S_SRDC, 4)}, s{sof} offen nt",
+                f"buffer_store_dwordx4 {vr(bank + 4)}, v{V_GCOG}, {sr(S_SRDC, 4)}, s{sof} offen nt"]
     return fix_valu_hazards(out)
 
 
@@ -1707,6 +1728,7 @@ def gb_lane_setup(e):
     e(f"v_add_u32 v{V_GLDS}, {LDS_GB}, v{V_GLDS}")           # + 16 tid (v0 is not needed past here)
     for k in range(8):
         e(f"v_mov_b32 v{V_GSUM + k}, 0")
+    e(f"v_mov_b32 v{V_GA3}, {GB_A[2]:#x}")
 
 
 def gb_setup_tile():
@@ -1730,7 +1752,7 @@ def gb_plan():
     """deferred row-groups per successor K-step: (idx, du location) with location ('v', reg) or ('l', k)"""
     deferred = [(GB_IMM + s, ("v", V_STASH + 4 * s)) for s in range(GB_STASH)] + \
                [(GB_IMM + GB_STASH + k, ("l", k)) for k in range(GB_LDS)]
-    per = [2] * 11 + [1] * 3
+    per = [2] * 14
     assert sum(per) == len(deferred)
     plan, k = [], 0
     for n in per:
@@ -1739,7 +1761,9 @@ def gb_plan():
     return plan
 
 
-def kernel_geglu_bwd(name):
+def kernel_geglu_bwd(name, diag=None):
+    global GB_DIAG
+    GB_DIAG = diag
     e = Emitter(name)
     e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")
     e(f"s_load_dwordx2 {sr(S_AUX1, 2)}, s[0:1], 0x20")
@@ -1754,9 +1778,9 @@ def kernel_geglu_bwd(name):
     e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
     e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
     e(f"s_mov_b32 s{S_GMASK}, 0x7fffffff")
-    e(f"s_mov_b32 s{S_GPR}, 0x3e6d3388")                 # 0.3275911 / sqrt 2
+    e(f"s_mov_b32 s{S_GPR}, 0x3eaa540e")                 # 0.47047 / sqrt 2
     e(f"s_mov_b32 s{S_GNH}, {GE_CONSTS['nhl2e']:#x}")     # -log2(e) / 2
-    e(f"s_mov_b32 s{S_GC2}, 0x3ecc422a")                 # 1 / sqrt(2 pi)
+    e(f"s_mov_b32 s{S_GC2}, 0xbfa9b21d")                 # log2(1 / sqrt(2 pi))
     e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
     e("s_cbranch_scc0 " + e.L("end"))
     lane_setup(e, "plain")
@@ -1792,18 +1816,19 @@ def kernel_geglu_bwd(name):
     for idx in range(GB_IMM):
         imm_loads += gb_load(idx, V_STASH + 8 * idx, S_GSOF[idx % 2], "imm")
     plan = gb_plan()
+    banks = (V_GBANK, V_GBANK + 8)
 
-    def bank_of(t, b):
-        return V_GBANK + 16 * (t % 2) + 8 * b
+    def load(t, b, tag):
+        return gb_load(plan[t][b][0], banks[b], S_GSOF[b], tag)
 
-    def loads_for(t):
-        out = []
-        for b, (idx, _) in enumerate(plan[t]):
-            out += gb_load(idx, bank_of(t, b), S_GSOF[b], f"bk{t}")
-        return out
+    def compute(t, b):
+        idx, loc = plan[t][b]
+        du = loc[1] if loc[0] == "v" else V_STASH + 4 * loc[1]
+        return gb_compute(idx, du, banks[b], S_GSOF[b])
 
     def after_last(vm, tag):
-        return len(vm) - 1 - max(k for k, ins in enumerate(vm) if ins.endswith("; @" + tag))
+        tagged = [k for k, ins in enumerate(vm) if ins.endswith("; @" + tag)]
+        return len(vm) - 1 - max(tagged) if tagged else 0     # (none in the nomem measurement build)
 
     def boundary_imm(vm_pen, vm_last):
         e(f"s_waitcnt vmcnt({after_last(vm_pen, 'imm') + len(vm_last)})")   # the immediate row-groups' a chunks
@@ -1812,16 +1837,17 @@ def kernel_geglu_bwd(name):
             i, r = divmod(idx, 4)
             t = V_ETMP + (idx % 4) * 12
             pack_row(e, "plain", i, r, t, t + 8)
-            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * idx, S_GSOF[idx % 2]))
+            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * idx, S_GSOF[idx % 2], temps2=GX2))
             n += 2
         return n
 
     e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
     e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("final"))
-    # ---- successor: 7 row-groups now, 25 under its K-steps 0..13 ----
+    # ---- successor: 4 row-groups now, 28 under its K-steps 0..13: in step t, row-group A's `a` chunks were
+    #      loaded in step t - 1 (after its A was stored), B's at the start of step t ----
     vm_pen = iteration(e, "penult", None, prefetch=True, pre=pre_next, work=imm_loads, work_span=(20, 60))
-    vm_last = iteration(e, "last", None, prefetch=True, work=loads_for(0), work_span=(1, 8))
+    vm_last = iteration(e, "last", None, prefetch=True, work=load(0, 0, "a0"), work_span=(1, 8))
     tile_boundary(e)
     n_st = boundary_imm(vm_pen, vm_last)
     for idx in range(GB_IMM, 32):
@@ -1835,9 +1861,8 @@ def kernel_geglu_bwd(name):
     e(f"s_waitcnt vmcnt({len(vm_last) + n_st})")         # the successor's step 0 landed
     e("s_barrier")
     body_head(e, "plain", 0)
-    prev_wait = after_last(vm_last, "bk0") + n_st
+    prev_wait = after_last(vm_last, "a0") + n_st
     for t in range(14):
-        work = loads_for(t + 1) if t + 1 < 14 else []
         at = []
         if t + 1 < 14:
             lds_next = [(idx, loc) for idx, loc in plan[t + 1] if loc[0] == "l"]
@@ -1846,18 +1871,16 @@ def kernel_geglu_bwd(name):
                 at.append((47 + n, f"ds_read_b128 {vr(V_STASH + 4 * loc[1])}, v{V_GLDS} offset:{4096 * loc[1]}"))
             if lds_next:
                 at.append((62, "s_waitcnt lgkmcnt(0)"))
-        comp = [f"@vmwait_prev:{prev_wait}"]
-        for b, (idx, loc) in enumerate(plan[t]):
-            du = loc[1] if loc[0] == "v" else V_STASH + 4 * loc[1]
-            comp += gb_compute(idx, du, bank_of(t, b), S_GSOF[b])
-        if t == 13:
-            comp += gb_finish()
-        vm = iteration(e, "first" if t == 0 else "loop", None, n_st if t == 0 else 0, work=work, work_span=(1, 6),
-                       work2=comp, work2_span=(8, 120), at=at)
-        if work:
-            prev_wait = after_last(vm, f"bk{t + 1}")
+        comp_a = [f"@vmwait_prev:{prev_wait}"] + compute(t, 0)
+        next_a = load(t + 1, 0, f"a{t + 1}") if t + 1 < 14 else []
+        comp_b = [f"@vmwait:b{t}"] + compute(t, 1) + (gb_finish() if t == 13 else [])
+        vm = iteration(e, "first" if t == 0 else "loop", None, n_st if t == 0 else 0, work=load(t, 1, f"b{t}"),
+                       work_span=(1, 4), work2=comp_a, work2_span=(8, 62), at=at,
+                       more=((next_a, (63, 65)), (comp_b, (66, 120))))
+        if next_a:
+            prev_wait = after_last(vm, f"a{t + 1}")
     e("s_branch " + e.L("tail"))
-    # ---- no successor: 7 row-groups, then the other 25 in three load batches ----
+    # ---- no successor: 4 row-groups, then the other 28 in three load batches ----
     e.label(e.L("final"))
     vm_pen = iteration(e, "penult", None, pre=pre_out, work=imm_loads, work_span=(20, 60))
     vm_last = iteration(e, "last", None)
@@ -1865,7 +1888,7 @@ def kernel_geglu_bwd(name):
         e("s_nop 7")
     boundary_imm(vm_pen, vm_last)
     rest = list(range(GB_IMM, 32))
-    for batch in (rest[:9], rest[9:17], rest[17:]):
+    for batch in (rest[:10], rest[10:19], rest[19:]):
         for n, idx in enumerate(batch):
             emit_all(e, gb_load(idx, V_STASH + 8 * n, S_GSOF[n % 2], "f"))
         e("s_waitcnt vmcnt(0)")
@@ -1873,11 +1896,12 @@ def kernel_geglu_bwd(name):
             i, r = divmod(idx, 4)
             t = V_ETMP + (n % 4) * 12
             pack_row(e, "plain", i, r, t, t + 8)
-            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * n, S_GSOF[n % 2]))
+            emit_all(e, gb_compute(idx, t + 8, V_STASH + 8 * n, S_GSOF[n % 2], temps2=GX2))
     emit_all(e, gb_finish())
     e.label(e.L("end"))
     e("s_waitcnt vmcnt(0)")
     e("s_endpgm")
+    GB_DIAG = None
     return e.text()
 
 
@@ -1885,7 +1909,8 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")] + [
-    ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent")]
+    ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
+    ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem")]
 
 
 def main(out, diag=False):
@@ -1900,7 +1925,7 @@ def main(out, diag=False):
         elif epi == "qkv":
             parts.append(kernel_qkv(name, dg))
         elif epi == "geglu_bwd":
-            parts.append(kernel_geglu_bwd(name))
+            parts.append(kernel_geglu_bwd(name, dg))
         else:
             parts.append(kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
