@@ -50,9 +50,10 @@ ext_modules = [
         libraries=["c10", "torch", "torch_cpu", "torch_python", "amdhip64", "c10_hip", "torch_hip", "hipblaslt"],
         language="c++",
         extra_compile_args={
-            "cxx": ["-O3", "-std=c++17"],
-            "nvcc": ["-O3", "--offload-arch=gfx950", "-std=c++17", "-munsafe-fp-atomics"],
+            "cxx": ["-O3", "-std=c++17", "-g0"],
+            "nvcc": ["-O3", "--offload-arch=gfx950", "-std=c++17", "-munsafe-fp-atomics", "-g0"],
         },
+        extra_link_args=["-s"],   # no host debug info: 21 MB -> the ~4 MB of code and embedded code objects
     ),
 ]
 
@@ -61,7 +62,8 @@ if os.path.exists(os.path.join(ROOT, "csrc/store/kvstore.cpp")):
         CppExtension(
             "dalle_amd._kvstore",
             ["csrc/store/kvstore.cpp"],
-            extra_compile_args=["-O2", "-std=c++17"],
+            extra_compile_args=["-O2", "-std=c++17", "-g0"],
+            extra_link_args=["-s"],
         )
     )
 
