@@ -1118,9 +1118,15 @@ def fix_trans_hazards(seq):
     return out
 
 
-def ge_u(src, temps, uout):
+GE_A = (0x3EB2303A, 0xBDC45CA1, 0x3F3F7377)    # A-S 7.1.25 a1, a2, a3 (erf(z) = 1 - (a1 t + a2 t^2 + a3 t^3) e^-z^2)
+V_GEA3 = 255                         # a3 in a VGPR for v_fmaak during the successor's K-steps (the bias is back in 'last')
+V_GEA3_B = 80                        # ... and at the tile boundary (fragment set 1 is free there)
+
+
+def ge_u(src, temps, uout, va3=V_GEA3):
     """u for the lane's 4 j from the packed row-group v[src..src+3] = [v0v1, v2v3, g0g1, g2g3]:
-    value * gelu(gate) (gelu_fast of csrc/kernels/common.h: A-S 7.1.26 erf), packed into uout[0], uout[1]"""
+    value * gelu(gate), erf by Abramowitz-Stegun 7.1.25 (|error| <= 2.5e-5, far below bf16 resolution), packed
+    into uout[0], uout[1]; ``va3``: the VGPR holding a3"""
     g, v, t1, t2, t3, t4, ue = temps
     c = GE_CONSTS
     out = []
@@ -1130,23 +1136,19 @@ def ge_u(src, temps, uout):
             out += [f"v_and_b32 v{g}, 0xffff0000, v{rg_}", f"v_and_b32 v{v}, 0xffff0000, v{rv}"]
         else:
             out += [f"v_lshlrev_b32 v{g}, 16, v{rg_}", f"v_lshlrev_b32 v{v}, 16, v{rv}"]
-        out += [f"v_mul_f32_e64 v{t1}, |v{g}|, s{S_RSQ2}",              # z = |x| / sqrt2
-                f"v_fma_f32 v{t1}, v{t1}, s{S_GP}, 1.0",
-                f"v_rcp_f32 v{t1}, v{t1}",                               # t
+        out += [f"v_fma_f32 v{t1}, |v{g}|, s{S_GP}, 1.0",                     # 1 + p |x| / sqrt2
+                f"v_rcp_f32 v{t1}, v{t1}",                                   # t
                 f"v_mul_f32 v{t3}, {c['nhl2e']:#x}, v{g}",
-                f"v_mul_f32 v{t2}, {c['a5']:#x}, v{t1}",
-                f"v_add_f32 v{t2}, {c['a4']:#x}, v{t2}",
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a3']:#x}",
-                f"v_mul_f32 v{t3}, v{t3}, v{g}",                         # -x^2 / 2 * log2 e
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a2']:#x}",
-                f"v_exp_f32 v{t3}, v{t3}",                               # exp(-x^2 / 2)
-                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {c['a1']:#x}",
-                f"v_mul_f32 v{t2}, v{t2}, v{t1}",                        # poly
-                f"v_fma_f32 v{t4}, -v{t2}, v{t3}, 1.0",                  # |erf|
-                f"v_bfi_b32 v{t4}, s{S_MASK7}, v{t4}, v{g}",             # copysign(., x)
-                f"v_fma_f32 v{t4}, 0.5, v{t4}, 0.5",                     # cdf
-                f"v_mul_f32 v{t4}, v{g}, v{t4}",                         # gelu
-                f"v_mul_f32 v{t4}, v{v}, v{t4}"]                         # u
+                f"v_fmaak_f32 v{t2}, v{t1}, v{va3}, {GE_A[1]:#x}",
+                f"v_mul_f32 v{t3}, v{t3}, v{g}",                             # -x^2 / 2 * log2 e
+                f"v_fmaak_f32 v{t2}, v{t2}, v{t1}, {GE_A[0]:#x}",
+                f"v_exp_f32 v{t3}, v{t3}",                                   # exp(-x^2 / 2)
+                f"v_mul_f32 v{t2}, v{t2}, v{t1}",                            # poly
+                f"v_fma_f32 v{t4}, -v{t2}, v{t3}, 1.0",                      # |erf|
+                f"v_bfi_b32 v{t4}, s{S_MASK7}, v{t4}, v{g}",                 # copysign(., x)
+                f"v_fma_f32 v{t4}, 0.5, v{t4}, 0.5",                         # cdf
+                f"v_mul_f32 v{t4}, v{g}, v{t4}",                             # gelu
+                f"v_mul_f32 v{t4}, v{v}, v{t4}"]                             # u
         if k & 1:
             out.append(f"v_cvt_pk_bf16_f32 v{uout[k >> 1]}, v{ue}, v{t4}")
         else:
@@ -1226,9 +1228,8 @@ def kernel_geglu(name, diag=None):
     e(f"s_lshl_b32 s{S_LDC2}, s{S_LDC}, 1")
     e(f"s_lshl_b32 s{S_LDU2}, s{S_LDU}, 1")
     e(f"s_lshl_b32 s{S_F2}, s{S_LDU}, 1")               # 2 F bytes: the gate half of an `a` row (ld_aux = F)
-    e(f"s_mov_b32 s{S_GP}, 0x3ea7ba05")                  # 0.3275911
+    e(f"s_mov_b32 s{S_GP}, 0x3eaa540e")                  # 0.47047 / sqrt 2
     e(f"s_mov_b32 s{S_MASK7}, 0x7fffffff")
-    e(f"s_mov_b32 s{S_RSQ2}, {GE_CONSTS['c_rsqrt2']:#x}")
     e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
     e("s_cbranch_scc0 " + e.L("end"))
     lane_setup(e, "bias")
@@ -1268,6 +1269,7 @@ def kernel_geglu(name, diag=None):
     after_bias = len(vm) - 1 - max(i for i, ins in enumerate(vm) if ins in BIAS_LOADS)
     e(f"s_waitcnt vmcnt({after_bias})")                  # this tile's bias is in
     tile_boundary(e)
+    e(f"v_mov_b32 v{V_GEA3_B}, {GE_A[2]:#x}")
     # ---- boundary: pack every row-group (+ bias); the first N_IMMEDIATE stored and their u computed now ----
     stash = []
     n_imm_vmem = 0
@@ -1278,7 +1280,7 @@ def kernel_geglu(name, diag=None):
             pack_row(e, "bias", i, r, t, t + 8)
             seq = ge_stores_a(i, r, t + 8)
             if diag not in ("nowork", "adjacent"):
-                seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
+                seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9), V_GEA3_B)
                 seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
                         f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
             emit_all(e, seq)
@@ -1287,6 +1289,7 @@ def kernel_geglu(name, diag=None):
             dst = V_STASH + 4 * (idx - N_IMMEDIATE)
             pack_row(e, "bias", i, r, t, dst)
             stash.append((i, r, dst))
+    e(f"v_mov_b32 v{V_GEA3}, {GE_A[2]:#x}")             # (over the bias: packed)
     e(f"s_waitcnt vmcnt({16 + n_imm_vmem})")             # the successor's step 0 landed
     e("s_barrier")
     body_head(e, "plain", 0)
@@ -1317,13 +1320,14 @@ def kernel_geglu(name, diag=None):
     e("s_waitcnt vmcnt(0)")
     for _ in range(3):
         e("s_nop 7")
+    e(f"v_mov_b32 v{V_GEA3_B}, {GE_A[2]:#x}")
     for idx in range(32):
         i, r = divmod(idx, 4)
         t = V_EPI + (idx % 4) * 12
         pack_row(e, "bias", i, r, t, t + 8)
         seq = ge_stores_a(i, r, t + 8)
         if diag not in ("nowork", "adjacent"):
-            seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9))
+            seq += ge_u(t + 8, (t, t + 1, t + 2, t + 3, t + 4, t + 5, t + 6), (t + 8, t + 9), V_GEA3_B)
             seq += [f"s_mul_i32 s{S_SOFFV}, s{S_LDU2}, {16 * i + r}",
                     f"buffer_store_dwordx2 v[{t + 8}:{t + 9}], v{V_CU}, {sr(S_SRDU, 4)}, s{S_SOFFV} offen"]
         emit_all(e, seq)
