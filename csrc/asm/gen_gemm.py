@@ -592,7 +592,8 @@ def body_head(e, epi, older_stores):
 
 
 def kernel(name, epi, diag=None):
-    global STORE_POLICY, STAGGER, SPLIT
+    global STORE_POLICY, STAGGER, SPLIT, PLAIN_DIAG
+    PLAIN_DIAG = diag if diag in ("nostore", "nopack") else None
     STORE_POLICY = "" if diag == "l2store" else " nt"
     STAGGER = diag != "nostagger"
     SPLIT = diag != "nosplit"
@@ -653,28 +654,37 @@ def kernel(name, epi, diag=None):
     e(f"s_add_u32 s{S_T0}, s{S_TILE}, s{S_GRID}")
     e(f"s_cmp_lt_u32 s{S_T0}, s{S_NT}")
     e("s_cbranch_scc0 " + e.L("final"))
+    # ---- successor with deferred stores: 6 stores now, 26 packed into v[144:247] and issued under the
+    #      successor's first K-steps (the HBM write of a tile overlaps the next tile's MFMAs instead of all CUs
+    #      storing 128 KB at once): two per step over steps 0..12 when the tile has >= 16 K-steps (measured
+    #      -1.5 % at N = 4096, -6 % at N = K = 1024 against [7, 7, 6, 6] over steps 0..3), else over 0..3 ----
+    def deferred(defer):
+        iteration(e, "penult", diag, prefetch=True, pre=pre_next)
+        iteration(e, "last", diag, prefetch=True)
+        tile_boundary(e)
+        groups = epilogue_stash(e, epi) if diag != "noepi" else []
+        n_imm = N_IMMEDIATE if groups and PLAIN_DIAG != "nostore" else 0
+        e(f"s_waitcnt vmcnt({16 + n_imm})")         # the successor's step 0 landed (step 1 + the stores younger)
+        e("s_barrier")
+        extra = body_head(e, epi, n_imm)
+        k = 0
+        for n, cnt in enumerate(defer):
+            grp = groups[k:k + cnt] if groups else []
+            k += cnt
+            iteration(e, "first" if n == 0 else "loop", diag, extra if n == 0 else 0, stores=grp)
+        e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, {3 + len(defer) - 1}")
+        e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+        e("s_cbranch_scc1 " + e.L("tail"))
+        e("s_branch " + e.L("kloop"))
+
+    if diag != "defer4":
+        e(f"s_cmp_lt_u32 s{S_KT}, {3 + len(DEFER_LONG) - 1}")
+        e("s_cbranch_scc1 " + e.L("defer4"))
+        deferred(DEFER_LONG)
+    e.label(e.L("defer4"))
     e(f"s_cmp_lt_u32 s{S_KT}, {3 + len(DEFER_SPLIT) - 1}")   # steps 0..3 peeled, penult after them
     e("s_cbranch_scc1 " + e.L("tail_imm"))
-    # ---- successor with deferred stores: 6 stores now, 26 packed into v[144:247] and issued under the
-    #      successor's K-steps 0..3 (the HBM write of a tile overlaps the next tile's MFMAs instead of all CUs
-    #      storing 128 KB at once) ----
-    iteration(e, "penult", diag, prefetch=True, pre=pre_next)
-    iteration(e, "last", diag, prefetch=True)
-    tile_boundary(e)
-    groups = epilogue_stash(e, epi) if diag != "noepi" else []
-    n_imm = N_IMMEDIATE if groups else 0
-    e(f"s_waitcnt vmcnt({16 + n_imm})")         # the successor's step 0 landed (step 1 + the stores younger)
-    e("s_barrier")
-    extra = body_head(e, epi, n_imm)
-    k = 0
-    for n, cnt in enumerate(DEFER_SPLIT):
-        grp = groups[k:k + cnt] if groups else []
-        k += cnt
-        iteration(e, "first" if n == 0 else "loop", diag, extra if n == 0 else 0, stores=grp)
-    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, {3 + len(DEFER_SPLIT) - 1}")
-    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
-    e("s_cbranch_scc1 " + e.L("tail"))
-    e("s_branch " + e.L("kloop"))
+    deferred(DEFER_SPLIT)
     # ---- successor, 4 K-steps per tile: all 32 stores at the boundary ----
     e.label(e.L("tail_imm"))
     iteration(e, "penult", diag, prefetch=True, pre=pre_next)
@@ -682,9 +692,10 @@ def kernel(name, epi, diag=None):
     tile_boundary(e)
     if diag != "noepi":
         epilogue_store(e, epi)
-    e(f"s_waitcnt vmcnt({16 + (32 if diag != 'noepi' else 0)})")
+    n_all = 32 if diag != "noepi" and PLAIN_DIAG != "nostore" else 0
+    e(f"s_waitcnt vmcnt({16 + n_all})")
     e("s_barrier")
-    extra = body_head(e, epi, 32 if diag != "noepi" else 0)
+    extra = body_head(e, epi, n_all)
     iteration(e, "first", diag, extra)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
     e("s_branch " + e.L("kloop"))
@@ -699,12 +710,14 @@ def kernel(name, epi, diag=None):
     e.label(e.L("end"))
     e("s_waitcnt vmcnt(0)")
     e("s_endpgm")
+    PLAIN_DIAG = None
     return e.text()
 
 
 # deferred epilogue: stores issued at the tile boundary, then per successor K-step 0..3
 N_IMMEDIATE = 6
 DEFER_SPLIT = [7, 7, 6, 6]
+DEFER_LONG = [2] * 13
 V_STASH = V_EPI                 # 26 packed stores x 4 VGPRs = v[144:247]
 V_ETMP = SET0_A                 # readout temps (the fragment sets are free until the successor's body_head)
 
@@ -716,8 +729,13 @@ def tile_boundary(e):
         e("s_nop 7")
 
 
+PLAIN_DIAG = None      # measurement builds of the plain kernel: "nostore" (pack, no stores), "nopack" (store, no pack)
+
+
 def pack_row(e, epi, i, r, t, dst):
     """output row (i, r) of this wave: 8 accumulators -> (+ bias) -> 4 packed bf16 pairs in v[dst:dst+3]"""
+    if PLAIN_DIAG == "nopack":
+        return
     for j in range(8):
         e(f"v_accvgpr_read_b32 v{t + j}, a{(i * 8 + j) * 4 + r}")
     if epi == "bias":
@@ -731,6 +749,8 @@ STORE_POLICY = " nt"    # cache-policy modifier of the C stores: streaming (meas
 
 
 def store_row(i, r, src):
+    if PLAIN_DIAG == "nostore":
+        return []
     return [f"s_mul_i32 s{S_SOFFC}, s{S_LDC2}, {16 * i + r}",
             f"buffer_store_dwordx4 {vr(src)}, v{V_CO}, {sr(S_SRDC, 4)}, s{S_SOFFC} offen{STORE_POLICY}"]
 
@@ -1912,7 +1932,8 @@ def kernel_geglu_bwd(name, diag=None):
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None),
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
-DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger")] + [
+DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger", "nostore",
+                                                                  "nopack", "defer4")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem")]
 

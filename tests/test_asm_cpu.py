@@ -123,3 +123,37 @@ def test_fused_epilogue_kernels_on_the_emulator(tmp_path):
     text = s.read_text()
     assert emu.selftest_geglu_bwd(text, M=2560, F=256, grid=8, wgs=(0,))
     assert emu.selftest_qkv(text, col=True, T=257, S=16, H=4, B=2, grid=8, wgs=[0])
+
+
+def test_plain_kernel_deferred_paths_on_the_emulator(tmp_path):
+    """Two tiles per workgroup through the plain and bias kernels: K = 1024 (stores spread over the successor's
+    K-steps 0..12) and K = 512 (over 0..3)."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import struct
+
+    import numpy as np
+
+    import emu
+    import gen_gemm
+
+    s = tmp_path / "g.s"
+    gen_gemm.main(str(s))
+    text = s.read_text()
+    for name, K, bias in (("dalle_gemm_nt_bias", 1024, True), ("dalle_gemm_nt_plain", 512, False)):
+        rng = np.random.default_rng(K)
+        M, N = 2560, 256
+        A = emu.f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
+        B = emu.f32_to_bf16(rng.standard_normal((N, K)).astype(np.float32))
+        b = rng.standard_normal(N).astype(np.float32)
+        mem = emu.Memory()
+        pa, pb = mem.alloc(A, "A"), mem.alloc(B, "B")
+        pc = mem.alloc(np.zeros((M, N), dtype=np.uint16), "C")
+        pbias = mem.alloc(b, "bias")
+        nt, grid = (M // 256) * (N // 256), 8
+        ka = struct.pack("<6Q16i", pa, pb, pc, pbias if bias else 0, 0, 0, M, N, K, K, K, N, N // 256, nt, grid,
+                         0, 0, 0, 0, 0, 0, 0)
+        emu.run_kernel(text, name, mem, ka, grid, [0])
+        got = emu.bf16_to_f32(mem.get(pc, np.uint16, (M, N)))
+        ref = emu.bf16_to_f32(A) @ emu.bf16_to_f32(B).T + (b if bias else 0)
+        rows = list(range(0, 256)) + list(range(8 * 256, 9 * 256))     # workgroup 0: tiles 0 and 8
+        assert np.abs(got[rows] - ref[rows]).max() / np.abs(ref).max() < 1e-2
