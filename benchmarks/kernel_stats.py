@@ -2,7 +2,7 @@
 
     python benchmarks/kernel_stats.py <rocprofv3 output dir> <steps profiled (warmup + timed)> [--top 30]
 
-Reads every ``*kernel_stats.csv`` under the directory and prints ms/step, share, calls/step and the mean
+Reads every ``*kernel_stats.csv`` (CSV output) or rocpd ``*.db`` (the default SQLite output) under the directory and prints ms/step, share, calls/step and the mean
 duration per kernel, plus the hipBLASLt (Cijk_*) share of the step."""
 import argparse
 import csv
@@ -17,6 +17,12 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
     rows = {}
+    for path in glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True):   # rocpd SQLite output
+        import sqlite3
+        con = sqlite3.connect(path)
+        for name, calls, total in con.execute("select name, count(*), sum(duration) from kernels group by name"):
+            c0, t0 = rows.get(name, (0, 0.0))
+            rows[name] = (c0 + calls, t0 + float(total))
     for path in glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True):
         with open(path) as f:
             for r in csv.DictReader(f):
