@@ -1313,14 +1313,14 @@ def kernel_geglu(name, diag=None):
     e(f"s_waitcnt vmcnt({16 + n_imm_vmem})")             # the successor's step 0 landed
     e("s_barrier")
     body_head(e, "plain", 0)
-    # ---- successor K-steps 0 .. 13, unrolled: `a` stores of the stashed row-groups in steps 0..3, their u
-    #      (gelu VALU + store) in steps 0..13 ----
+    # ---- successor K-steps 0 .. 13, unrolled: `a` stores of the stashed row-groups and their u (gelu VALU +
+    #      store), two row-groups per step ----
     ui = 0
-    per_step_a = [7, 7, 6, 6]
+    per_step_a = [2] * 13               # with each row-group's u, in the same step (over [7, 7, 6, 6]: see r5_asm_geglu_v4)
     ai = 0
     for t in range(14):
         work = []
-        if t < 4:
+        if t < len(per_step_a):
             for (i, r, src) in stash[ai:ai + per_step_a[t]]:
                 work += ge_stores_a(i, r, src)
             ai += per_step_a[t]
