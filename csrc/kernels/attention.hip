@@ -616,26 +616,36 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   // LDS slot (phase A's buffers are not in use yet), 8 lanes per row: every load instruction covers 8 whole
   // 128-B lines, where the per-lane operand-layout loads touched 32 lines per instruction (round 4). delta
   // = rowsum(dO * O) from the same registers, reduced over each row's 8 lanes (fixed xor tree).
+  // All twelve loads (Q, dO, O x 4) are issued before the first use: one HBM round trip per wave instead of
+  // eight (the per-j load -> LDS store form compiled to a vmcnt(0) drain per load pair, ~330 us of the
+  // kernel's memory skeleton at micro-batch 128). Padding rows load row 0 unconditionally and are zeroed
+  // afterwards (no divergent load to hold the batch up).
   __bf16* Ps = smem + wave * (2 * TILE);
   float dpart[4];
+  s16x8 qv[4], dv[4], ov[4];
+  int toff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
     const int srow = (active ? qb * 32 : 0) + row;
-    const int toff = tok_row(g, srow);
-    const s16x8 qv = *reinterpret_cast<const s16x8*>(Q + base + (size_t)srow * 64 + col);
-    const s16x8 dv = ld_tok(dob, toff, col);
-    *reinterpret_cast<s16x8*>(Ps + lds_idx(row, col)) = qv;
-    *reinterpret_cast<s16x8*>(Ps + TILE + lds_idx(row, col)) = dv;
-    dpart[j] = 0.f;
-    if (!delta_ready) {
-      const s16x8 ov = ld_tok(outb, toff, col);
-      float fd[8], fo[8];
-      unpack8(dv, fd);
-      unpack8(ov, fo);
+    toff[j] = tok_row(g, srow);
+    const int safe = toff[j] < 0 ? 0 : toff[j];
+    qv[j] = *reinterpret_cast<const s16x8*>(Q + base + (size_t)srow * 64 + col);
+    dv[j] = *reinterpret_cast<const s16x8*>(dob + safe + col);
+    ov[j] = *reinterpret_cast<const s16x8*>(outb + safe + col);
+  }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dpart[j] = fmaf(fd[i], fo[i], dpart[j]);
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j, row = c >> 3, col = (c & 7) * 8;
+    if (toff[j] < 0) dv[j] = s16x8{};
+    *reinterpret_cast<s16x8*>(Ps + lds_idx(row, col)) = qv[j];
+    *reinterpret_cast<s16x8*>(Ps + TILE + lds_idx(row, col)) = dv[j];
+    float fd[8], fo[8];
+    unpack8(dv[j], fd);
+    unpack8(ov[j], fo);
+    dpart[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dpart[j] = fmaf(fd[i], fo[i], dpart[j]);
   }
   if (!delta_ready) {
 #pragma unroll
