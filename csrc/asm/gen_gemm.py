@@ -184,7 +184,11 @@ def glds_list():
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}",
                     f"buffer_load_dwordx4 v{V_GB1 if par(s) else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
-    return out
+    return out[8:] + out[:8] if BFIRST and not TN else out
+
+
+BFIRST = True       # B's k-half-1 fragments, image release and DMA ahead of A's (~1 % on every plain shape,
+                    # profiles/r5_asm_gemm_bfirst.jsonl): B -- re-read by every column tile -- gets the longer lead
 
 
 STAGGER = True      # per-XCD K start (the diagnostic nostagger build turns it off)
@@ -286,7 +290,9 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     elif SPLIT:
         set1_slots = SPLIT_SET1_SLOTS
         reads = frag_reads(SET1_A, SET1_B, 1)
-        reads = [r for r in reads if f", v{V_RA1} " in r] + [r for r in reads if f", v{V_RB1} " in r]
+        ra_ = [r for r in reads if f", v{V_RA1} " in r]
+        rb_ = [r for r in reads if f", v{V_RB1} " in r]
+        reads = rb_ + ra_ if BFIRST else ra_ + rb_
         assert len(reads) == 16
         dma_slots = SPLIT_DMA_SLOTS
     else:
@@ -594,6 +600,8 @@ def body_head(e, epi, older_stores):
 def kernel(name, epi, diag=None):
     global STORE_POLICY, STAGGER, SPLIT, PLAIN_DIAG
     PLAIN_DIAG = diag if diag in ("nostore", "nopack") else None
+    global BFIRST
+    BFIRST = diag != "afirst"
     STORE_POLICY = "" if diag == "l2store" else " nt"
     STAGGER = diag != "nostagger"
     SPLIT = diag != "nosplit"
@@ -711,6 +719,7 @@ def kernel(name, epi, diag=None):
     e("s_waitcnt vmcnt(0)")
     e("s_endpgm")
     PLAIN_DIAG = None
+    BFIRST = True
     return e.text()
 
 
@@ -1933,7 +1942,7 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger", "nostore",
-                                                                  "nopack", "defer4")] + [
+                                                                  "nopack", "defer4", "afirst")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem")]
 
