@@ -102,7 +102,7 @@ def check_tn(mod, shapes):
     return ok
 
 
-def bench_tn(mod, shapes, iters=10, rounds=5):
+def bench_tn(mod, shapes, iters=10, rounds=5, diag=None):
     for (Ktot, M, N, splits) in shapes:
         A = torch.rand(Ktot, M, device="cuda").sub_(0.5).to(torch.bfloat16)
         B = torch.rand(Ktot, N, device="cuda").sub_(0.5).to(torch.bfloat16)
@@ -113,6 +113,8 @@ def bench_tn(mod, shapes, iters=10, rounds=5):
             "asm_tn": lambda: run_tn(mod, A, B, part, splits),
             "asm_tn+fold": lambda: (run_tn(mod, A, B, part, splits), torch.sum(part, 0, out=out)),
         }
+        if diag is not None:
+            fns["asm_tn_nodma"] = lambda: diag.launch("dalle_gemm_diag_tn_nodma", *tn_args(A, B, part, splits))
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -296,7 +298,8 @@ def main():
                         diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
     if a.tn:
         bench_tn(mod, [(163840, 1024, 1024, 16), (163840, 3072, 1024, 16), (163840, 8192, 1024, 2),
-                       (163840, 1024, 4096, 4)], rounds=a.rounds)
+                       (163840, 1024, 4096, 4)], rounds=a.rounds,
+                 diag=Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco")) if a.diag else None)
     if a.skip_plain:
         return
     shapes = [tuple(int(x) for x in s.split(":")) for s in a.shapes.split(",")]

@@ -1001,7 +1001,7 @@ def mul64(e, a, b):
     e(f"s_mul_hi_u32 s{S_T1}, s{a}, s{b}")
 
 
-def kernel_tn(name):
+def kernel_tn(name, diag=None):
     global TN
     TN = True
     e = Emitter(name)
@@ -1083,15 +1083,15 @@ def kernel_tn(name):
     for ins in frag_reads(SET0_A, SET0_B, 0):
         e(ins)
     e("s_waitcnt lgkmcnt(0)")
-    iteration(e, "first")
+    iteration(e, "first", diag)
     e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, 3")
     e.label(e.L("kloop"))
-    iteration(e, "loop")
+    iteration(e, "loop", diag)
     e(f"s_sub_u32 s{S_LOOP}, s{S_LOOP}, 1")
     e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
     e("s_cbranch_scc0 " + e.L("kloop"))
-    iteration(e, "penult")
-    iteration(e, "last")
+    iteration(e, "penult", diag)
+    iteration(e, "last", diag)
     for _ in range(3):
         e("s_nop 7")
     # ---- fp32 partial tile: lane holds column 16 j + c of rows 16 i + 4 g + r ----
@@ -1944,7 +1944,8 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger", "nostore",
                                                                   "nopack", "defer4", "afirst")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
-    ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem")]
+    ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
+    ("dalle_gemm_diag_tn_nodma", "tn", "nodma")]
 
 
 def main(out, diag=False):
@@ -1953,7 +1954,7 @@ def main(out, diag=False):
     for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
         if epi == "tn":
-            parts.append(kernel_tn(name))
+            parts.append(kernel_tn(name, dg))
         elif epi == "geglu":
             parts.append(kernel_geglu(name, dg))
         elif epi == "qkv":
