@@ -455,8 +455,16 @@ def d0(t):
     return int(t[0][1:])
 
 
-def run_kernel(asm_text, name, mem, kernarg, grid, wgs=None, lds_alloc=131072):
+def kernel_lds_bytes(asm_text, name):
+    """the kernel descriptor's group_segment_fixed_size (the LDS the kernel allocates)"""
+    m = re.search(r"\.amdhsa_kernel " + re.escape(name) + r"\s*\n\s*\.amdhsa_group_segment_fixed_size (\d+)", asm_text)
+    return int(m.group(1)) if m else 131072
+
+
+def run_kernel(asm_text, name, mem, kernarg, grid, wgs=None, lds_alloc=None):
     code, labels = parse_kernel(asm_text, name)
+    if lds_alloc is None:
+        lds_alloc = kernel_lds_bytes(asm_text, name)
     for wg in (range(grid) if wgs is None else wgs):
         Workgroup(code, labels, mem, kernarg, wg, lds_alloc=lds_alloc).run()
 
