@@ -115,6 +115,7 @@ def bench_tn(mod, shapes, iters=10, rounds=5, diag=None):
         }
         if diag is not None:
             fns["asm_tn_nodma"] = lambda: diag.launch("dalle_gemm_diag_tn_nodma", *tn_args(A, B, part, splits))
+            fns["asm_tn_afirst"] = lambda: diag.launch("dalle_gemm_diag_tn_afirst", *tn_args(A, B, part, splits))
         for f in fns.values():
             f()
         torch.cuda.synchronize()

@@ -184,7 +184,7 @@ def glds_list():
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}",
                     f"buffer_load_dwordx4 v{V_GB1 if par(s) else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
-    return out[8:] + out[:8] if BFIRST and not TN else out
+    return out[8:] + out[:8] if (BFIRST and not TN) or (TN and TN_BFIRST) else out
 
 
 BFIRST = True       # B's k-half-1 fragments, image release and DMA ahead of A's (~1 % on every plain shape,
@@ -286,6 +286,8 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     if TN:
         set1_slots = TN_SET1_SLOTS
         reads = frag_reads(SET1_A, SET1_B, 1)      # 16 A then 16 B transposed reads
+        if TN_BFIRST:
+            reads = reads[16:] + reads[:16]
         dma_slots = TN_DMA_SLOTS
     elif SPLIT:
         set1_slots = SPLIT_SET1_SLOTS
@@ -883,6 +885,8 @@ def descriptor(name):
 # slabs into the fp32 weight grad (deterministic).
 # ----------------------------------------------------------------------------------------------------
 TN = False
+TN_BFIRST = True     # B's transposed reads, image release and DMA ahead of A's: 0.6-1.2 % on the three large
+                     # weight-grad shapes, 1.8 % slower on the small K163840 M1024 N1024 (profiles/r5_asm_wgrad_tn_bfirst)
 V_TRA = 5            # A transposed-read bases (rd, i parity): v5..v8
 V_TRB = 144          # B bases: v144..v147
 V_TNT = 148          # TN temps v148..v159
@@ -1002,6 +1006,15 @@ def mul64(e, a, b):
 
 
 def kernel_tn(name, diag=None):
+    global TN_BFIRST
+    TN_BFIRST = diag != "tn_afirst"
+    try:
+        return _kernel_tn(name, None if diag == "tn_afirst" else diag)
+    finally:
+        TN_BFIRST = True
+
+
+def _kernel_tn(name, diag=None):
     global TN
     TN = True
     e = Emitter(name)
@@ -1945,7 +1958,7 @@ DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma",
                                                                   "nopack", "defer4", "afirst")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
-    ("dalle_gemm_diag_tn_nodma", "tn", "nodma")]
+    ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst")]
 
 
 def main(out, diag=False):
