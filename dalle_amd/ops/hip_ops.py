@@ -1300,6 +1300,8 @@ class _SplitXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, w, b, labels, text_seq_len, Vt, img_w):
+        if _head_asm_ok(h, w, b, ctx):
+            return _SplitXent._forward_asm(ctx, h, w, b, labels, text_seq_len, Vt, img_w)
         B, n, d = h.shape
         wb, bb = bf16_weight(w), bf16_weight(b)
         den = 1.0 + img_w
@@ -1345,6 +1347,56 @@ class _SplitXent(torch.autograd.Function):
             col0 += rows
         ctx.save_for_backward(dh, dW, db)
         ctx.params = (w, b)
+        ctx.segs = None
+        return loss
+
+    @staticmethod
+    def _forward_asm(ctx, h, w, b, labels, text_seq_len, Vt, img_w):
+        """The same chunked forward + eager backward with all three head products on the assembly GEMMs:
+        logits = h W_s^T + b_s (nt_bias), dh = dlogits W_s (nt_plain against a cached transposed copy,
+        K = the split's width), dW_s += dlogits^T h (tn_wgrad, fp32). Each vocabulary split is padded to a
+        multiple of 256 columns (the text split: 32356 -> 32512) with zero weight rows and a bias of -3e4:
+        a padded logit is -3e4, its probability exp(-3e4 - max) is exactly 0 in fp32, so its dlogit is 0
+        and it adds nothing to dh, dW or db; the padded rows of dW / db are dropped in ``backward``."""
+        B, n, d = h.shape
+        den = 1.0 + img_w
+        V = w.shape[0]
+        splits = ((h[:, :text_seq_len], labels[:, :text_seq_len], 0, Vt, 1.0),
+                  (h[:, text_seq_len:], labels[:, text_seq_len:] - Vt, Vt, V, img_w))
+        pads = [-(-(v1 - v0) // 256) * 256 for _, _, v0, v1, _ in splits]
+        dh = torch.empty(B, n, d, dtype=torch.bfloat16, device=h.device)
+        dW = torch.zeros(sum(pads), d, dtype=torch.float32, device=h.device)
+        db = torch.zeros(sum(pads), dtype=torch.float32, device=h.device)
+        loss = torch.zeros((), dtype=torch.float32, device=h.device)
+        col0, off, segs = 0, 0, []
+        for (hs, ls, v0, v1, wt), Vp in zip(splits, pads):
+            ws, bs, wst = _head_split_weights(w, b, v0, v1, Vp)
+            rows = hs.shape[1]
+            hs2 = hs.reshape(-1, d).contiguous()
+            ls2 = ls.reshape(-1).contiguous()
+            N = hs2.shape[0]
+            gscale = wt / (den * N)
+            dW_s, db_s = dW[off:off + Vp], db[off:off + Vp]
+            sw = asm_wgrad_splits(min(N, HEAD_CHUNK_ROWS), Vp, d)
+            dh_parts = []
+            for r0 in range(0, N, HEAD_CHUNK_ROWS):
+                r1 = min(N, r0 + HEAD_CHUNK_ROWS)
+                hc = hs2[r0:r1]
+                logit = C().asm_gemm(hc, ws, bs, None)
+                lc = C().xent_colsum_(logit, ls2[r0:r1], gscale, db_s)  # logit -> dL/dlogits in place
+                loss = loss + lc.sum() * gscale
+                dh_parts.append(C().asm_gemm(logit, wst, None, None))
+                s = sw if (r1 - r0) == min(N, HEAD_CHUNK_ROWS) else asm_wgrad_splits(r1 - r0, Vp, d)
+                C().asm_wgrad_(dW_s, logit, hc, max(s, 1), True)
+                del logit
+            dh[:, col0:col0 + rows] = (dh_parts[0] if len(dh_parts) == 1 else torch.cat(dh_parts)).view(B, rows, d)
+            segs.append((v0, v1, off))
+            col0 += rows
+            off += Vp
+        _count("asm_head")
+        ctx.save_for_backward(dh, dW, db)
+        ctx.params = (w, b)
+        ctx.segs = segs
         return loss
 
     @staticmethod
@@ -1354,11 +1406,34 @@ class _SplitXent(torch.autograd.Function):
         w, b = ctx.params
         gw, gb = grad_sink(w, ctx.needs_input_grad[1]), grad_sink(b, ctx.needs_input_grad[2])
         dh = (dh * g.to(dh.dtype)) if g.numel() else dh
+        segs = ctx.segs if ctx.segs is not None else ((0, w.shape[0], 0),)  # padded assembly-path splits
         if gw is not None and gb is not None:  # accumulate into the arena, no host read of g
-            gw.view(w.shape).addcmul_(dW, g)
-            gb.view(b.shape).addcmul_(db, g)
+            for v0, v1, off in segs:
+                gw.view(w.shape)[v0:v1].addcmul_(dW[off:off + v1 - v0], g)
+                gb.view(b.shape)[v0:v1].addcmul_(db[off:off + v1 - v0], g)
             return dh, None, None, None, None, None, None
+        if ctx.segs is not None:
+            dW = torch.cat([dW[off:off + v1 - v0] for v0, v1, off in segs])
+            db = torch.cat([db[off:off + v1 - v0] for v0, v1, off in segs])
         return dh, dW * g, db * g, None, None, None, None
+
+
+def _head_asm_ok(h, w, b, ctx) -> bool:
+    """The assembly head path: eager (the gradient is wanted), bf16-able operands on the GPU, d = 1024 rows
+    that tile (B * text_len and B * image_len multiples of 256 follow from text_len, image_len % 256 == 0)."""
+    return (ASM_GEMM and h.is_cuda and all(ctx.needs_input_grad[:3]) and h.dim() == 3 and h.shape[-1] == 1024
+            and HEAD_CHUNK_ROWS % 256 == 0 and w.dim() == 2 and w.shape[1] == 1024 and b is not None)
+
+
+def _head_split_weights(w, b, v0: int, v1: int, Vp: int):
+    """(W_s padded to Vp rows bf16, b_s padded with -3e4 fp32, W_s^T padded (d, Vp) bf16), cached per forward."""
+    def make():
+        ws = torch.zeros(Vp, w.shape[1], dtype=torch.bfloat16, device=w.device)
+        ws[:v1 - v0] = w.detach()[v0:v1]
+        bs = torch.full((Vp,), -3.0e4, dtype=torch.float32, device=w.device)
+        bs[:v1 - v0] = b.detach()[v0:v1].float()
+        return ws, bs, ws.t().contiguous()
+    return _cached(("head", id(w), v0, v1), w, make)
 
 
 # rows of one head chunk (logits of 4096 text rows: 265 MB bf16, image rows: 67 MB)

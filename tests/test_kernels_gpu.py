@@ -143,6 +143,37 @@ def test_split_logits_loss(cuda, chunk, monkeypatch):
     assert _rel(bias.grad, b2.grad) < 3e-2
 
 
+@pytest.mark.parametrize("chunk", [16384, 256])
+def test_split_logits_loss_asm_head(cuda, chunk, monkeypatch):
+    """K12 on the assembly GEMMs (d = 1024): logits / dh / dW through nt_bias / nt_plain / tn_wgrad, the text
+    split padded 1064 -> 1280 columns (zero rows, bias -3e4), one or several chunks; checked against fp32."""
+    from dalle_amd.ops import hip_ops
+
+    monkeypatch.setattr(hip_ops, "HEAD_CHUNK_ROWS", chunk)
+    torch.manual_seed(6)
+    B, tsl, n_img, d, Vt, Vi = 2, 256, 512, 1024, 1064, 512
+    n = tsl + n_img
+    out = torch.randn(B, n, d, device=cuda, requires_grad=True)
+    nw = torch.ones(d, device=cuda, requires_grad=True)
+    nb = torch.zeros(d, device=cuda, requires_grad=True)
+    W = (torch.randn(Vt + Vi, d, device=cuda) * 0.03).requires_grad_(True)
+    bias = (torch.randn(Vt + Vi, device=cuda) * 0.1).requires_grad_(True)
+    labels = torch.cat([torch.randint(0, Vt, (B, tsl)), torch.randint(Vt, Vt + Vi, (B, n_img))], 1).to(cuda)
+    hip_ops.begin_forward()
+    before = hip_ops.PATH_COUNTS.get("asm_head", 0)
+    loss = hip_ops.logits_loss(out, nw, nb, W, bias, labels, tsl, Vt, 7.0)
+    (loss * 3.0).backward()
+    assert hip_ops.PATH_COUNTS.get("asm_head", 0) == before + 1, "the assembly head path did not run"
+    o2, W2, b2 = (t.detach().clone().requires_grad_(True) for t in (out, W, bias))
+    h = F.layer_norm(o2, (d,))
+    loss_r = ref.split_logits_loss(h, W2, b2, labels, tsl, Vt, 7.0)
+    (loss_r * 3.0).backward()
+    assert abs(loss.item() - loss_r.item()) < 1e-2
+    assert _rel(out.grad, o2.grad) < 3e-2
+    assert _rel(W.grad, W2.grad) < 3e-2
+    assert _rel(bias.grad, b2.grad) < 3e-2
+
+
 def test_nonfinite(cuda):
     from dalle_amd.ops import hip_ops
 
