@@ -127,11 +127,14 @@ def acc(i, j):
 # ----------------------------------------------------------------------------------------------------
 # main-loop building blocks
 # ----------------------------------------------------------------------------------------------------
+SERPENTINE = False   # (measurement build "serp": j reversed on odd i, so consecutive MFMAs at a row change share B)
+
+
 def mfma_list(set_a, set_b, zero_c):
     """the 64 MFMAs of one k-half (i-major), as instruction strings"""
     out = []
     for i in range(8):
-        for j in range(8):
+        for j in (range(7, -1, -1) if SERPENTINE and i & 1 else range(8)):
             c = "0" if zero_c else acc(i, j)
             out.append(f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {vr(set_a + 4 * i)}, {vr(set_b + 4 * j)}, {c}")
     return out
@@ -602,8 +605,9 @@ def body_head(e, epi, older_stores):
 def kernel(name, epi, diag=None):
     global STORE_POLICY, STAGGER, SPLIT, PLAIN_DIAG
     PLAIN_DIAG = diag if diag in ("nostore", "nopack") else None
-    global BFIRST
+    global BFIRST, SERPENTINE
     BFIRST = diag != "afirst"
+    SERPENTINE = diag == "serp"
     STORE_POLICY = "" if diag == "l2store" else " nt"
     STAGGER = diag != "nostagger"
     SPLIT = diag != "nosplit"
@@ -722,6 +726,7 @@ def kernel(name, epi, diag=None):
     e("s_endpgm")
     PLAIN_DIAG = None
     BFIRST = True
+    SERPENTINE = False
     return e.text()
 
 
@@ -1955,7 +1960,7 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger", "nostore",
-                                                                  "nopack", "defer4", "afirst")] + [
+                                                                  "nopack", "defer4", "afirst", "serp")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
     ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst")]
