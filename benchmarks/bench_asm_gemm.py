@@ -247,7 +247,7 @@ def bench(mod, shapes, iters=20, diag=None, rounds=5):
             "asm_plain": lambda: run(mod, "dalle_gemm_nt_plain", A, B, C),
         }
         if diag is not None:
-            for v in ("noepi", "nodma", "nosplit", "nostagger", "nostore", "nopack", "defer4", "afirst", "serp"):
+            for v in ("noepi", "nodma", "split", "nostagger", "nostore", "nopack", "defer4", "afirst", "serp", "ant", "abnt"):
                 fns[f"asm_{v}"] = (lambda v=v: run(diag, f"dalle_gemm_diag_{v}", A, B, C))
         for f in fns.values():
             f()

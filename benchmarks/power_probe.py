@@ -104,6 +104,8 @@ def main():
     run("asm_nt_K8192", lambda: C().asm_gemm(A, B, None, Cm), a.seconds, None)
     run("asm_nt_K8192_nodma", lambda: diag.launch("dalle_gemm_diag_nodma", 256, args), a.seconds, None)
     run("asm_nt_K8192_serp", lambda: diag.launch("dalle_gemm_diag_serp", 256, args), a.seconds, None)
+    run("asm_nt_K8192_ant", lambda: diag.launch("dalle_gemm_diag_ant", 256, args), a.seconds, None)
+    run("asm_nt_K8192_abnt", lambda: diag.launch("dalle_gemm_diag_abnt", 256, args), a.seconds, None)
     run("asm_nt_K8192_again", lambda: C().asm_gemm(A, B, None, Cm), a.seconds, None)
     run("hipblaslt_K8192", lambda: torch.mm(A, B.t(), out=Cm), a.seconds, None)
     Z = torch.zeros_like(A)

@@ -175,6 +175,9 @@ def set0_waits(set1_slots):
     return waits
 
 
+LOAD_POLICY = ("", "")   # cache-policy modifiers of the A / B LDS-DMA loads (measurement builds "ant", "abnt": streaming)
+
+
 def glds_list():
     """16 LDS-DMA instructions of one K-step as (M0 write, DMA) pairs: this wave's A image rows 64q + 8s .. +7,
     then its B image rows (s = 0..7); M0 = S_MBASE (+ B_IMG) + s KB.  The M0 write needs one wait state
@@ -183,10 +186,10 @@ def glds_list():
     par = (lambda s: (s >> 1) & 1) if TN else (lambda s: s & 1)   # which per-lane source offset
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {s * PIECE}",
-                    f"buffer_load_dwordx4 v{V_GA1 if par(s) else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen lds"))
+                    f"buffer_load_dwordx4 v{V_GA1 if par(s) else V_GA0}, {sr(S_SRDA, 4)}, s{S_OFFA + s} offen{LOAD_POLICY[0]} lds"))
     for s in range(8):
         out.append((f"s_add_u32 m0, s{S_MBASE}, {B_IMG + s * PIECE}",
-                    f"buffer_load_dwordx4 v{V_GB1 if par(s) else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen lds"))
+                    f"buffer_load_dwordx4 v{V_GB1 if par(s) else V_GB0}, {sr(S_SRDB, 4)}, s{S_OFFB + s} offen{LOAD_POLICY[1]} lds"))
     return out[8:] + out[:8] if (BFIRST and not TN) or (TN and TN_BFIRST) else out
 
 
@@ -605,12 +608,15 @@ def body_head(e, epi, older_stores):
 def kernel(name, epi, diag=None):
     global STORE_POLICY, STAGGER, SPLIT, PLAIN_DIAG
     PLAIN_DIAG = diag if diag in ("nostore", "nopack") else None
-    global BFIRST, SERPENTINE
+    global BFIRST, SERPENTINE, LOAD_POLICY
     BFIRST = diag != "afirst"
     SERPENTINE = diag == "serp"
+    LOAD_POLICY = {"ant": (" nt", ""), "abnt": (" nt", " nt")}.get(diag, ("", ""))
     STORE_POLICY = "" if diag == "l2store" else " nt"
     STAGGER = diag != "nostagger"
-    SPLIT = diag != "nosplit"
+    # plain / bias: one stage-release barrier (B2) -- 0.6-0.7 % faster than the split release on every plain
+    # shape in a sustained (power-limited) A/B, profiles/r5_ab_sustained.txt; the fused kernels keep SPLIT
+    SPLIT = diag == "split"
     e = Emitter(name)
     # ---- arguments ----
     e(f"s_load_dwordx8 {sr(S_A, 8)}, s[0:1], 0x0")          # A B C AUX0
@@ -727,6 +733,8 @@ def kernel(name, epi, diag=None):
     PLAIN_DIAG = None
     BFIRST = True
     SERPENTINE = False
+    LOAD_POLICY = ("", "")
+    SPLIT = True
     return e.text()
 
 
@@ -1959,8 +1967,8 @@ def kernel_geglu_bwd(name, diag=None):
 KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias", None), ("dalle_gemm_tn_wgrad", "tn", None),
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
-DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "nosplit", "nostagger", "nostore",
-                                                                  "nopack", "defer4", "afirst", "serp")] + [
+DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "split", "nostagger", "nostore",
+                                                                  "nopack", "defer4", "afirst", "serp", "ant", "abnt")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
     ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst")]

@@ -36,12 +36,14 @@ def test_asm_gemm_builds(tmp_path):
     big = sum(1 for name, _, _ in gen_gemm.KERNELS if name in gen_gemm.LDS_BYTES)
     assert notes.count(".group_segment_fixed_size: 131072") == len(gen_gemm.KERNELS) - big
     assert notes.count(".group_segment_fixed_size: 163840") == big
-    # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads, 3 barriers in the loop body
-    # (A image released, B image released, next step landed)
-    body = text.split("dalle_gemm_nt_plain_kloop:")[1].split("s_cbranch_scc0")[0]
-    assert body.count("v_mfma_f32_16x16x32_bf16") == 128
-    assert body.count(" lds") == 16 and body.count("ds_read_b128") == 32 and body.count("s_barrier") == 3
-    assert "s_nop" not in body   # every wait state of the loop is an MFMA
+    # per K-step and wave: 128 MFMAs, 16 LDS-DMA pieces, 32 fragment reads; the plain kernel's loop body has 2
+    # barriers (stage released, next step landed), the fused kernels' 3 (A image released, B image released,
+    # next step landed)
+    for name, nbar in (("dalle_gemm_nt_plain", 2), ("dalle_gemm_nt_geglu", 3)):
+        body = text.split(f"{name}_kloop:")[1].split("s_cbranch_scc0")[0]
+        assert body.count("v_mfma_f32_16x16x32_bf16") == 128
+        assert body.count(" lds") == 16 and body.count("ds_read_b128") == 32 and body.count("s_barrier") == nbar
+        assert "s_nop" not in body   # every wait state of the loop is an MFMA
 
 
 def test_fragment_reads_are_bank_conflict_free():
