@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import statistics
+import struct
 import sys
 import time
 
@@ -58,11 +59,60 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--suite", default="order", choices=["order", "nosplit"])
+    ap.add_argument("--suite", default="order", choices=["order", "nosplit", "plain", "fused"])
+    ap.add_argument("--variants", default="nostagger,defer4,l2store", help="suite plain: diag builds vs production")
+    ap.add_argument("--shapes", default="1024:1024,8192:1024,1024:8192", help="suite plain: N:K at M = 163840")
     a = ap.parse_args()
     prod = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_gfx950.hsaco"))
     diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco"))
     M = 163840
+    if a.suite == "fused":  # split release (production) vs one release barrier: TN weight grad, FF-in + GEGLU, GEGLU bwd
+        for Mw, Nw, sp in ((8192, 1024, 2), (1024, 4096, 4), (3072, 1024, 16)):
+            A = torch.randn(M, Mw, device="cuda", dtype=torch.bfloat16) * 0.02
+            B = torch.randn(M, Nw, device="cuda", dtype=torch.bfloat16) * 0.02
+            part = torch.empty(sp, Mw, Nw, device="cuda")
+            units, args = tn_args(A, B, part, sp)
+            compare(f"tn {Mw}x{Nw} s{sp}: production vs tn_onebar",
+                    lambda: prod.launch("dalle_gemm_tn_wgrad", units, args),
+                    lambda: diag.launch("dalle_gemm_diag_tn_onebar", units, args), a.seconds, a.rounds)
+            del A, B, part
+        F, K = 4096, 1024
+        x = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+        w = torch.rand(2 * F, K, device="cuda").sub_(0.5).mul_(0.06).to(torch.bfloat16)
+        b = torch.zeros(2 * F, device="cuda")
+        av = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+        u = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+        nt = (M // 256) * (2 * F // 256)
+        grid = min(256, (nt + 7) // 8 * 8)
+        args = struct.pack("<6Q16i", x.data_ptr(), w.data_ptr(), av.data_ptr(), b.data_ptr(), u.data_ptr(), 0,
+                           M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
+        compare("geglu F4096: production vs nosplit", lambda: prod.launch("dalle_gemm_nt_geglu", grid, args),
+                lambda: diag.launch("dalle_gemm_diag_geglu_nosplit", grid, args), a.seconds, a.rounds)
+        del x, w, av, u
+        dy = torch.rand(M, K, device="cuda").sub_(0.5).to(torch.bfloat16)
+        w2t = torch.rand(F, K, device="cuda").sub_(0.5).mul_(0.06).to(torch.bfloat16)
+        h = torch.randn(M, 2 * F, device="cuda").to(torch.bfloat16)
+        dh = torch.empty_like(h)
+        part = torch.empty(M // 128, 2 * F, device="cuda")
+        nt = (M // 256) * (F // 256)
+        grid = min(256, (nt + 7) // 8 * 8)
+        args = struct.pack("<6Q16i", dy.data_ptr(), w2t.data_ptr(), dh.data_ptr(), h.data_ptr(), part.data_ptr(), 0,
+                           M, F, K, K, K, 2 * F, F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
+        compare("geglu_bwd F4096: production vs nosplit", lambda: prod.launch("dalle_gemm_nt_geglu_bwd", grid, args),
+                lambda: diag.launch("dalle_gemm_diag_gbwd_nosplit", grid, args), a.seconds, a.rounds)
+        return
+    if a.suite == "plain":  # production plain kernel vs each named diagnostic build
+        for sh in a.shapes.split(","):
+            N, K = (int(x) for x in sh.split(":"))
+            A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16) * 0.02
+            B = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+            Cm = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            args = gemm_args(A, B, Cm)
+            for v in a.variants.split(","):
+                compare(f"nt N{N} K{K}: production vs {v}", lambda: prod.launch("dalle_gemm_nt_plain", 256, args),
+                        lambda v=v: diag.launch(f"dalle_gemm_diag_{v}", 256, args), a.seconds, a.rounds)
+            del A, B, Cm
+        return
     if a.suite == "nosplit":  # every plain shape of the step: one stage-release barrier (prod) vs the split release
         for N, K in ((1024, 1024), (3072, 1024), (1024, 3072), (1024, 4096), (8192, 1024), (1024, 8192)):
             A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16) * 0.02

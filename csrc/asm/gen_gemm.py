@@ -294,7 +294,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
         reads = frag_reads(SET1_A, SET1_B, 1)      # 16 A then 16 B transposed reads
         if TN_BFIRST:
             reads = reads[16:] + reads[:16]
-        dma_slots = TN_DMA_SLOTS
+        dma_slots = TN_ONEBAR_DMA_SLOTS if TN_ONEBAR else TN_DMA_SLOTS
     elif SPLIT:
         set1_slots = SPLIT_SET1_SLOTS
         reads = frag_reads(SET1_A, SET1_B, 1)
@@ -328,7 +328,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     for n, ins in at:
         slots[n].append(ins)
     dma = (kind in ("first", "loop") or prefetch) and diag != "nodma"
-    if dma and (SPLIT or TN):
+    if dma and (SPLIT or TN) and not (TN and TN_ONEBAR):
         # BA after the A k-half-1 reads (and this step's k-half-0 reads) retired: stage X's A image is free;
         # BB after the B reads: its B image.  Each refilled with step t + 2's piece.
         ba, bb = (TN_BA_SLOT, TN_BB_SLOT) if TN else (BA_SLOT, BB_SLOT)
@@ -340,8 +340,9 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
         slots[bb].append("s_barrier")
     elif dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
-        slots[B2_SLOT].append("s_waitcnt lgkmcnt(0)")
-        slots[B2_SLOT].append("s_barrier")
+        b2 = TN_B2_SLOT if TN else B2_SLOT
+        slots[b2].append("s_waitcnt lgkmcnt(0)")
+        slots[b2].append("s_barrier")
     else:
         slots[max(set1_slots) + 2].append("s_waitcnt lgkmcnt(0)")
     if dma:
@@ -906,6 +907,9 @@ V_TNT = 148          # TN temps v148..v159
 S_STEPA, S_STEPB, S_SPLIT = 79, 80, 81
 TN_SET1_SLOTS = list(range(16)) + [18 + 2 * n for n in range(16)]     # 16 A reads, then 16 B reads
 TN_BA_SLOT, TN_BB_SLOT = 21, 52
+TN_ONEBAR = False    # (measurement build tn_onebar: one stage-release barrier after all 32 reads, then the 16 DMAs)
+TN_B2_SLOT = 50
+TN_ONEBAR_DMA_SLOTS = [52 + round(4.8 * n) for n in range(16)]   # 52 .. 124
 TN_DMA_SLOTS = [23 + 4 * n for n in range(8)] + [56 + round(9.7 * n) for n in range(8)]   # 23..51, 56..124
 
 
@@ -1019,12 +1023,25 @@ def mul64(e, a, b):
 
 
 def kernel_tn(name, diag=None):
-    global TN_BFIRST
+    global TN_BFIRST, TN_ONEBAR
     TN_BFIRST = diag != "tn_afirst"
+    TN_ONEBAR = diag == "tn_onebar"
     try:
-        return _kernel_tn(name, None if diag == "tn_afirst" else diag)
+        return _kernel_tn(name, None if diag in ("tn_afirst", "tn_onebar") else diag)
     finally:
-        TN_BFIRST = True
+        TN_BFIRST, TN_ONEBAR = True, False
+
+
+def _one_barrier(dg, gen):
+    """measurement build "nosplit" of a fused kernel: one stage-release barrier (SPLIT off while it is generated)"""
+    global SPLIT
+    if dg != "nosplit":
+        return gen(dg)
+    SPLIT = False
+    try:
+        return gen(None)
+    finally:
+        SPLIT = True
 
 
 def _kernel_tn(name, diag=None):
@@ -1649,7 +1666,8 @@ S_SRDAA, S_SRDP = S_SRDX, 84                    # a / part resources of the fini
 S_GSOF = (88, 89)
 S_GMASK, S_GPR, S_GNH, S_GC2, S_GF = 90, 91, 92, 93, 94
 LDS_GB = 2 * STAGE
-for _n in ("dalle_gemm_nt_geglu_bwd", "dalle_gemm_diag_gbwd_novalu", "dalle_gemm_diag_gbwd_nomem"):
+for _n in ("dalle_gemm_nt_geglu_bwd", "dalle_gemm_diag_gbwd_novalu", "dalle_gemm_diag_gbwd_nomem",
+           "dalle_gemm_diag_gbwd_nosplit"):
     LDS_BYTES[_n] = LDS_GB + 256 * 16 * GB_LDS       # 160 KB: the whole LDS
 
 
@@ -1968,10 +1986,12 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "split", "nostagger", "nostore",
-                                                                  "nopack", "defer4", "afirst", "serp", "ant", "abnt")] + [
+                                                                  "nopack", "defer4", "afirst", "serp", "ant", "abnt", "l2store")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
-    ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst")]
+    ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst"),
+    ("dalle_gemm_diag_tn_onebar", "tn", "tn_onebar"), ("dalle_gemm_diag_geglu_nosplit", "geglu", "nosplit"),
+    ("dalle_gemm_diag_gbwd_nosplit", "geglu_bwd", "nosplit")]
 
 
 def main(out, diag=False):
@@ -1982,11 +2002,11 @@ def main(out, diag=False):
         if epi == "tn":
             parts.append(kernel_tn(name, dg))
         elif epi == "geglu":
-            parts.append(kernel_geglu(name, dg))
+            parts.append(_one_barrier(dg, lambda d: kernel_geglu(name, d)))
         elif epi == "qkv":
             parts.append(kernel_qkv(name, dg))
         elif epi == "geglu_bwd":
-            parts.append(kernel_geglu_bwd(name, dg))
+            parts.append(_one_barrier(dg, lambda d: kernel_geglu_bwd(name, d)))
         else:
             parts.append(kernel(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
