@@ -1426,14 +1426,17 @@ def _head_asm_ok(h, w, b, ctx) -> bool:
 
 
 def _head_split_weights(w, b, v0: int, v1: int, Vp: int):
-    """(W_s padded to Vp rows bf16, b_s padded with -3e4 fp32, W_s^T padded (d, Vp) bf16), cached per forward."""
+    """(W_s padded to Vp rows bf16, b_s padded with -3e4 fp32, W_s^T padded (d, Vp) bf16): the weight copies are
+    cached per forward (keyed on W's version), the bias slice is refreshed on every call (a frozen W with a
+    trained bias never reads a stale bias)."""
     def make():
         ws = torch.zeros(Vp, w.shape[1], dtype=torch.bfloat16, device=w.device)
         ws[:v1 - v0] = w.detach()[v0:v1]
         bs = torch.full((Vp,), -3.0e4, dtype=torch.float32, device=w.device)
-        bs[:v1 - v0] = b.detach()[v0:v1].float()
         return ws, bs, ws.t().contiguous()
-    return _cached(("head", id(w), v0, v1), w, make)
+    ws, bs, wst = _cached(("head", id(w), v0, v1), w, make)
+    bs[:v1 - v0].copy_(b.detach()[v0:v1])
+    return ws, bs, wst
 
 
 # rows of one head chunk (logits of 4096 text rows: 265 MB bf16, image rows: 67 MB)
