@@ -33,7 +33,7 @@ class CollaborationSummary:
     loss: float
     alive_peers: int
     samples: int
-    performance: float
+    performance: Optional[float]   # None until some peer's EMA has a measured interval
 
     def as_record(self) -> dict:
         """The key names the reference logs to wandb (``run_aux_peer.py:135-141``)."""
@@ -49,12 +49,15 @@ def summarize(records: Iterable) -> Optional[CollaborationSummary]:
     if not records:
         return None
     mini = sum(int(r.mini_steps) for r in records)
+    perf = sum(float(r.samples_per_second) for r in records)
     return CollaborationSummary(
         step=max(int(r.step) for r in records),
         loss=sum(float(r.loss) for r in records) / max(mini, 1),
         alive_peers=len(records),
         samples=sum(int(r.samples_accumulated) for r in records),
-        performance=sum(float(r.samples_per_second) for r in records),
+        # an epoch that closes before any peer's throughput EMA has an interval (epoch 0 on its first
+        # micro-step) has no throughput yet: reported as None, not as 0 samples/s
+        performance=perf if perf > 0 else None,
     )
 
 
@@ -172,7 +175,7 @@ def run_monitor(poller: MetricsPoller, keeper: Optional[SnapshotKeeper], sinks: 
         if summary is not None:
             rec = summary.as_record()
             logger.info(f"epoch #{summary.step}: loss {summary.loss:.5f}, {summary.alive_peers} peers, "
-                        f"{summary.performance:.1f} samples/s")
+                        + (f"{summary.performance:.1f} samples/s" if summary.performance is not None else "throughput n/a"))
             history.append(rec)
             for sink in sinks:
                 sink(rec)

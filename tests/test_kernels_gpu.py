@@ -174,6 +174,30 @@ def test_split_logits_loss_asm_head(cuda, chunk, monkeypatch):
     assert _rel(bias.grad, b2.grad) < 3e-2
 
 
+def test_asm_head_sees_bias_updates(cuda):
+    """The padded head weights are cached per forward; a bias changed in place (W untouched, no begin_forward)
+    must still reach the logits: the loss matches the fp32 reference with the NEW bias."""
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(7)
+    B, tsl, n_img, d, Vt, Vi = 1, 256, 256, 1024, 700, 512
+    n = tsl + n_img
+    out = torch.randn(B, n, d, device=cuda, requires_grad=True)
+    nw = torch.ones(d, device=cuda, requires_grad=True)
+    nb = torch.zeros(d, device=cuda, requires_grad=True)
+    W = (torch.randn(Vt + Vi, d, device=cuda) * 0.03).requires_grad_(True)
+    bias = torch.zeros(Vt + Vi, device=cuda, requires_grad=True)
+    labels = torch.cat([torch.randint(0, Vt, (B, tsl)), torch.randint(Vt, Vt + Vi, (B, n_img))], 1).to(cuda)
+    hip_ops.begin_forward()
+    hip_ops.logits_loss(out, nw, nb, W, bias, labels, tsl, Vt, 7.0).backward()
+    with torch.no_grad():
+        bias.add_(torch.randn_like(bias))
+    loss = hip_ops.logits_loss(out, nw, nb, W, bias, labels, tsl, Vt, 7.0)
+    h = F.layer_norm(out.detach(), (d,))
+    loss_r = ref.split_logits_loss(h, W.detach(), bias.detach(), labels, tsl, Vt, 7.0)
+    assert abs(loss.item() - loss_r.item()) < 1e-2
+
+
 def test_nonfinite(cuda):
     from dalle_amd.ops import hip_ops
 
