@@ -29,14 +29,20 @@ def main():
     wall = (t1 - t0) / 1e3 / a.steps
     busy, cur_s, cur_e = 0, None, None
     gaps = []
-    for s, e, _ in win:
+    pair_gap = defaultdict(list)   # (previous kernel, next kernel) -> idle gaps between them
+    prev_name = None
+    for s, e, n in win:
         if cur_e is None or s > cur_e:
             if cur_e is not None:
                 busy += cur_e - cur_s
                 gaps.append(s - cur_e)
+                pair_gap[(prev_name, n)].append(s - cur_e)
             cur_s, cur_e = s, e
         else:
+            if cur_e is not None:
+                pair_gap[(prev_name, n)].append(0)
             cur_e = max(cur_e, e)
+        prev_name = n
     busy += cur_e - cur_s
     ksum = sum(e - s for s, e, _ in win)
     print(f"# {a.steps} decode steps: wall {wall:.1f} us/step, GPU busy {busy / 1e3 / a.steps:.1f}, summed kernel time "
@@ -45,6 +51,10 @@ def main():
     if gaps:
         print(f"# idle gaps: {len(gaps) / a.steps:.0f} per step, total {sum(gaps) / 1e3 / a.steps:.1f} us/step, "
               f"median {gaps[len(gaps) // 2] / 1e3:.2f} us, p90 {gaps[int(len(gaps) * 0.9)] / 1e3:.2f} us")
+    short = lambda n: n.split("(")[0].replace("void ", "")[-60:]  # noqa: E731
+    print("# idle us/step  transitions/step  mean_gap_us  previous -> next kernel")
+    for (pn, nn), g in sorted(pair_gap.items(), key=lambda kv: -sum(kv[1]))[:12]:
+        print(f"{sum(g) / 1e3 / a.steps:9.1f} {len(g) / a.steps:8.1f} {sum(g) / len(g) / 1e3:8.2f}  {short(pn or '')} -> {short(nn)}")
     per = defaultdict(list)
     for s, e, n in win:
         per[n].append(e - s)
