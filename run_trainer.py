@@ -66,5 +66,21 @@ def main(argv=None):
     return trainer, task
 
 
+def _teardown(task) -> None:
+    """Release the communicator before the interpreter exits: a gloo / RCCL group still alive at interpreter
+    finalisation tears its worker threads down in arbitrary order (an occasional SIGABRT after a finished
+    run). Local only -- the key/value store host stays up for peers still writing their last records."""
+    import torch.distributed as dist
+
+    try:
+        if getattr(task, "_elastic", None) is not None:
+            task._elastic.shutdown()
+        elif dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - teardown of a broken group must not fail a finished run
+        logger.warning(f"process group teardown: {e!r}")
+
+
 if __name__ == "__main__":
-    main()
+    _trainer, _task = main()
+    _teardown(_task)
