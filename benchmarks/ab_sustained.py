@@ -59,13 +59,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--suite", default="order", choices=["order", "nosplit", "plain", "fused"])
+    ap.add_argument("--suite", default="order", choices=["order", "nosplit", "plain", "fused", "splits"])
     ap.add_argument("--variants", default="nostagger,defer4,l2store", help="suite plain: diag builds vs production")
     ap.add_argument("--shapes", default="1024:1024,8192:1024,1024:8192", help="suite plain: N:K at M = 163840")
     a = ap.parse_args()
     prod = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_gfx950.hsaco"))
     diag = Module(os.path.join(HERE, "..", "dalle_amd", "gemm_diag_gfx950.hsaco"))
     M = 163840
+    if a.suite == "splits":  # weight-grad split count, kernel + deterministic fold (the extension's asm_wgrad_)
+        from dalle_amd.ops.hip_ops import C
+        for Mw, Nw, sa, sb in ((3072, 1024, 16, 5), (3072, 1024, 16, 10), (1024, 1024, 16, 10), (1024, 4096, 4, 5)):
+            A = torch.randn(M, Mw, device="cuda", dtype=torch.bfloat16) * 0.02
+            B = torch.randn(M, Nw, device="cuda", dtype=torch.bfloat16) * 0.02
+            out = torch.zeros(Mw, Nw, device="cuda")
+            compare(f"wgrad {Mw}x{Nw}: s{sa} vs s{sb}", lambda: C().asm_wgrad_(out, A, B, sa, True),
+                    lambda: C().asm_wgrad_(out, A, B, sb, True), a.seconds, a.rounds)
+            del A, B, out
+        return
     if a.suite == "fused":  # split release (production) vs one release barrier: TN weight grad, FF-in + GEGLU, GEGLU bwd
         for Mw, Nw, sp in ((8192, 1024, 2), (1024, 4096, 4), (3072, 1024, 16)):
             A = torch.randn(M, Mw, device="cuda", dtype=torch.bfloat16) * 0.02

@@ -318,22 +318,24 @@ def _weight_grad_t(gw, fused: bool, g2, x2):
 
 def asm_wgrad_splits(M: int, N: int, K: int) -> int:
     """Split count of the assembly TN weight-grad kernel for an (N x K) weight over M tokens, or 0 when the
-    shape does not tile: the (tile, split) units should fill whole waves of the 256 CUs (then the fewest
-    splits: every split adds an fp32 partial slab to the fold).  Measured at M = 163840
-    (profiles/r5_asm_wgrad_tn.jsonl): 1024x1024 s16 1439 TF/s, 3072x1024 s16 1441, 8192x1024 s2 1535,
-    1024x4096 s4 1493 (hipBLASLt on the same token-major operands: 496 / 742 / 1130 / 992)."""
+    shape does not tile. Cost model: the main loop takes (whole waves of the 256 CUs the (tile, split) units
+    occupy) x (work per unit), at ~1.45 PF/s; every split adds an fp32 partial slab that is written and read
+    back by the fold (8 B per weight element, ~5 TB/s). Checked with sustained A/B runs at M = 163840
+    (profiles/r5_ab_sustained.txt): 3072x1024 s5 732 us vs s16 768 (the old whole-wave rule picked 16),
+    1024x1024 s16 264 vs s10 317, 1024x4096 s4 957 vs s5 1264; 8192x1024 stays at s2."""
     if N % 256 or K % 256:
         return 0
     tiles = (N // 256) * (K // 256)
+    main = 2.0 * M * N * K / 1.45e15
     best = None
     for s in (1, 2, 4, 5, 8, 10, 16, 20, 32):
         if M % (128 * s) or M // s < 256:
             continue
         units = tiles * s
-        util = units / (-(-units // 256) * 256)
-        key = (round(util, 2), -s)
-        if best is None or key > best[0]:
-            best = (key, s)
+        waves = -(-units // 256)
+        cost = main * waves * 256 / units + s * N * K * 8 / 5e12
+        if best is None or cost < best[0]:
+            best = (cost, s)
     return best[1] if best else 0
 
 
