@@ -256,6 +256,8 @@ def toggle_reads():
 B2_SLOT = 36
 B3_SLOT = 90
 DMA_SLOTS = [40 + round(5.6 * n) for n in range(16)]          # 40 .. 124
+PLAIN_B2, PLAIN_DMA = B2_SLOT, DMA_SLOTS   # (measurement builds "b2_33": release at 33, DMA 35..123; "dma_dense": DMA 38..98)
+PLAIN_SCHEDS = {"b2_33": (33, [35 + round(5.9 * n) for n in range(16)]), "dma_dense": (36, [38 + 4 * n for n in range(16)])}
 ADVANCE_SLOT = 126
 # split release (default): the k-half-1 A fragments are read first and a barrier (BA) frees the stage's A image
 # early, so its 8 DMAs start under MFMA 20 while the B fragments are still being read; a second barrier (BB)
@@ -306,7 +308,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
     else:
         set1_slots = [2 * n for n in range(16)]
         reads = frag_reads(SET1_A, SET1_B, 1)
-        dma_slots = DMA_SLOTS
+        dma_slots = PLAIN_DMA
     for n, ins in zip(set1_slots, reads):
         slots[n].append(ins)
     # the k-half-0 fragments still in flight from the previous step: wait for each as its MFMA comes up
@@ -340,7 +342,7 @@ def iteration(e, kind, diag=None, extra=0, prefetch=False, pre=(), stores=(), he
         slots[bb].append("s_barrier")
     elif dma:
         # B2 after the k-half-1 reads retired: stage X is free; refill it with step t + 2
-        b2 = TN_B2_SLOT if TN else B2_SLOT
+        b2 = TN_B2_SLOT if TN else PLAIN_B2
         slots[b2].append("s_waitcnt lgkmcnt(0)")
         slots[b2].append("s_barrier")
     else:
@@ -613,6 +615,8 @@ def kernel(name, epi, diag=None):
     BFIRST = diag != "afirst"
     SERPENTINE = diag == "serp"
     LOAD_POLICY = {"ant": (" nt", ""), "abnt": (" nt", " nt")}.get(diag, ("", ""))
+    global PLAIN_B2, PLAIN_DMA
+    PLAIN_B2, PLAIN_DMA = PLAIN_SCHEDS.get(diag, (B2_SLOT, DMA_SLOTS))
     STORE_POLICY = "" if diag == "l2store" else " nt"
     STAGGER = diag != "nostagger"
     # plain / bias: one stage-release barrier (B2) -- 0.6-0.7 % faster than the split release on every plain
@@ -736,6 +740,7 @@ def kernel(name, epi, diag=None):
     SERPENTINE = False
     LOAD_POLICY = ("", "")
     SPLIT = True
+    PLAIN_B2, PLAIN_DMA = B2_SLOT, DMA_SLOTS
     return e.text()
 
 
@@ -1986,7 +1991,8 @@ KERNELS = [("dalle_gemm_nt_plain", "plain", None), ("dalle_gemm_nt_bias", "bias"
            ("dalle_gemm_nt_geglu", "geglu", None), ("dalle_gemm_nt_qkv_row", "qkv", 0), ("dalle_gemm_nt_qkv_col", "qkv", 1),
            ("dalle_gemm_nt_geglu_bwd", "geglu_bwd", None)]
 DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma", "split", "nostagger", "nostore",
-                                                                  "nopack", "defer4", "afirst", "serp", "ant", "abnt", "l2store")] + [
+                                                                  "nopack", "defer4", "afirst", "serp", "ant", "abnt", "l2store", "b2_33",
+                                                                  "dma_dense")] + [
     ("dalle_gemm_diag_geglu_nowork", "geglu", "nowork"), ("dalle_gemm_diag_geglu_adjacent", "geglu", "adjacent"),
     ("dalle_gemm_diag_gbwd_novalu", "geglu_bwd", "novalu"), ("dalle_gemm_diag_gbwd_nomem", "geglu_bwd", "nomem"),
     ("dalle_gemm_diag_tn_nodma", "tn", "nodma"), ("dalle_gemm_diag_tn_afirst", "tn", "tn_afirst"),
