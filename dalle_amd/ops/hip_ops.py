@@ -1302,7 +1302,7 @@ class _SplitXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, w, b, labels, text_seq_len, Vt, img_w):
-        if _head_asm_ok(h, w, b, ctx):
+        if _head_asm_ok(h, w, b, ctx, text_seq_len, Vt):
             return _SplitXent._forward_asm(ctx, h, w, b, labels, text_seq_len, Vt, img_w)
         B, n, d = h.shape
         wb, bb = bf16_weight(w), bf16_weight(b)
@@ -1391,7 +1391,8 @@ class _SplitXent(torch.autograd.Function):
                 s = sw if (r1 - r0) == min(N, HEAD_CHUNK_ROWS) else asm_wgrad_splits(r1 - r0, Vp, d)
                 C().asm_wgrad_(dW_s, logit, hc, max(s, 1), True)
                 del logit
-            dh[:, col0:col0 + rows] = (dh_parts[0] if len(dh_parts) == 1 else torch.cat(dh_parts)).view(B, rows, d)
+            if dh_parts:
+                dh[:, col0:col0 + rows] = (dh_parts[0] if len(dh_parts) == 1 else torch.cat(dh_parts)).view(B, rows, d)
             segs.append((v0, v1, off))
             col0 += rows
             off += Vp
@@ -1420,11 +1421,16 @@ class _SplitXent(torch.autograd.Function):
         return dh, dW * g, db * g, None, None, None, None
 
 
-def _head_asm_ok(h, w, b, ctx) -> bool:
-    """The assembly head path: eager (the gradient is wanted), bf16-able operands on the GPU, d = 1024 rows
-    that tile (B * text_len and B * image_len multiples of 256 follow from text_len, image_len % 256 == 0)."""
-    return (ASM_GEMM and h.is_cuda and all(ctx.needs_input_grad[:3]) and h.dim() == 3 and h.shape[-1] == 1024
-            and HEAD_CHUNK_ROWS % 256 == 0 and w.dim() == 2 and w.shape[1] == 1024 and b is not None)
+def _head_asm_ok(h, w, b, ctx, text_seq_len: int, Vt: int) -> bool:
+    """The assembly head path: eager (the gradient is wanted), operands on the GPU, d = 1024, row counts that
+    tile (B * text_len and B * image_len multiples of 256) and padded vocabulary splits the fused CE kernel's
+    LDS column sums hold; anything else takes the hipBLASLt path."""
+    if not (ASM_GEMM and h.is_cuda and all(ctx.needs_input_grad[:3]) and h.dim() == 3 and h.shape[-1] == 1024
+            and HEAD_CHUNK_ROWS % 256 == 0 and w.dim() == 2 and w.shape[1] == 1024 and b is not None):
+        return False
+    B, n = h.shape[0], h.shape[1]
+    pads = [-(-v // 256) * 256 for v in (Vt, w.shape[0] - Vt)]
+    return (B * text_seq_len) % 256 == 0 and (B * (n - text_seq_len)) % 256 == 0 and max(pads) <= XENT_COLSUM_MAXV
 
 
 def _head_split_weights(w, b, v0: int, v1: int, Vp: int):
