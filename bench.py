@@ -227,6 +227,9 @@ def run_rank(args) -> None:
     named = list(model.named_parameters())
     pg = dist.group.WORLD if world > 1 else None
 
+    gen = torch.Generator().manual_seed(1000 + rank)
+    batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
+                               cfg.num_image_tokens, gen, device=device) for _ in range(4)]
     if args.engine == "collab":
         from dalle_amd.parallel.compression import reference_averaging_compression, NoCompression
         from dalle_amd.parallel.optimizer import CollaborativeOptimizer
@@ -253,8 +256,18 @@ def run_rank(args) -> None:
             from dalle_amd.parallel.dp import tune_grad_sync
             algos = ("rccl", "rs_ag") if algo == "auto" else (algo,)
             mbs = (16, 32, 64, 128) if bucket_bytes is None else (bucket_bytes / 2 ** 20,)
-            algo, bucket_bytes, ar_tuning = tune_grad_sync(arena, world, grad_dtype=args.grad_dtype, algos=algos,
-                                                        bucket_mb=mbs)
+
+            def tune_step(gs):
+                # the candidate inside a real step: zero, forward, backward (final grads handed to gs as they
+                # appear when overlapped), the remaining all-reduce -- no optimizer step, params untouched
+                arena.zero_grad()
+                b = batches[0]
+                model(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True).backward()
+                gs.all_reduce()
+
+            algo, bucket_bytes, ar_tuning = tune_grad_sync(
+                arena, world, grad_dtype=args.grad_dtype, algos=algos, bucket_mb=mbs, step_fn=tune_step,
+                overlap=os.environ.get("DALLE_AMD_DP_OVERLAP", "1") != "0")
         if algo == "auto":
             algo = "rccl"
         if bucket_bytes is None:
@@ -284,9 +297,6 @@ def run_rank(args) -> None:
             opt.step()
         zero = arena.zero_grad
 
-    gen = torch.Generator().manual_seed(1000 + rank)
-    batches = [synthetic_batch(args.batch, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens,
-                               cfg.num_image_tokens, gen, device=device) for _ in range(4)]
 
     from dalle_amd.utils.profiling import StepTimer, prof_range
 

@@ -89,7 +89,7 @@ bool asm_gemm_nt(const char* kernel, const void* A, const void* B, void* C, cons
 
 bool asm_qkv_rope(bool col, const void* h, const void* w, void* qkv, const float* cs3, int M, int N, int K, int lda, int ldb,
                   int n, int T, int Tp, int Np, int H, int logS, hipStream_t st) {
-  if (M <= 0 || M % 256 || N % 256 || K != 1024 || n % 256 || M % n || (H * 64) % 256 || N != 3 * H * 64) return false;
+  if (M <= 0 || M % 256 || N % 256 || K < 1024 || K % 128 || n % 256 || M % n || (H * 64) % 256 || N != 3 * H * 64) return false;
   GemmArgs args;
   std::memset(&args, 0, sizeof(args));
   args.a = h; args.b = w; args.c = qkv; args.aux0 = cs3;

@@ -647,7 +647,8 @@ def tile_of_wg_id(tile, tiles_m, tiles_n):
     return (tiles_m & ~7) + w % rem, w // rem
 
 
-def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):
+def selftest_geglu(text, M=2048, F=256, K=1024, grid=8, wgs=None, rows=None):
+    """``wgs``: run only these workgroups and compare only output ``rows`` (the rows their tiles cover)"""
     rng = np.random.default_rng(1)
     x = f32_to_bf16(rng.standard_normal((M, K)).astype(np.float32))
     w1 = (rng.standard_normal((2 * F, K)) * 0.03).astype(np.float32)
@@ -662,10 +663,11 @@ def selftest_geglu(text, M=2048, F=256, K=1024, grid=8):
     pu = mem.alloc(np.zeros((M, F), dtype=np.uint16), "u")
     nt = (M // 256) * (2 * F // 256)
     ka = struct.pack("<6Q16i", pa, pb, pc, pbias, pu, 0, M, 2 * F, K, K, K, 2 * F, 2 * F // 256, nt, grid, F, 0, 0, 0, 0, 0, 0)
-    run_kernel(text, "dalle_gemm_nt_geglu", mem, ka, grid)
-    a = bf16_to_f32(mem.get(pc, np.uint16, (M, 2 * F)))
-    u = bf16_to_f32(mem.get(pu, np.uint16, (M, F)))
-    a_ref = bf16_to_f32(x) @ bf16_to_f32(f32_to_bf16(w1)).T + b1
+    run_kernel(text, "dalle_gemm_nt_geglu", mem, ka, grid, wgs)
+    sel = slice(None) if rows is None else rows
+    a = bf16_to_f32(mem.get(pc, np.uint16, (M, 2 * F)))[sel]
+    u = bf16_to_f32(mem.get(pu, np.uint16, (M, F)))[sel]
+    a_ref = (bf16_to_f32(x) @ bf16_to_f32(f32_to_bf16(w1)).T + b1)[sel]
     err_a = float(np.abs(a - a_ref).max() / np.abs(a_ref).max())
     ab = a.astype(np.float64)
     u_ref = ab[:, :F] * gelu_ref(ab[:, F:])

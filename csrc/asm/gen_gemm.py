@@ -1167,10 +1167,36 @@ def _kernel_tn(name, diag=None):
 # writes `a` back in the ORIGINAL column order as two 8-byte chunks (value j / gate F + j: 16 lanes = one whole
 # 128-byte line each) and computes its 4 u from the same registers -- no exchange, no reload.  Both are deferred
 # like the plain kernel's stores: the packed bf16 row-groups (the numbers the unfused geglu kernel would read)
-# wait in v[144:247] while the successor tile's K-steps 0..13 (unrolled: needs kt = 16, K = 1024; the host
+# wait in v[144:247] while the successor tile's K-steps 0..13 (unrolled: needs kt >= 16, K >= 1024; the host
 # checks) store them and spread the gelu VALU over their MFMA gaps.  The tile's bias is loaded during its last
 # K-step, so v[248:255] serve as the gelu temps meanwhile.
 # ----------------------------------------------------------------------------------------------------
+
+# ----------------------------------------------------------------------------------------------------
+# K generality of the fused kernels: their successor tile's K-steps 0..13 are unrolled (the deferred epilogue
+# work rides in those steps' MFMA gaps), so a tile needs kt >= 16 K-steps (K >= 1024) and, as every kernel
+# here, an even count (the successor's steps 0 / 1 land in stages 0 / 1).  Steps 14 .. kt - 3 then run in the
+# ordinary K-loop and penult / last in the shared tail: K = 1024 (d_model 1024) and K = 2048 (the ~1.3B
+# config's d_model) take the same code.
+# ----------------------------------------------------------------------------------------------------
+FUSED_UNROLL = 14
+
+
+def kt_guard(e):
+    """leave (no work) unless kt >= FUSED_UNROLL + 2 and even (the host rejects other shapes too)"""
+    e(f"s_cmp_lt_u32 s{S_KT}, {FUSED_UNROLL + 2}")
+    e("s_cbranch_scc1 " + e.L("end"))
+    e(f"s_bitcmp1_b32 s{S_KT}, 0")
+    e("s_cbranch_scc1 " + e.L("end"))
+
+
+def successor_rest(e):
+    """after the unrolled successor steps 0..13: kt - 16 plain loop steps (none at K = 1024), then the tail"""
+    e(f"s_sub_u32 s{S_LOOP}, s{S_KT}, {FUSED_UNROLL + 2}")
+    e(f"s_cmp_eq_u32 s{S_LOOP}, 0")
+    e("s_cbranch_scc1 " + e.L("tail"))
+    e("s_branch " + e.L("kloop"))
+
 S_SRDU = 84          # u resource (4)
 S_SOFFV, S_GP, S_MASK7, S_F2, S_LDU2, S_RSQ2 = 88, 89, 90, 91, 92, 93
 S_AUX1, S_LDU = 22, 21
@@ -1307,8 +1333,7 @@ def kernel_geglu(name, diag=None):
     e(f"s_lshl_b32 s{S_F2}, s{S_LDU}, 1")               # 2 F bytes: the gate half of an `a` row (ld_aux = F)
     e(f"s_mov_b32 s{S_GP}, 0x3eaa540e")                  # 0.47047 / sqrt 2
     e(f"s_mov_b32 s{S_MASK7}, 0x7fffffff")
-    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
-    e("s_cbranch_scc0 " + e.L("end"))
+    kt_guard(e)
     lane_setup(e, "bias")
     geglu_lane_setup(e, diag)
     e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
@@ -1375,7 +1400,7 @@ def kernel_geglu(name, diag=None):
     ui = 0
     per_step_a = [2] * 13               # with each row-group's u, in the same step (over [7, 7, 6, 6]: see r5_asm_geglu_v4)
     ai = 0
-    for t in range(14):
+    for t in range(FUSED_UNROLL):
         work = []
         if t < len(per_step_a):
             for (i, r, src) in stash[ai:ai + per_step_a[t]]:
@@ -1390,7 +1415,7 @@ def kernel_geglu(name, diag=None):
             ui += GE_SPLIT[t]
         iteration(e, "first" if t == 0 else "loop", None, n_imm_vmem if t == 0 else 0, work=work,
                   work_span=(1, 118))
-    e("s_branch " + e.L("tail"))
+    successor_rest(e)
     e.label(e.L("final"))
     iteration(e, "penult", None, pre=pre_out)
     vm = iteration(e, "last", None, work=BIAS_LOADS, work_span=(1, 4))
@@ -1548,8 +1573,7 @@ def kernel_qkv(name, col):
     e("s_nop 1")
     e("s_waitcnt lgkmcnt(0)")
     e(f"s_lshr_b32 s{S_KT}, s{S_K}, 6")
-    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
-    e("s_cbranch_scc0 " + e.L("end"))
+    kt_guard(e)
     e(f"s_lshl_b32 s{S_QHD}, s{S_QH}, 6")                # H * 64 columns per part
     magic(e, S_QMAGN, S_QN)
     e(f"s_mul_hi_u32 s{S_QBT}, s{S_M}, s{S_QMAGN}")      # batch = M / n
@@ -1620,7 +1644,7 @@ def kernel_qkv(name, col):
     e(f"s_waitcnt vmcnt({16 + n_vm})")                   # the successor's step 0 landed
     e("s_barrier")
     body_head(e, "plain", 0)
-    for t in range(14):
+    for t in range(FUSED_UNROLL):
         loads, comp = [], []
         for b_, (i, r, src) in enumerate(stash[2 * t:2 * t + 2] if t < 12 else []):
             tag = f"q{b_}"
@@ -1628,7 +1652,7 @@ def kernel_qkv(name, col):
             comp += [f"@vmwait:{tag}"] + qkv_rotate_store(i, r, src, Q_BANKS[b_], col)
         iteration(e, "first" if t == 0 else "loop", None, n_vm if t == 0 else 0, work=loads, work_span=(1, 4),
                   work2=comp, work2_span=(60, 118))
-    e("s_branch " + e.L("tail"))
+    successor_rest(e)
     e.label(e.L("final"))
     iteration(e, "penult", None, pre=pre_out)
     boundary(True)
@@ -1645,7 +1669,7 @@ def kernel_qkv(name, col):
 
 
 # ----------------------------------------------------------------------------------------------------
-# FF-out dgrad + GEGLU backward: du = dy W2 (M x F; A = dy (M x K), B = W2^T (F x K), K = 1024), then with the
+# FF-out dgrad + GEGLU backward: du = dy W2 (M x F; A = dy (M x K), B = W2^T (F x K), K = d_model), then with the
 # FF-in pre-activation a (M x 2F, [value | gate], aux0):  da_value = du gelu(gate), da_gate = du value gelu'(gate)
 # into dh (M x 2F, C; ldc = 2F, ld_aux = F), and the FF-in bias gradient's column sums per 128-row block into
 # part (M / 128 x 2F fp32, aux1; the host folds it).  du is rounded to bf16 first, as the unfused path stores
@@ -1653,7 +1677,7 @@ def kernel_qkv(name, col):
 # gate halves: two 16-byte loads, two 16-byte stores, no exchange.  The GEGLU backward is VALU-heavy (~27
 # instructions per element), so it runs under the successor tile's MFMAs: 7 row-groups at the tile boundary,
 # 17 with du packed in v[144:211] and 8 with du in the LDS above the two operand stages (32 KB), processed two
-# per successor K-step 0..13 (unrolled: K = 1024) with their `a` chunks loaded one K-step ahead (two banks of
+# per successor K-step 0..13 (unrolled: K >= 1024) with their `a` chunks loaded one K-step ahead (two banks of
 # 16 VGPRs).  Column sums: each element's (da, dg) pair is folded over lanes g, g + 2 by v_permlane32_swap into
 # 8 running sums; at the tile's end v_permlane16_swap folds g, g + 1 and each lane stores 4 of the 128-row
 # block's sums (16 bytes).
@@ -1863,8 +1887,7 @@ def kernel_geglu_bwd(name, diag=None):
     e(f"s_mov_b32 s{S_GPR}, 0x3eaa540e")                 # 0.47047 / sqrt 2
     e(f"s_mov_b32 s{S_GNH}, {GE_CONSTS['nhl2e']:#x}")     # -log2(e) / 2
     e(f"s_mov_b32 s{S_GC2}, 0xbfa9b21d")                 # log2(1 / sqrt(2 pi))
-    e(f"s_cmp_eq_u32 s{S_KT}, 16")                      # the unrolled successor body is for K = 1024
-    e("s_cbranch_scc0 " + e.L("end"))
+    kt_guard(e)
     lane_setup(e, "plain")
     gb_lane_setup(e)
     e(f"s_and_b32 s{S_T0}, s{S_WG}, 7")
@@ -1944,7 +1967,7 @@ def kernel_geglu_bwd(name, diag=None):
     e("s_barrier")
     body_head(e, "plain", 0)
     prev_wait = after_last(vm_last, "a0") + n_st
-    for t in range(14):
+    for t in range(FUSED_UNROLL):
         at = []
         if t + 1 < 14:
             lds_next = [(idx, loc) for idx, loc in plan[t + 1] if loc[0] == "l"]
@@ -1961,7 +1984,7 @@ def kernel_geglu_bwd(name, diag=None):
                        more=((next_a, (63, 65)), (comp_b, (66, 120))))
         if next_a:
             prev_wait = after_last(vm, f"a{t + 1}")
-    e("s_branch " + e.L("tail"))
+    successor_rest(e)
     # ---- no successor: 4 row-groups, then the other 28 in three load batches ----
     e.label(e.L("final"))
     vm_pen = iteration(e, "penult", None, pre=pre_out, work=imm_loads, work_span=(20, 60))
@@ -2000,21 +2023,48 @@ DIAG_KERNELS = [(f"dalle_gemm_diag_{d}", "plain", d) for d in ("noepi", "nodma",
     ("dalle_gemm_diag_gbwd_nosplit", "geglu_bwd", "nosplit")]
 
 
-def main(out, diag=False):
+# The schedule knobs the kernel builders read are module globals (the measurement variants flip them for one
+# build).  Every kernel is generated from a fresh copy of their defaults, so a kernel's code depends only on
+# (name, epilogue, variant) -- never on which kernels were generated before it (tests/test_asm_cpu.py
+# generates the production set in two opposite orders, diagnostic variants interleaved, and compares).
+_KNOBS = ("SERPENTINE", "LOAD_POLICY", "BFIRST", "STAGGER", "SPLIT", "STORE_POLICY", "PLAIN_DIAG", "PLAIN_B2",
+          "PLAIN_DMA", "TN", "TN_BFIRST", "TN_ONEBAR", "GB_DIAG")
+
+
+def _knob_defaults():
+    g = globals()
+    g.setdefault("PLAIN_B2", B2_SLOT)
+    g.setdefault("PLAIN_DMA", DMA_SLOTS)
+    return {k: (list(g[k]) if isinstance(g[k], list) else g[k]) for k in _KNOBS}
+
+
+def generate(name, epi, dg=None):
+    """the assembly of one kernel, from the default knobs (restored afterwards as well)"""
+    g = globals()
+    saved = _knob_defaults()
+    g.update({k: (list(v) if isinstance(v, list) else v) for k, v in _DEFAULT_KNOBS.items()})
+    try:
+        if epi == "tn":
+            return kernel_tn(name, dg)
+        if epi == "geglu":
+            return _one_barrier(dg, lambda d: kernel_geglu(name, d))
+        if epi == "qkv":
+            return kernel_qkv(name, dg)
+        if epi == "geglu_bwd":
+            return _one_barrier(dg, lambda d: kernel_geglu_bwd(name, d))
+        return kernel(name, epi, dg)
+    finally:
+        g.update(_DEFAULT_KNOBS if saved is None else saved)
+
+
+def main(out, diag=False, kernels=None):
+    """``kernels``: (name, epilogue, variant) list to emit (default: the production set, + the diagnostic
+    variants when ``diag``)"""
     parts = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 6", "\t.text"]
     metas = []
-    for name, epi, dg in (KERNELS + DIAG_KERNELS if diag else KERNELS):
+    for name, epi, dg in (kernels if kernels is not None else (KERNELS + DIAG_KERNELS if diag else KERNELS)):
         parts += [f"\t.globl\t{name}", "\t.p2align\t8", f"\t.type\t{name},@function", f"{name}:"]
-        if epi == "tn":
-            parts.append(kernel_tn(name, dg))
-        elif epi == "geglu":
-            parts.append(_one_barrier(dg, lambda d: kernel_geglu(name, d)))
-        elif epi == "qkv":
-            parts.append(kernel_qkv(name, dg))
-        elif epi == "geglu_bwd":
-            parts.append(_one_barrier(dg, lambda d: kernel_geglu_bwd(name, d)))
-        else:
-            parts.append(kernel(name, epi, dg))
+        parts.append(generate(name, epi, dg))
         parts.append(f"\t.size\t{name}, .-{name}")
         parts.append(descriptor(name))
         metas.append(metadata(name))
@@ -2022,6 +2072,9 @@ def main(out, diag=False):
                  + "amdhsa.target:   amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\n\t.end_amdgpu_metadata")
     with open(out, "w") as f:
         f.write("\n".join(parts) + "\n")
+
+
+_DEFAULT_KNOBS = _knob_defaults()
 
 
 if __name__ == "__main__":

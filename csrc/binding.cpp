@@ -417,14 +417,29 @@ std::vector<Tensor> ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optiona
   return {dh, db};
 }
 
-// The same on the assembly kernel (csrc/asm/gen_gemm.py kernel_geglu_bwd): K = 1024, M and F multiples of 256
+// Row-strided operands of the assembly kernels: the kernels form a tile's base address in 64-bit scalar math but
+// a lane's offset inside the tile as 32-bit (row < 256) x (stride * 2 bytes), and a buffer resource's num_records
+// from 256 rows of stride: keep every operand's last byte under 2^40 and its row stride under 2^20 elements.
+static void check_asm_operand(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, what, ": 2-D with unit column stride");
+  TORCH_CHECK(t.stride(0) >= t.size(1) && t.stride(0) < (1 << 20), what, ": row stride out of range");
+  TORCH_CHECK((int64_t)t.size(0) * t.stride(0) * 2 < (1ll << 40), what, ": operand exceeds 2^40 bytes");
+}
+
+// The same on the assembly kernel (csrc/asm/gen_gemm.py kernel_geglu_bwd): K a multiple of 128 and >= 1024 (the
+// unrolled successor K-steps), M and F multiples of 256
 std::vector<Tensor> asm_ff_dgrad_geglu(Tensor dy, Tensor w2t, Tensor h, c10::optional<Tensor> gb) {
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == torch::kBFloat16 && w2t.scalar_type() == torch::kBFloat16, "asm_ff_dgrad_geglu: bf16");
   CHECK_IN(h, torch::kBFloat16);
   TORCH_CHECK(dy.dim() == 2 && w2t.dim() == 2 && h.dim() == 2 && dy.stride(1) == 1 && w2t.stride(1) == 1, "asm_ff_dgrad_geglu: 2-D, K-contiguous");
   const long M = dy.size(0), K = dy.size(1), F = w2t.size(0);
   TORCH_CHECK(w2t.size(1) == K && h.size(0) == M && h.size(1) == 2 * F, "asm_ff_dgrad_geglu: shape mismatch");
-  TORCH_CHECK(K == 1024 && M % 256 == 0 && F % 256 == 0, "asm_ff_dgrad_geglu: K = 1024, M and F multiples of 256");
+  TORCH_CHECK(K >= 1024 && K % 128 == 0 && M % 256 == 0 && F % 256 == 0,
+              "asm_ff_dgrad_geglu: K a multiple of 128 (>= 1024), M and F multiples of 256");
+  check_asm_operand(dy, "asm_ff_dgrad_geglu dy");
+  check_asm_operand(w2t, "asm_ff_dgrad_geglu w2t");
+  TORCH_CHECK(h.is_contiguous(), "asm_ff_dgrad_geglu: h contiguous");
+  check_asm_operand(h, "asm_ff_dgrad_geglu h");
   auto dh = torch::empty_like(h);
   auto part = torch::empty({M / 128, 2 * F}, h.options().dtype(torch::kFloat32));
   float* pb = sink_ptr(gb, 2 * F, "asm_ff_dgrad_geglu dbias");
@@ -538,7 +553,8 @@ void asm_wgrad_(Tensor out, Tensor A, Tensor B, int64_t splits, bool accumulate)
   TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N, "asm_wgrad: out (M, N)");
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && splits > 0 && Ktot % splits == 0 && (Ktot / splits) % 128 == 0 &&
                   Ktot / splits >= 256, "asm_wgrad: M, N multiples of 256, Ktot / splits a multiple of 128 (>= 256)");
-  TORCH_CHECK((int64_t)Ktot * A.stride(0) * 2 < (1ll << 40) && A.stride(0) < (1 << 23) && B.stride(0) < (1 << 23), "asm_wgrad: strides");
+  TORCH_CHECK((int64_t)Ktot * A.stride(0) * 2 < (1ll << 40) && (int64_t)Ktot * B.stride(0) * 2 < (1ll << 40) &&
+                  A.stride(0) < (1 << 23) && B.stride(0) < (1 << 23), "asm_wgrad: strides");
   Tensor part = torch::empty({splits, M, N}, out.options());
   TORCH_CHECK(dalle::asm_gemm_tn(A.data_ptr(), B.data_ptr(), part.data_ptr(), M, N, Ktot, (int)A.stride(0), (int)B.stride(0),
                                  (int)splits, cur_stream()),
@@ -546,12 +562,14 @@ void asm_wgrad_(Tensor out, Tensor A, Tensor B, int64_t splits, bool accumulate)
   dalle::splitk_accum(part.data_ptr<float>(), out.data_ptr<float>(), (long)M * N, (int)splits, accumulate ? 1 : 0, cur_stream());
 }
 
-// QKV + rotary on the assembly kernel: h (M, 1024) bf16, w (3 H 64, 1024) bf16, cs3 (3, n + 1, 32, 2) fp32 (q's
+// QKV + rotary on the assembly kernel: h (M, d) bf16, w (3 H 64, d) bf16 (d a multiple of 128, >= 1024), cs3 (3, n + 1, 32, 2) fp32 (q's
 // (cos, sin) pre-scaled, k's and v's plain: all three rotated) -> q, k, v (B H, Np, 64) storage views (padding rows zeroed)
 std::vector<Tensor> asm_qkv_rope(Tensor h, Tensor w, Tensor cs3, int64_t T, int64_t S, int64_t H, int64_t n, bool col_major) {
   CHECK_IN(h, torch::kBFloat16); CHECK_IN(w, torch::kBFloat16); CHECK_IN(cs3, torch::kFloat32);
   TORCH_CHECK(h.dim() == 2 && w.dim() == 2 && w.size(0) == 3 * H * 64 && w.size(1) == h.size(1), "asm_qkv_rope: shapes");
   const int M = h.size(0), K = h.size(1);
+  check_asm_operand(h, "asm_qkv_rope h");
+  check_asm_operand(w, "asm_qkv_rope w");
   TORCH_CHECK(cs3.dim() == 4 && cs3.size(0) == 3 && cs3.size(1) >= n + 1 && cs3.size(2) == 32 && cs3.size(3) == 2,
               "asm_qkv_rope: cs3 (3, n + 1, 32, 2)");
   auto g = make_attn_geom(T, S, n, 1, H, 0);
@@ -565,7 +583,7 @@ std::vector<Tensor> asm_qkv_rope(Tensor h, Tensor w, Tensor cs3, int64_t T, int6
   return {q, k, v};
 }
 
-// FF-in GEMM + GEGLU on the assembly kernel: x (M, 1024) bf16, w1p (2F, 1024) bf16 = W1 with its rows in the
+// FF-in GEMM + GEGLU on the assembly kernel: x (M, d) bf16, w1p (2F, d) bf16 (d a multiple of 128, >= 1024) = W1 with its rows in the
 // interleaved [value 8 | gate 8] order (hip_ops.ff_in_perm), b1p (2F,) fp32 in the same order ->
 // a (M, 2F) bf16 pre-activation in the ORIGINAL [value | gate] order, u (M, F) = value * gelu(gate)
 std::vector<Tensor> asm_ff_in_geglu(Tensor x, Tensor w1p, Tensor b1p) {
@@ -574,7 +592,10 @@ std::vector<Tensor> asm_ff_in_geglu(Tensor x, Tensor w1p, Tensor b1p) {
               "asm_ff_in_geglu: x (M, K), w1p (2F, K), K-contiguous");
   CHECK_IN(b1p, torch::kFloat32);
   const int M = x.size(0), N = w1p.size(0), K = x.size(1);
-  TORCH_CHECK(K == 1024 && M % 256 == 0 && N % 256 == 0 && b1p.numel() == N, "asm_ff_in_geglu: K = 1024, M and 2F multiples of 256");
+  TORCH_CHECK(K >= 1024 && K % 128 == 0 && M % 256 == 0 && N % 256 == 0 && b1p.numel() == N,
+              "asm_ff_in_geglu: K a multiple of 128 (>= 1024), M and 2F multiples of 256");
+  check_asm_operand(x, "asm_ff_in_geglu x");
+  check_asm_operand(w1p, "asm_ff_in_geglu w1p");
   auto a = torch::empty({M, N}, x.options());
   auto u = torch::empty({M, N / 2}, x.options());
   TORCH_CHECK(dalle::asm_gemm_nt("dalle_gemm_nt_geglu", x.data_ptr(), w1p.data_ptr(), a.data_ptr(), b1p.data_ptr(), u.data_ptr(), nullptr,
@@ -589,7 +610,8 @@ Tensor asm_gemm(Tensor A, Tensor B, c10::optional<Tensor> bias, c10::optional<Te
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1, "asm_gemm: K-contiguous operands");
   const int M = A.size(0), N = B.size(0), K = A.size(1);
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K >= 256, "asm_gemm: M, N multiples of 256, K of 128 (>= 256)");
-  TORCH_CHECK((int64_t)M * A.stride(0) * 2 < (1ll << 40) && A.stride(0) < (1 << 20) && B.stride(0) < (1 << 20), "asm_gemm: strides");
+  check_asm_operand(A, "asm_gemm A");
+  check_asm_operand(B, "asm_gemm B");
   const void* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     CHECK_IN((*bias), torch::kFloat32);

@@ -140,9 +140,17 @@ def ff_in_perm(F: int, device) -> torch.Tensor:
     return p
 
 
+def asm_fused_k(d: int) -> bool:
+    """the fused assembly kernels (QKV + rotary, FF-in + GEGLU, FF-dgrad + GEGLU backward) take K = d_model a
+    multiple of 128 and >= 1024: their successor tile's first 14 K-steps are unrolled (gen_gemm.FUSED_UNROLL),
+    the rest runs in the ordinary K-loop -- d = 1024 (bench24 / reference) and d = 2048 (the ~1.3B preset)"""
+    return d >= 1024 and d % 128 == 0
+
+
 def _ff_in_geglu_ok(h2: torch.Tensor, w1: torch.Tensor) -> bool:
     return (ASM_GEMM and h2.is_cuda and h2.dtype == torch.bfloat16 and h2.dim() == 2 and h2.stride(1) == 1
-            and h2.shape[1] == 1024 and h2.shape[0] % 256 == 0 and w1.shape[0] % 256 == 0 and w1.shape[1] == 1024)
+            and asm_fused_k(h2.shape[1]) and h2.shape[0] % 256 == 0 and w1.shape[0] % 256 == 0
+            and w1.shape[1] == h2.shape[1])
 
 
 def ff_in_geglu(h2: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
@@ -622,7 +630,7 @@ def _attn_core_fwd(inp, h, mean, rstd, w_qkv, w_out, b_out, scale, cos, sin, met
     h2 = h.view(-1, d)
     wq = bf16_weight(w_qkv)
     col = pattern == PATTERN_IDS["axial_col"]
-    if ASM_GEMM and n % 256 == 0 and d == 1024 and wq.shape[0] == 3 * H * 64 and (H * 64) % 256 == 0 and h2.stride(1) == 1:
+    if ASM_GEMM and n % 256 == 0 and asm_fused_k(d) and wq.shape[0] == 3 * H * 64 and (H * 64) % 256 == 0 and h2.stride(1) == 1:
         # QKV GEMM on the assembly kernel, the rotary applied to its stored bf16 values in the deferred epilogue
         q, k, v = C().asm_qkv_rope(h2, wq, _cs3_from_tables(cos, sin, 0.125), T, S, H, n, col)
         _count("qkv_rope")
@@ -688,7 +696,7 @@ def _ff_core_bwd(saved, params, dy, sk):
     ln_w, ln_b, w1, b1, w2, b2, scale = params
     dy = dy.view(-1, dy.shape[-1])
     M, F = dy.shape[0], w2b.shape[1]
-    if ASM_GEMM and M % 256 == 0 and F % 256 == 0 and dy.shape[1] == 1024 and dy.stride(1) == 1:
+    if ASM_GEMM and M % 256 == 0 and F % 256 == 0 and asm_fused_k(dy.shape[1]) and dy.stride(1) == 1:
         # du = dy W2 on the assembly GEMM, the GEGLU backward + b1 column sums under the next tile's K-steps
         da, db1 = C().asm_ff_dgrad_geglu(dy, bf16_weight_t(w2), a.view(M, 2 * F), sk[3] if sk is not None else None)
         _count("ff_dgrad_geglu")
@@ -1422,11 +1430,12 @@ class _SplitXent(torch.autograd.Function):
 
 
 def _head_asm_ok(h, w, b, ctx, text_seq_len: int, Vt: int) -> bool:
-    """The assembly head path: eager (the gradient is wanted), operands on the GPU, d = 1024, row counts that
+    """The assembly head path: eager (the gradient is wanted), operands on the GPU, d a multiple of 256 (>= 1024), row counts that
     tile (B * text_len and B * image_len multiples of 256) and padded vocabulary splits the fused CE kernel's
     LDS column sums hold; anything else takes the hipBLASLt path."""
-    if not (ASM_GEMM and h.is_cuda and all(ctx.needs_input_grad[:3]) and h.dim() == 3 and h.shape[-1] == 1024
-            and HEAD_CHUNK_ROWS % 256 == 0 and w.dim() == 2 and w.shape[1] == 1024 and b is not None):
+    if not (ASM_GEMM and h.is_cuda and all(ctx.needs_input_grad[:3]) and h.dim() == 3 and h.shape[-1] % 256 == 0
+            and h.shape[-1] >= 1024
+            and HEAD_CHUNK_ROWS % 256 == 0 and w.dim() == 2 and w.shape[1] == h.shape[-1] and b is not None):
         return False
     B, n = h.shape[0], h.shape[1]
     pads = [-(-v // 256) * 256 for v in (Vt, w.shape[0] - Vt)]

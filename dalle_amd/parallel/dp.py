@@ -53,7 +53,7 @@ class GradSync:
         self.group = group
         self.grad_dtype = grad_dtype
         self.average = average
-        self.bucket_elems = max(1, bucket_bytes // 4)
+        self.bucket_elems = max(1, int(bucket_bytes) // 4)
         elems = self.bucket_elems
         self.buckets = [(s, min(s + elems, arena.numel)) for s in range(0, arena.numel, elems)]
         self._lowp = None
@@ -264,11 +264,17 @@ class GradSync:
 
 @torch.no_grad()
 def tune_grad_sync(arena: FlatArena, world_size: int, group=None, grad_dtype: str = "fp32",
-                   algos=("rccl", "rs_ag"), bucket_mb=(16, 32, 64, 128), reps: int = 3):
+                   algos=("rccl", "rs_ag"), bucket_mb=(16, 32, 64, 128), reps: int = 3, step_fn=None,
+                   overlap: bool = True, top: int = 3, step_reps: int = 2):
     """Time the full-arena gradient all-reduce for every (algorithm, bucket size) candidate on the real
     communicator and return ``(algo, bucket_bytes, table)`` of the fastest. Times are the max over ranks
     (``all_gather_object``), so every rank sees the same table and selects the same candidate. The arena
-    grads are restored afterwards. With one rank there is nothing to tune: the defaults come back."""
+    grads are restored afterwards. With one rank there is nothing to tune: the defaults come back.
+
+    ``step_fn(gs)``: a training step body (zero grads, forward, backward, ``gs.all_reduce()``) -- the
+    ``top`` standalone winners are then re-timed INSIDE it, with the candidate attached to the fused
+    backward (``overlap``), and the selection is made on that ``step_ms`` column: in the step most of the
+    bytes leave during backward, beside MFMA-heavy kernels, where the standalone order need not hold."""
     import time
 
     if world_size <= 1:
@@ -276,26 +282,47 @@ def tune_grad_sync(arena: FlatArena, world_size: int, group=None, grad_dtype: st
     g = arena.grad
     saved = g.clone()
     sync = torch.cuda.synchronize if g.is_cuda else (lambda: None)
+
+    def timed(fn, n):
+        sync()
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        sync()
+        t = (time.perf_counter() - t0) / n
+        ts = [None] * world_size
+        dist.all_gather_object(ts, t, group=group)
+        return max(ts)
+
     table = []
     for algo in algos:
         for mb in bucket_mb:
             gs = GradSync(arena, world_size=world_size, group=group, grad_dtype=grad_dtype,
-                          bucket_bytes=mb * 2 ** 20, algo=algo)
+                          bucket_bytes=int(mb * 2 ** 20), algo=algo)
             gs.all_reduce()          # warm-up: communicator paths, shard / wire buffers
-            sync()
-            dist.barrier(group=group)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                gs.all_reduce()
-            sync()
-            t = (time.perf_counter() - t0) / reps
-            ts = [None] * world_size
-            dist.all_gather_object(ts, t, group=group)
-            t = max(ts)
+            t = timed(gs.all_reduce, reps)
             nbytes = g.numel() * (2 if grad_dtype == "bf16" else 4)
             table.append({"algo": algo, "bucket_mb": mb, "ms": round(t * 1e3, 3),
-                          "busbw_GBps": round(2 * (world_size - 1) / world_size * nbytes / t / 1e9, 1)})
+                          "busbw_GBps": round(2 * (world_size - 1) / world_size * nbytes / t / 1e9, 1),
+                          "step_ms": None})
             g.copy_(saved)
-    best = min(table, key=lambda r: (r["ms"], r["algo"], r["bucket_mb"]))
+    key = "ms"
+    if step_fn is not None and len(table) > 1:
+        for row in sorted(table, key=lambda r: (r["ms"], r["algo"], r["bucket_mb"]))[:top]:
+            gs = GradSync(arena, world_size=world_size, group=group, grad_dtype=grad_dtype,
+                          bucket_bytes=int(row["bucket_mb"] * 2 ** 20), algo=row["algo"])
+            if overlap:
+                gs.attach()
+            try:
+                with torch.enable_grad():
+                    step_fn(gs)      # warm-up of this candidate inside the step
+                    row["step_ms"] = round(timed(lambda: step_fn(gs), step_reps) * 1e3, 3)
+            finally:
+                gs.detach()
+        key = "step_ms"
+    g.copy_(saved)
     del saved
-    return best["algo"], best["bucket_mb"] * 2 ** 20, table
+    ranked = [r for r in table if r[key] is not None]
+    best = min(ranked, key=lambda r: (r[key], r["algo"], r["bucket_mb"]))
+    return best["algo"], int(best["bucket_mb"] * 2 ** 20), table

@@ -883,21 +883,9 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
         dist.broadcast_object_list(meta, src=donor_global, group=self.group, device=dev if dev.type == "cuda" else None)
         skeleton, sched = meta[0]
         specs = _tensor_specs(skeleton)
-        for dtype in sorted({sp[1] for sp in specs}, key=str):
-            idx = [i for i, sp in enumerate(specs) if sp[1] == dtype]
-            total = sum(specs[i][2] for i in idx)
-            if rank == donor:
-                flat = torch.cat([tensors[i].detach().reshape(-1).to(dev) for i in idx]) if idx else None
-            else:
-                flat = torch.empty(total, dtype=dtype, device=dev)
-            dist.broadcast(flat, src=donor_global, group=self.group)
-            if rank != donor:
-                off = 0
-                for i in idx:
-                    n = specs[i][2]
-                    tensors.append((i, flat[off:off + n].view(specs[i][0])))
-                    off += n
+        received = _broadcast_state_tensors(tensors if rank == donor else None, specs, donor_global, self.group, dev)
         if rank != donor:
+            tensors = list(received.items())
             by_id = dict(tensors)
             self.load_state_dict(_fill_tensors(skeleton, by_id))
             if self.scheduler is not None and sched is not None:
@@ -939,6 +927,51 @@ class CollaborativeOptimizer(torch.optim.Optimizer):
     def shutdown(self):
         self.apply_pending()
         self.tracker.shutdown()
+
+
+STATE_CHUNK_BYTES = 128 * 2 ** 20   # staging window of a state transfer (one per rank, reused)
+
+
+def _broadcast_state_tensors(src, specs, donor_global, group, dev, chunk_bytes: int = None):
+    """Broadcast the state tensors of a transfer from the donor (``src`` = its tensors, in ``specs`` order;
+    None on receivers) in fixed windows: per dtype, the tensors form one virtual flat stream cut into windows of
+    ``chunk_bytes``; the donor packs each window into a staging buffer, broadcasts it, and every receiver scatters
+    it into the destination tensors it preallocated. The peak extra memory is one window per rank -- not a
+    second copy of the whole optimizer state (8-bit moments + absmax + fp32 tensors: GBs at the 1.3B scale).
+    Returns ``{index: tensor}`` on receivers, {} on the donor."""
+    chunk_bytes = chunk_bytes or STATE_CHUNK_BYTES
+    out = {}
+    for dtype in sorted({sp[1] for sp in specs}, key=str):
+        idx = [i for i, sp in enumerate(specs) if sp[1] == dtype]
+        if not idx:
+            continue
+        total = sum(specs[i][2] for i in idx)
+        win = max(1, chunk_bytes // torch.empty((), dtype=dtype).element_size())
+        stage = torch.empty(min(win, total), dtype=dtype, device=dev)
+        if src is None:
+            for i in idx:
+                out[i] = torch.empty(specs[i][0], dtype=dtype, device=dev)
+        flats = [(src[i] if src is not None else out[i]).reshape(-1) for i in idx]
+        starts, acc = [], 0
+        for i in idx:
+            starts.append(acc)
+            acc += specs[i][2]
+        for w0 in range(0, total, win):
+            w1 = min(total, w0 + win)
+            pieces = []   # (flat tensor, its [a, b) range, the window offset)
+            for f, st in zip(flats, starts):
+                a, b = max(w0, st), min(w1, st + f.numel())
+                if a < b:
+                    pieces.append((f, a - st, b - st, a - w0))
+            buf = stage[:w1 - w0]
+            if src is not None:
+                for f, a, b, o in pieces:
+                    buf[o:o + b - a].copy_(f[a:b].detach())
+            dist.broadcast(buf, src=donor_global, group=group)
+            if src is None:
+                for f, a, b, o in pieces:
+                    f[a:b].copy_(buf[o:o + b - a])
+    return out
 
 
 class _TensorSlot:

@@ -46,6 +46,34 @@ def test_asm_gemm_builds(tmp_path):
         assert "s_nop" not in body   # every wait state of the loop is an MFMA
 
 
+def test_kernel_generation_is_order_independent(tmp_path):
+    """Every kernel is generated from the default schedule knobs: the production set emitted in its own order
+    and in the reverse order with every diagnostic variant interleaved gives byte-identical production code."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import gen_gemm
+
+    fwd, rev = tmp_path / "fwd.s", tmp_path / "rev.s"
+    gen_gemm.main(str(fwd))
+    mix = []
+    for i, k in enumerate(gen_gemm.KERNELS):
+        mix += gen_gemm.DIAG_KERNELS[3 * i:3 * i + 3] + [k]
+    mix += gen_gemm.DIAG_KERNELS[3 * len(gen_gemm.KERNELS):]
+    gen_gemm.main(str(rev), kernels=list(reversed(mix)))
+    a, b = fwd.read_text(), rev.read_text()
+
+    def body(text, name):
+        i = text.index(f"{name}:\n")
+        return text[i:text.index(f"\t.size\t{name}", i)]
+
+    for name, _, _ in gen_gemm.KERNELS:
+        assert body(a, name) == body(b, name), name
+
+
+def test_default_build_skips_diagnostic_kernels():
+    src = open(os.path.join(ROOT, "csrc", "asm", "build_asm.py")).read()
+    assert 'os.environ.get("DALLE_AMD_BUILD_DIAG", "0") != "1"' in src
+
+
 def test_fragment_reads_are_bank_conflict_free():
     """The operand image layout (row-major 128-B rows, chunk c of row r at position c ^ ((r >> 1) & 7)) read as
     gen_gemm.lane_setup / frag_reads address it: under the ds_read_b128 lane grouping (4 groups of 16 lanes,
@@ -125,6 +153,22 @@ def test_fused_epilogue_kernels_on_the_emulator(tmp_path):
     text = s.read_text()
     assert emu.selftest_geglu_bwd(text, M=2560, F=256, grid=8, wgs=(0,))
     assert emu.selftest_qkv(text, col=True, T=257, S=16, H=4, B=2, grid=8, wgs=[0])
+
+
+def test_fused_kernels_at_k2048_on_the_emulator(tmp_path):
+    """The fused kernels at K = 2048 (the ~1.3B config's d_model): the successor tile's unrolled K-steps 0..13
+    hand over to the ordinary K-loop for steps 14..29 before the tail -- one workgroup walking two or three
+    tiles of the GEGLU backward, FF-in + GEGLU and QKV + rotary kernels."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc", "asm"))
+    import emu
+    import gen_gemm
+
+    s = tmp_path / "g.s"
+    gen_gemm.main(str(s))
+    text = s.read_text()
+    assert emu.selftest_geglu_bwd(text, M=2560, F=256, K=2048, grid=8, wgs=(0,))
+    assert emu.selftest_geglu(text, M=4096, F=256, K=2048, grid=8, wgs=[0], rows=slice(0, 256))
+    assert emu.selftest_qkv(text, col=False, T=257, S=16, H=4, B=4, K=2048, grid=8, wgs=[0])
 
 
 def test_plain_kernel_deferred_paths_on_the_emulator(tmp_path):

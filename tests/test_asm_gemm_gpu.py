@@ -85,15 +85,15 @@ def test_weight_grad_routes_to_asm(cuda, C):
     assert hip_ops.PATH_COUNTS.get("asm_wgrad", 0) == before + 1
 
 
-@pytest.mark.parametrize("M,F", [(512, 1024), (10240, 4096), (2560, 512)])
-def test_asm_ff_in_geglu(cuda, C, M, F):
+@pytest.mark.parametrize("M,F,K", [(512, 1024, 1024), (10240, 4096, 1024), (2560, 512, 1024), (5120, 8192, 2048)])
+def test_asm_ff_in_geglu(cuda, C, M, F, K):
     """FF-in GEMM + GEGLU in one assembly kernel (permuted W1 rows, u from the stored bf16 pre-activation,
     deferred under the next tile's K-steps): a vs fp32 x W1^T + b1, u vs the unfused GEGLU of that a."""
     from dalle_amd.ops import hip_ops
 
     torch.manual_seed(M + F)
-    x = torch.randn(M, 1024, device=cuda).to(torch.bfloat16)
-    w1 = torch.randn(2 * F, 1024, device=cuda) * 0.03
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w1 = torch.randn(2 * F, K, device=cuda) * 0.03
     b1 = torch.randn(2 * F, device=cuda) * 0.1
     a, u = hip_ops.ff_in_geglu(x, w1, b1)
     ref_a = x.float() @ w1.to(torch.bfloat16).float().t() + b1
@@ -104,9 +104,9 @@ def test_asm_ff_in_geglu(cuda, C, M, F):
     assert torch.equal(u, C.geglu_fwd(a)) or ((u.float() - C.geglu_fwd(a).float()).abs().max() <= 2 ** -6 * ref_u.abs().max())
 
 
-@pytest.mark.parametrize("B", [2, 8])
+@pytest.mark.parametrize("B,H", [(2, 16), (8, 16), (8, 32)])
 @pytest.mark.parametrize("col", [False, True])
-def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B):
+def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B, H):
     """QKV projection + 3-axis rotary on the assembly kernel (rotation deferred onto the stored bf16 values) ==
     the unfused path (the projection, then rope_fwd on its bf16 output) on the reference geometry
     (257 text + 32x32 image tokens, 16 heads: tiles straddle the text / image boundary). Two samples = 120
@@ -116,11 +116,12 @@ def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B):
     from dalle_amd.ops.hip_ops import _cs3_from_tables, _rope_tables
 
     torch.manual_seed(7)
-    T, S, H = 257, 32, 16
+    T, S = 257, 32
+    d = H * 64          # 16 heads: d_model 1024 (K-steps 0..13 unrolled + tail); 32 heads: d_model 2048 (+ 16 looped)
     n = T + S * S - 1
     geom = AttnGeometry(T, S, 5)
-    h = torch.randn(B * n, 1024, device=cuda).to(torch.bfloat16)
-    w = (torch.randn(3 * H * 64, 1024, device=cuda) * 0.03).to(torch.bfloat16)
+    h = torch.randn(B * n, d, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(3 * H * 64, d, device=cuda) * 0.03).to(torch.bfloat16)
     cos, sin = _rope_tables(geom, 64, cuda)
     q, k, v = C.asm_qkv_rope(h, w, _cs3_from_tables(cos, sin, 0.125), T, S, H, n, col)
     qkv = (h.float() @ w.float().t()).to(torch.bfloat16).view(B, n, -1)
@@ -131,14 +132,14 @@ def test_asm_qkv_rope_matches_separate_path(cuda, C, col, B):
         assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("M,F", [(512, 256), (2560, 1024), (20480, 4096)])
-def test_asm_ff_dgrad_geglu(cuda, C, M, F):
+@pytest.mark.parametrize("M,F,K", [(512, 256, 1024), (2560, 1024, 1024), (20480, 4096, 1024), (10240, 8192, 2048)])
+def test_asm_ff_dgrad_geglu(cuda, C, M, F, K):
     """FF-out dgrad + GEGLU backward + FF-in bias column sums on the assembly kernel vs fp32: du = bf16(dy W2),
     da_value = du gelu(gate), da_gate = du value gelu'(gate) (exact erf GELU), db = column sums of (da_value,
     da_gate). 20480 x 4096 = 1280 tiles: workgroups walk several (the deferred path)."""
     torch.manual_seed(M + F)
-    dy = torch.randn(M, 1024, device=cuda).to(torch.bfloat16)
-    w2t = (torch.randn(F, 1024, device=cuda) * 0.03).to(torch.bfloat16)
+    dy = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w2t = (torch.randn(F, K, device=cuda) * 0.03).to(torch.bfloat16)
     h = torch.randn(M, 2 * F, device=cuda).to(torch.bfloat16)
     dh, db = C.asm_ff_dgrad_geglu(dy, w2t, h, None)
     du = (dy.float() @ w2t.float().t()).to(torch.bfloat16).float()

@@ -11,6 +11,36 @@ from dalle_amd.optim import FlatArena, LAMB8bit
 pytestmark = pytest.mark.gpu
 
 
+def param_class(name: str) -> str:
+    """parameter class of a DALLE state-dict name: sublayer kind + the module's own name, without layer indices
+    (transformer.layers.layers.3.1.fn.fn.fn.net.0.weight -> ff.net.0.weight)"""
+    import re
+
+    m = re.match(r"transformer\.layers\.layers\.\d+\.(\d)\.(.*)$", name)
+    if not m:
+        return name
+    rest = re.sub(r"^(fn\.)+", "", m.group(2))
+    return ("attn." if m.group(1) == "0" else "ff.") + rest
+
+
+def grad_errors(m_hip, m_ref) -> dict:
+    """worst relative gradient error (||g - g_ref|| / ||g_ref||) per parameter class"""
+    ref = dict(m_ref.named_parameters())
+    out = {}
+    for name, p in m_hip.named_parameters():
+        g, gr = p.grad.float().cpu(), ref[name].grad
+        rel = ((g - gr).norm() / (gr.norm() + 1e-12)).item()
+        c = param_class(name)
+        out[c] = max(out.get(c, 0.0), rel)
+    return out
+
+
+def report(tag: str, errs: dict) -> None:
+    import json
+
+    print(f"GRAD_ERR {tag} " + json.dumps({k: round(v, 5) for k, v in sorted(errs.items())}))
+
+
 def _cfg(reversible):
     c = tiny(reversible)
     types = ["axial_row", "axial_col", "conv_like", "full"]
@@ -33,15 +63,9 @@ def test_model_hip_matches_reference(cuda, reversible):
     loss = m_hip(text.to(cuda), img.to(cuda), return_loss=True)
     loss.backward()
     assert abs(loss.item() - loss_ref.item()) < 2e-2 * abs(loss_ref.item())
-    ref_params = dict(m_ref.named_parameters())
-    worst = 0.0
-    for name, p in m_hip.named_parameters():
-        gr = ref_params[name].grad
-        g = p.grad.float().cpu()
-        rel = ((g - gr).norm() / (gr.norm() + 1e-8)).item()
-        worst = max(worst, rel)
-        assert rel < 0.1, (name, rel)
-    print("worst grad rel err", worst)
+    errs = grad_errors(m_hip, m_ref)
+    report(f"tiny_rev{int(reversible)}", errs)
+    assert max(errs.values()) < 0.1, errs
 
 
 def test_fused_lamb_matches_torch_path(cuda):
@@ -311,14 +335,44 @@ def test_reference_geometry_end_to_end(cuda, reversible, asm, monkeypatch):
     loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
     loss_ref.backward()
     assert abs(loss.item() - loss_ref.item()) < 5e-3 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
-    ref = dict(m_ref.named_parameters())
-    worst = 0.0
-    for name, p in m_hip.named_parameters():
-        g, gr = p.grad.float().cpu(), ref[name].grad
-        rel = ((g - gr).norm() / (gr.norm() + 1e-12)).item()
-        worst = max(worst, rel)
-        assert rel < 0.05, (name, rel)
-    print(f"reference geometry: loss {loss.item():.5f} vs {loss_ref.item():.5f}, worst grad rel err {worst:.4f}")
+    errs = grad_errors(m_hip, m_ref)
+    report(f"refgeom_rev{int(reversible)}_asm{int(asm)}", errs)
+    assert max(errs.values()) < 0.05, errs
+
+
+@pytest.mark.parametrize("reversible", [False, True])
+def test_1p3b_geometry_on_the_assembly_kernels(cuda, reversible):
+    """BASELINE config 4's layer geometry (d_model 2048, 32 heads, 256 text + 32x32 image tokens, unshared
+    layers) at depth 2, B = 2: QKV + rotary, FF-in + GEGLU, FF-dgrad + GEGLU backward and the tied head all run
+    on the assembly kernels at K = 2048 (their successor K-steps 14..29 in the plain loop). Loss and every
+    gradient vs the fp32 PyTorch model on the CPU."""
+    from dalle_amd.config import large_1p3b, reference_attn_types
+    from dalle_amd.data.synthetic import synthetic_batch
+    from dalle_amd.ops import hip_ops
+
+    torch.manual_seed(0)
+    big = large_1p3b()
+    cfg = DALLEConfig(**{**big.to_dict(), "depth": 2, "attn_types": reference_attn_types(2), "shared_attn_ids": [0, 1],
+                         "shared_ff_ids": [0, 1], "reversible": reversible})
+    assert cfg.dim == 2048 and cfg.heads == 32
+    m_ref = DALLE(cfg)
+    m_hip = copy.deepcopy(m_ref).to(cuda)
+    FlatArena(m_hip.parameters(), device=cuda)
+    b = synthetic_batch(2, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens, cfg.num_image_tokens,
+                        torch.Generator().manual_seed(3))
+    hip_ops.PATH_COUNTS.clear()
+    loss = m_hip(b["input_ids"].to(cuda), b["image"].to(cuda), mask=b["attention_mask"].to(cuda), return_loss=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    for path in ("asm_qkv_rope", "asm_ff_in_geglu", "asm_ff_dgrad_geglu", "asm_head", "asm_wgrad"):
+        assert hip_ops.PATH_COUNTS.get(path, 0) > 0, (path, hip_ops.PATH_COUNTS)
+    torch.set_num_threads(16)
+    loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
+    loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 5e-3 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
+    errs = grad_errors(m_hip, m_ref)
+    report(f"1p3b_rev{int(reversible)}", errs)
+    assert max(errs.values()) < 0.05, errs
 
 
 @pytest.mark.parametrize("reversible", [False, True])

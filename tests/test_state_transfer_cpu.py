@@ -4,17 +4,22 @@ tensor shapes / dtypes) is an object broadcast. Checked on CPU/gloo with 2 ranks
 moments are several MB: no pickled payload over 1 MB, and the joiner's state equals the donor's."""
 import pickle
 
+import pytest
 import torch
 import torch.distributed as dist
 
 from test_collab_cpu import _init, _run
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, chunk=None):
     try:
         _init(rank, world, port)
         from dalle_amd.optim import LAMB8bit, get_linear_schedule_with_warmup
+        from dalle_amd.parallel import optimizer as copt_mod
         from dalle_amd.parallel.optimizer import CollaborativeOptimizer
+
+        if chunk:
+            copt_mod.STATE_CHUNK_BYTES = chunk   # windows that cut through tensors
 
         sizes = []
         orig = dist.broadcast_object_list
@@ -50,9 +55,12 @@ def _worker(rank, world, port, q):
         q.put(pickle.dumps(("error", rank, traceback.format_exc())))
 
 
-def test_state_transfer_moves_tensors_not_pickles():
+@pytest.mark.parametrize("chunk", [None, 1000003])
+def test_state_transfer_moves_tensors_not_pickles(chunk):
+    """(chunk: the transfer's staging window -- the default 128 MB, or ~1 MB so every moment tensor straddles
+    several windows)"""
     (r0, rec0, ep0, w0, s10, s20, a0, sb0, step0, le0, big0), (r1, rec1, ep1, w1, s11, s21, a1, sb1, step1, le1, big1) = \
-        _run(_worker, 2)
+        _run(_worker, 2, chunk)
     assert not rec0 and rec1 and ep0 == ep1 == 5
     assert torch.equal(w0, w1)
     assert s10.dtype == torch.uint8 and s10.numel() > 1 << 20
