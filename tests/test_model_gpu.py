@@ -16,11 +16,29 @@ def param_class(name: str) -> str:
     (transformer.layers.layers.3.1.fn.fn.fn.net.0.weight -> ff.net.0.weight)"""
     import re
 
-    m = re.match(r"transformer\.layers\.layers\.\d+\.(\d)\.(.*)$", name)
-    if not m:
-        return name
-    rest = re.sub(r"^(fn\.)+", "", m.group(2))
-    return ("attn." if m.group(1) == "0" else "ff.") + rest
+    m = re.match(r"transformer\.layers\.layers\.\d+\.(\d)\.(.*)$", name)          # sequential stack
+    if m:
+        kind = "attn." if m.group(1) == "0" else "ff."
+    else:
+        m = re.match(r"transformer\.layers\.blocks\.\d+\.([fg])\.net\.(.*)$", name)  # reversible stack
+        if not m:
+            return name
+        kind = "attn." if m.group(1) == "f" else "ff."
+    return kind + re.sub(r"^(fn\.)+", "", m.group(2))
+
+
+# Per-class bounds on the relative gradient error (||g - g_ref|| / ||g_ref||, HIP bf16 path vs the fp32 CPU
+# model), pinned at ~2x the worst value measured over every configuration below on the round-6 tree
+# (profiles/r6_grad_err_pinned.txt: 0.0026-0.0074 for the layer parameters). The final LayerNorm bias of the
+# reversible models is the sum over rows of a gradient that nearly cancels (measured up to 0.028): its own bound.
+GRAD_BOUNDS = {"to_logits.0.bias": 0.06, "to_logits.1.bias": 0.02, "to_logits.0.weight": 0.008,
+               "to_logits.1.weight": 0.012}
+GRAD_BOUND_LAYER = 0.015
+
+
+def check_grad_errors(errs: dict) -> None:
+    bad = {k: v for k, v in errs.items() if v > GRAD_BOUNDS.get(k, GRAD_BOUND_LAYER)}
+    assert not bad, bad
 
 
 def grad_errors(m_hip, m_ref) -> dict:
@@ -65,7 +83,7 @@ def test_model_hip_matches_reference(cuda, reversible):
     assert abs(loss.item() - loss_ref.item()) < 2e-2 * abs(loss_ref.item())
     errs = grad_errors(m_hip, m_ref)
     report(f"tiny_rev{int(reversible)}", errs)
-    assert max(errs.values()) < 0.1, errs
+    check_grad_errors(errs)
 
 
 def test_fused_lamb_matches_torch_path(cuda):
@@ -337,7 +355,7 @@ def test_reference_geometry_end_to_end(cuda, reversible, asm, monkeypatch):
     assert abs(loss.item() - loss_ref.item()) < 5e-3 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
     errs = grad_errors(m_hip, m_ref)
     report(f"refgeom_rev{int(reversible)}_asm{int(asm)}", errs)
-    assert max(errs.values()) < 0.05, errs
+    check_grad_errors(errs)
 
 
 @pytest.mark.parametrize("reversible", [False, True])
@@ -372,7 +390,44 @@ def test_1p3b_geometry_on_the_assembly_kernels(cuda, reversible):
     assert abs(loss.item() - loss_ref.item()) < 5e-3 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
     errs = grad_errors(m_hip, m_ref)
     report(f"1p3b_rev{int(reversible)}", errs)
-    assert max(errs.values()) < 0.05, errs
+    check_grad_errors(errs)
+
+
+def test_loss_trajectory_20_lamb_steps(cuda):
+    """20 LAMB steps on the reference geometry (d 1024, 16 heads, 256 text + 32x32 image tokens, the recipe's
+    attention / sharing cycle, depth 2): the HIP path (flat arena, fused LAMB) against the fp32 PyTorch model and
+    the torch LAMB on the CPU, same init, same batches. Every step's loss stays within 1 % of the reference."""
+    from dalle_amd.config import reference_attn_types, reference_shared_ids
+    from dalle_amd.data.synthetic import synthetic_batch
+
+    torch.manual_seed(0)
+    cfg = DALLEConfig(depth=2, attn_types=reference_attn_types(2), shared_attn_ids=reference_shared_ids(2),
+                      shared_ff_ids=reference_shared_ids(2), reversible=False)
+    m_ref = DALLE(cfg)
+    m_hip = copy.deepcopy(m_ref).to(cuda)
+    arena = FlatArena(m_hip.parameters(), device=cuda)
+    kw = dict(lr=2e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.0, max_grad_norm=4.0, optim_bits=32)
+    opt_hip = LAMB8bit(m_hip.parameters(), arena=arena, **kw)
+    opt_ref = LAMB8bit(m_ref.parameters(), **kw)
+    gen = torch.Generator().manual_seed(5)
+    batches = [synthetic_batch(2, cfg.text_seq_len, cfg.image_seq_len, cfg.num_text_tokens, cfg.num_image_tokens, gen)
+               for _ in range(4)]
+    torch.set_num_threads(16)
+    dev = []
+    for step in range(20):
+        b = batches[step % 4]
+        arena.zero_grad()
+        loss = m_hip(b["input_ids"].to(cuda), b["image"].to(cuda), mask=b["attention_mask"].to(cuda), return_loss=True)
+        loss.backward()
+        opt_hip.step()
+        opt_ref.zero_grad(set_to_none=True)
+        loss_ref = m_ref(b["input_ids"], b["image"], mask=b["attention_mask"], return_loss=True)
+        loss_ref.backward()
+        opt_ref.step()
+        dev.append(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))
+        print(f"step {step}: hip {loss.item():.5f} ref {loss_ref.item():.5f}")
+    print("TRAJ max rel dev", max(dev))
+    assert max(dev) < 1e-2, dev
 
 
 @pytest.mark.parametrize("reversible", [False, True])
