@@ -47,15 +47,16 @@ def wgrad_sweep(M):
                 part = torch.bmm(g.view(s, M // s, N).transpose(1, 2), x.view(s, M // s, K), out_dtype=torch.float32)
                 C.splitk_accum_(acc, part, True)
             res[f"s{s}_TF"] = round(fl / timeit(f) / 1e9)
-        # hand-written MN-major MFMA kernel (gemm_wgrad_), every split count that tiles the tokens
+        # the assembly TN weight-grad kernel (asm_wgrad_: token-major operands, split-K slabs + fold), every
+        # split count whose K-range tiles
         ref = g.float().t() @ x.float()
         for s in (1, 2, 4, 5, 8, 16):
-            if M % (64 * s):
+            if M % s or (M // s) % 128 or M // s < 256:
                 continue
             out = torch.zeros(N, K, device=dev)
-            C.gemm_wgrad_(g, x, out, s, True)
-            res[f"own_s{s}_relerr"] = float((out - ref).norm() / ref.norm())
-            res[f"own_s{s}_TF"] = round(fl / timeit(lambda s=s: C.gemm_wgrad_(g, x, acc, s, True)) / 1e9)
+            C.asm_wgrad_(out, g, x, s, True)
+            res[f"asm_s{s}_relerr"] = float((out - ref).norm() / ref.norm())
+            res[f"asm_s{s}_TF"] = round(fl / timeit(lambda s=s: C.asm_wgrad_(acc, g, x, s, True)) / 1e9)
         print(json.dumps(res), flush=True)
 
 

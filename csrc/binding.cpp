@@ -14,7 +14,8 @@ namespace dalle {
 
 void attn_fwd(const void*, const void*, const void*, void*, float*, const AttnGeom&, int, hipStream_t);
 void attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, float*, void*, void*,
-              void*, const AttnGeom&, int, hipStream_t, const float*, const float*, void*, float);
+              void*, const AttnGeom&, int, hipStream_t, const float*, const float*, void*, float, const float* rotf = nullptr,
+              int rot_nl = 0, int rot_np = 0, float rot_img_text_pos = 0.f, float rot_text_axial = 0.f);
 void rope_fwd(const void*, const float*, const float*, void*, void*, void*, const RopeGeom&, int, float, hipStream_t);
 void rope_bwd(const void*, const void*, const void*, const float*, const float*, void*, const RopeGeom&, int, float, hipStream_t);
 bool ln_shift_fwd(const float*, const float*, const float*, void*, float*, float*, const ShiftGeom&, int, int, float, hipStream_t,
@@ -331,8 +332,12 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor do
 
 // Attention backward with the rotary backward fused into its epilogues: returns dqkv (B, n, 3*H*64)
 // directly (no (B*H, Np, 64) dq / dk / dv intermediates, no rope_bwd pass).
+// rotf (optional): the rotary frequencies of rotary.rotary_freq_split ((64,) fp32 on the device) with their axis
+// split (n_lang, n_pix) and fixed positions -- given, the axial S = 32 backward runs as the fused one-workgroup-
+// per-head kernel, which computes the rotary angles in-kernel instead of reading the tables
 Tensor attn_bwd_rope(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, Tensor cosT, Tensor sinT, int64_t B,
-                     int64_t T, int64_t S, int64_t n, int64_t K, int64_t H, int64_t pattern, double qscale) {
+                     int64_t T, int64_t S, int64_t n, int64_t K, int64_t H, int64_t pattern, double qscale,
+                     c10::optional<Tensor> rotf, int64_t n_lang, int64_t n_pix, double img_text_pos, double text_axial) {
   CHECK_IN(q, torch::kBFloat16); CHECK_IN(k, torch::kBFloat16); CHECK_IN(v, torch::kBFloat16);
   CHECK_IN(out, torch::kBFloat16); CHECK_IN(dout, torch::kBFloat16); CHECK_IN(lse, torch::kFloat32);
   CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
@@ -345,9 +350,16 @@ Tensor attn_bwd_rope(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tens
               "attn_bwd_rope: rotary tables must be (>= n, 64)");
   auto delta = torch::empty({B * H, g.Np}, lse.options());
   auto dqkv = torch::empty({B, n, 3 * H * 64}, q.options());
+  const float* rf = nullptr;
+  if (rotf.has_value() && rotf->defined()) {
+    CHECK_IN((*rotf), torch::kFloat32);
+    TORCH_CHECK(rotf->numel() == 64 && n_lang >= 0 && n_pix >= 0 && n_lang + 2 * n_pix <= 32, "attn_bwd_rope: rotf (64,) + axis split");
+    rf = rotf->data_ptr<float>();
+  }
   dalle::attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                   delta.data_ptr<float>(), nullptr, nullptr, nullptr, g, B * H, cur_stream(),
-                  cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(), (float)qscale);
+                  cosT.data_ptr<float>(), sinT.data_ptr<float>(), dqkv.data_ptr(), (float)qscale, rf, (int)n_lang, (int)n_pix,
+                  (float)img_text_pos, (float)text_axial);
   return dqkv;
 }
 
@@ -1281,7 +1293,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_bwd", &rope_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
-  m.def("attn_bwd_rope", &attn_bwd_rope);
+  m.def("attn_bwd_rope", &attn_bwd_rope, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("dout"),
+        py::arg("lse"), py::arg("cosT"), py::arg("sinT"), py::arg("B"), py::arg("T"), py::arg("S"), py::arg("n"), py::arg("K"),
+        py::arg("H"), py::arg("pattern"), py::arg("qscale"), py::arg("rotf") = py::none(), py::arg("n_lang") = 0,
+        py::arg("n_pix") = 0, py::arg("img_text_pos") = 0.0, py::arg("text_axial") = 0.0);
   m.def("geglu_fwd", &geglu_fwd);
   m.def("geglu_bwd", &geglu_bwd);
   m.def("geglu_bwd_bias", &geglu_bwd_bias, py::arg("h"), py::arg("dout"), py::arg("gb") = py::none());

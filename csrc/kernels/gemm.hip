@@ -208,13 +208,7 @@ __device__ __forceinline__ void epi_store16(s16x8* dst, const s16x8& v, int nt) 
   else *dst = v;
 }
 
-static int gemm_nt_store_default() {
-  static const int v = [] {
-    const char* e = (const char*)nullptr;
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+static int gemm_nt_store_default() { return 0; }
 
 __device__ __forceinline__ int rope_epi_seq2st(const RopeEpi& e, int p) {
   if (p < e.T) return p;
@@ -957,19 +951,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_2wg_kernel(const __bf16* __res
 }
 
 // former switch GEGLU_BWD_2WG=1: the FF-out dgrad + GEGLU backward on the two-workgroup kernel (gemm_set_geglu_bwd_2wg)
-static int g_geglu_bwd_2wg = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 0;
-}();
+static int g_geglu_bwd_2wg = 0;
 void gemm_set_geglu_bwd_2wg(int v) { g_geglu_bwd_2wg = v; }
 // former switch 2WG_STAGGER=<ticks>[,<first_wave>] (10 ns ticks; first_wave < 0: delay the second slot's first
 // workgroups, > 0: the 4-phase stagger_start over the first first_wave workgroups)
-static int g_2wg_stagger[2] = {-1, -256};
+static int g_2wg_stagger[2] = {0, -256};
 static void w2_stagger(RopeEpi& e) {
-  if (g_2wg_stagger[0] < 0) {
-    g_2wg_stagger[0] = 0;
-    if (const char* s = (const char*)nullptr) sscanf(s, "%d,%d", &g_2wg_stagger[0], &g_2wg_stagger[1]);
-  }
   e.stagger = g_2wg_stagger[0];
   e.first_wave = g_2wg_stagger[1];
 }

@@ -812,21 +812,12 @@ static int pt_grid(int ntiles) {
     if (cus <= 0) cus = 256;
   }
   // one workgroup per CU (128 KiB of LDS); a multiple of 8 keeps each workgroup on one XCD's range.
-  // former switch PT_GRID caps the workgroup count (measurement: epilogue cost vs concurrent storers)
-  const char* gcap = (const char*)nullptr;
-  if (gcap && atoi(gcap) > 0 && atoi(gcap) < cus) return atoi(gcap) < ntiles ? atoi(gcap) : ntiles;
   int g = cus < ntiles ? cus : ntiles;
   if (g > 8 && ntiles > g) g &= ~7;
   return g;
 }
 
-static int pt_persist_default() {
-  static const int v = [] {
-    const char* s = (const char*)nullptr;
-    return s ? atoi(s) : 0;
-  }();
-  return v;
-}
+static int pt_persist_default() { return 0; }
 
 static int pt_cus() {
   static int cus = 0;
@@ -844,22 +835,14 @@ static int pt_cus() {
 // measured SLOWER on every training shape (e.g. M61440 N1024 K8192 874 vs 766 us, N3072 K1024 374 vs 359;
 // profiles/r3_gemm_stagger.jsonl) -- the stores' cost is not the simultaneity of the epilogues.
 int gemm_stagger_ticks(int ntiles, int K) {
-  static const int pct = [] {
-    const char* s = (const char*)nullptr;
-    return s ? atoi(s) : 0;
-  }();
-  const int cus = pt_cus();
-  if (pct <= 0 || ntiles <= cus) return 0;
-  const double tile_s = 2.0 * 256.0 * 256.0 * K / (1.3e15 / cus);
-  return (int)(tile_s * pct / 100.0 * 1e8);
+  (void)ntiles;
+  (void)K;
+  return 0;
 }
 
 // former switch GEMM_CPOL: cache policy of every hand-written GEMM's output stores (common.h cstore16);
 // gemm_set_cpol overrides it at run time (benchmarks)
-static int g_gemm_cpol = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 0;
-}();
+static int g_gemm_cpol = 0;
 void gemm_set_cpol(int c) { g_gemm_cpol = c; }
 int gemm_cpol() { return g_gemm_cpol; }
 
@@ -867,38 +850,23 @@ int gemm_cpol() { return g_gemm_cpol; }
 // vmcnt(0)) before it ends. Measured: a one-tile-per-workgroup GEMM whose waves end with their
 // epilogue stores still in flight runs 4-11 % slower than the same kernel draining them first
 // (profiles/r3_gemm_epilogue_stamps.jsonl); gemm_set_drain overrides it at run time
-static int g_gemm_drain = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 1;
-}();
+static int g_gemm_drain = 1;
 void gemm_set_drain(int d) { g_gemm_drain = d; }
 int gemm_drain() { return g_gemm_drain; }
 
 // former switch GEMM_LINES (default 1): epilogue stores of whole 128-B lines (8 rows x 128 B per store
 // instruction, lines16) instead of 16 rows x 64 B; gemm_set_lines overrides it at run time (benchmarks)
-static int g_gemm_lines = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 1;
-}();
+static int g_gemm_lines = 1;
 void gemm_set_lines(int v) { g_gemm_lines = v; }
 // former switch GEMM_PREFETCH (default 0 until measured): the FF-out dgrad + GEGLU-backward GEMM prefetches
 // its epilogue's pre-activation lines during the main loop; gemm_set_prefetch overrides it at run time
-static int g_gemm_prefetch = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 0;
-}();
+static int g_gemm_prefetch = 0;
 void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
 // former switch PT_OVERLAP (default 0; measured slower at every B128 shape): persistent plain GEMMs (no bias) issue a tile's stores beside the next
 // tile's first K-step (see gemm_pt_kernel phase 1); former switch PT_STAGGER=<percent of one tile>: start the
 // persistent workgroups at four phases so their epilogues do not all hit HBM at once
-static int g_pt_overlap = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 0;
-}();
-static int g_pt_stagger = [] {
-  const char* s = (const char*)nullptr;
-  return s ? atoi(s) : 0;
-}();
+static int g_pt_overlap = 0;
+static int g_pt_stagger = 0;
 void gemm_set_pt_overlap(int v, int stagger_pct) {
   g_pt_overlap = v;
   g_pt_stagger = stagger_pct;
@@ -946,13 +914,7 @@ static void pt_launch(const void* A, const void* B, int M, int N, int K, PtArgs&
 
 static bool pt_shape_ok(int M, int N, int K) { return M > 0 && N > 0 && M % pt::BM == 0 && N % pt::BN == 0 && K % pt::BK == 0 && K >= 2 * pt::BK; }
 
-static int pt_group_default() {
-  static const int v = [] {
-    const char* s = (const char*)nullptr;
-    return s ? atoi(s) : 4;
-  }();
-  return v;
-}
+static int pt_group_default() { return 4; }
 
 // C (M, ldc) = A B^T (+ bias); epi 5 = main loop only (measurement)
 bool gemm_pt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int ldc, int epi, int group,

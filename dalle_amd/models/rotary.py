@@ -82,6 +82,36 @@ def rotary_tables(text_len: int, image_size: int, dim_head: int, device=None):
     return cos, sin
 
 
+IMAGE_TEXT_POS = 8192.0   # the text position of every image token (rotary_angles)
+TEXT_AXIAL_POS = -10.0    # the axial (row / column) position of every text token
+
+
+@lru_cache(maxsize=16)
+def _freq_split_cpu(dim_head: int):
+    """The rotary frequencies per pair in revolutions per position unit, for angles computed in a kernel
+    (the fused attention backward): (64,) fp32 = hi[32] + lo[32] with hi rounded to a 12-bit mantissa (so that
+    position x hi is exact in fp32 for positions of <= 12 significant bits: text positions, 8192, -10) and lo the
+    remainder; pairs [0, n_lang) turn with the text position, the next n_pix with the image row coordinate
+    (linspace(-1, 1, S)), the next n_pix with the column coordinate, the rest (if any) not at all."""
+    rot_dim = dim_head // 3
+    f = torch.cat([_lang_freqs(rot_dim), _pixel_freqs(rot_dim), _pixel_freqs(rot_dim)]) / (2.0 * math.pi)
+    n_lang, n_pix = _lang_freqs(rot_dim).numel(), _pixel_freqs(rot_dim).numel()
+    assert f.numel() <= dim_head // 2 <= 32
+    hi = torch.zeros(32, dtype=torch.float64)
+    lo = torch.zeros(32, dtype=torch.float64)
+    for j, v in enumerate(f.tolist()):
+        m, e = math.frexp(v)
+        h = math.ldexp(round(m * 4096.0) / 4096.0, e)
+        hi[j], lo[j] = h, v - h
+    return torch.cat([hi, lo]).float().contiguous(), n_lang, n_pix
+
+
+def rotary_freq_split(dim_head: int, device=None):
+    """``(rotf, n_lang, n_pix, image_text_pos, text_axial_pos)`` for ``attn_bwd_rope`` (see _freq_split_cpu)."""
+    t, n_lang, n_pix = _freq_split_cpu(dim_head)
+    return (t.to(device) if device is not None else t), n_lang, n_pix, IMAGE_TEXT_POS, TEXT_AXIAL_POS
+
+
 def rotate_pairs(x: torch.Tensor) -> torch.Tensor:
     """(x0, x1) -> (x1, x0) on interleaved pairs (sign lives in the sin table)."""
     shp = x.shape

@@ -184,6 +184,20 @@ def _rope_tables(geom: AttnGeometry, dim_head: int, device):
 
 
 _cs_tables: Dict[tuple, torch.Tensor] = {}
+_rot_freq_cache: Dict[str, tuple] = {}
+
+
+def _rot_freqs(device) -> tuple:
+    """(rotf, n_lang, n_pix, image_text_pos, text_axial_pos) of the 64-dim heads on ``device`` (cached): the fused
+    attention backward computes the rotary angles in-kernel from these (rotary.rotary_freq_split)."""
+    key = str(device)
+    t = _rot_freq_cache.get(key)
+    if t is None:
+        from ..models.rotary import rotary_freq_split
+
+        t = rotary_freq_split(64, device)
+        _rot_freq_cache[key] = t
+    return t
 
 
 def rope_cs_table(geom: AttnGeometry, dim_head: int, device) -> torch.Tensor:
@@ -582,7 +596,7 @@ class _AttnCore(torch.autograd.Function):
         q, k, v, out, lse, cos, sin = ctx.saved_tensors
         B, T, S, n, K, H, pattern, col = ctx.geo
         gout = gout.to(torch.bfloat16).contiguous()
-        dqkv = C().attn_bwd_rope(q, k, v, out, gout, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125)
+        dqkv = C().attn_bwd_rope(q, k, v, out, gout, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125, *_rot_freqs(q.device))
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -663,7 +677,8 @@ def _attn_core_bwd(saved, params, dy):
     do = input_grad(dy, w_out).view(out.shape)
     dwo = weight_grad(w_out, dy, o2)
     # rotary backward inside the attention-backward epilogues
-    dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125).view(B * n, -1)
+    dqkv = C().attn_bwd_rope(q, k, v, out, do, lse, cos, sin, B, T, S, n, K, H, pattern, 0.125,
+                             *_rot_freqs(q.device)).view(B * n, -1)
     del do
     dh = input_grad(dqkv, w_qkv).view(x.shape)
     dwq = weight_grad(w_qkv, dqkv, h2)

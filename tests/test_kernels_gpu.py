@@ -307,9 +307,47 @@ def test_fused_rotary_backward_matches_separate_pass(cuda, attn_type):
     assert _rel(grads[0], grads[1]) < 8e-3, attn_type
 
 
+@pytest.mark.parametrize("T,B,H", [(257, 2, 3), (260, 1, 2), (65, 2, 2), (1, 1, 1), (256, 1, 2), (261, 1, 1)])
+@pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
+def test_fused_one_workgroup_backward(cuda, attn_type, T, B, H, monkeypatch):
+    """The one-workgroup-per-head axial backward (S = 32: dQ, dK, dV from one S / dP per tile pair, the 9th
+    text tile's real keys accumulated in LDS) == the two-kernel backward (DALLE_AMD_ATTN_FUSED_BWD=0) to bf16
+    resolution, and the fp32 reference. The fused kernel computes the rotary angles in-kernel (frequencies
+    of rotary.rotary_freq_split), the two-kernel form reads the tables: this also pins the two against each other."""
+    from dalle_amd.models.patterns import PATTERN_IDS
+    from dalle_amd.ops import hip_ops
+
+    C = hip_ops.C()
+    torch.manual_seed(11 + T)
+    S = 32
+    n = T + S * S - 1
+    geom = AttnGeometry(T, S, 5)
+    qkv = torch.randn(B, n, 3 * H * 64, device=cuda).to(torch.bfloat16)
+    g = torch.randn(B, n, H * 64, device=cuda).to(torch.bfloat16)
+    cos, sin = rotary_tables(T, S, 64, device=cuda)
+    col, pat = attn_type == "axial_col", PATTERN_IDS[attn_type]
+    q, k, v = C.rope_fwd(qkv, cos, sin, T, S, H, col, 0.125)
+    out, lse = C.attn_fwd(q, k, v, B, T, S, n, geom.kernel_size, H, pat)
+    rf = hip_ops._rot_freqs(q.device)
+    monkeypatch.setenv("DALLE_AMD_ATTN_FUSED_BWD", "1")
+    fused = C.attn_bwd_rope(q, k, v, out, g, lse, cos, sin, B, T, S, n, geom.kernel_size, H, pat, 0.125, *rf).float()
+    monkeypatch.setenv("DALLE_AMD_ATTN_FUSED_BWD", "0")
+    two = C.attn_bwd_rope(q, k, v, out, g, lse, cos, sin, B, T, S, n, geom.kernel_size, H, pat, 0.125, *rf).float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(fused).all()
+    assert _rel(fused, two) < 8e-3, (attn_type, T)
+    for part in range(3):   # q, k and v gradients each (a missing store would hide in the total)
+        sl = slice(part * H * 64, (part + 1) * H * 64)
+        assert _rel(fused[..., sl], two[..., sl]) < 8e-3, (attn_type, T, part)
+    xr = qkv.float().requires_grad_(True)
+    qr, kr, vr = ref.qkv_rotary(xr, H, cos, sin)
+    ref.sparse_attention_core(qr, kr, vr, geom, attn_type).backward(g.float())
+    assert _rel(fused.view_as(xr.grad), xr.grad) < 3e-2, attn_type
+
+
 @pytest.mark.parametrize("S", [16, 32])
 @pytest.mark.parametrize("attn_type", ["axial_row", "axial_col"])
-def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S):
+def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S, monkeypatch):
     """Axial patterns: the image keys' dK / dV computed inside the dQ kernel (the rotary-fused backward the
     model runs) must match the separate key-centric kernel's (attn_bwd + rope_bwd) to bf16 resolution, and the
     fp32 reference."""
@@ -317,6 +355,7 @@ def test_axial_local_dkdv_fused_into_dq_kernel(cuda, attn_type, S):
     from dalle_amd.ops import hip_ops
 
     C = hip_ops.C()
+    monkeypatch.setenv("DALLE_AMD_ATTN_FUSED_BWD", "0")   # the two-kernel form (the fused one: test above)
     torch.manual_seed(5)
     T, B, H = 65, 2, 2
     n = T + S * S - 1
