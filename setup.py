@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 hip_sources = [
     "csrc/binding.cpp",
     "csrc/kernels/attention.hip",
+    "csrc/kernels/attention_fused.hip",
     "csrc/kernels/rotary.hip",
     "csrc/kernels/layernorm_shift.hip",
     "csrc/kernels/elementwise.hip",

@@ -396,7 +396,8 @@ def test_1p3b_geometry_on_the_assembly_kernels(cuda, reversible):
 def test_loss_trajectory_20_lamb_steps(cuda):
     """20 LAMB steps on the reference geometry (d 1024, 16 heads, 256 text + 32x32 image tokens, the recipe's
     attention / sharing cycle, depth 2): the HIP path (flat arena, fused LAMB) against the fp32 PyTorch model and
-    the torch LAMB on the CPU, same init, same batches. Every step's loss stays within 1 % of the reference."""
+    the torch LAMB on the CPU, same init, same batches. Every step's loss stays within 0.1 % of the reference
+    (measured max 7.3e-5 relative over the 20 steps, profiles/r6_grad_err_pinned.txt)."""
     from dalle_amd.config import reference_attn_types, reference_shared_ids
     from dalle_amd.data.synthetic import synthetic_batch
 
@@ -427,7 +428,7 @@ def test_loss_trajectory_20_lamb_steps(cuda):
         dev.append(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))
         print(f"step {step}: hip {loss.item():.5f} ref {loss_ref.item():.5f}")
     print("TRAJ max rel dev", max(dev))
-    assert max(dev) < 1e-2, dev
+    assert max(dev) < 1e-3, dev
 
 
 @pytest.mark.parametrize("reversible", [False, True])
