@@ -67,6 +67,8 @@ void prefill_rope(const void*, const float*, const float*, void*, void*, void*, 
 void decode_attn_part(const float*, int, const float*, const float*, float, void*, void*, void*, const int*, const DecodeGeom&, int,
                       hipStream_t);
 bool skinny_partials(SkinnyArgs, hipStream_t);
+bool skinny_partials_ln(SkinnyArgs, hipStream_t);
+bool skinny_partials_ln_ok(int, int, int);
 int skinny_partials_ks(int, int, int);
 void skinny_partials_config(int, int);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
@@ -793,6 +795,46 @@ Tensor skinny_partials(Tensor X, Tensor W) {
   return part;
 }
 
+// The residual projection's split-K slabs with the NEXT LayerNorm in the same launch (skinny EPI 5): x +=
+// scale * (X W^T + bias), then y = shift(LN(x)) with the LN history row at *pos -- decode_ln_shift_ folded
+// into the projection's last workgroups. cnt: this launch site's ticket word (int32, zeroed once per
+// generate call), err: set to 1 if a tail gave up waiting.
+void skinny_partials_ln_(Tensor X, Tensor W, c10::optional<Tensor> bias, Tensor scale, Tensor x, Tensor ln_w, Tensor ln_b,
+                         Tensor hist, Tensor y, Tensor pos, int64_t T, int64_t S, bool shift, Tensor cnt, Tensor err) {
+  CHECK_CUDA(X); CHECK_DT(X, torch::kBFloat16); CHECK_IN(W, torch::kBFloat16);
+  CHECK_IN(scale, torch::kFloat32); CHECK_IN(x, torch::kFloat32); CHECK_IN(ln_w, torch::kFloat32); CHECK_IN(ln_b, torch::kFloat32);
+  CHECK_IN(hist, torch::kBFloat16); CHECK_IN(y, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
+  CHECK_CUDA(cnt); CHECK_DT(cnt, torch::kInt32); CHECK_CUDA(err); CHECK_DT(err, torch::kInt32);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && W.dim() == 2 && X.size(1) == W.size(1), "skinny_partials_ln_: X (M, K), W (N, K)");
+  const int M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && N % 16 == 0 && K % 128 == 0 && X.stride(0) % 8 == 0, "skinny_partials_ln_: shapes");
+  TORCH_CHECK(dalle::skinny_partials_ln_ok(M, N, K), "skinny_partials_ln_: no tail tiling for this shape");
+  TORCH_CHECK(x.numel() == (int64_t)M * N && y.numel() == (int64_t)M * N && scale.numel() == N && ln_w.numel() == N &&
+              ln_b.numel() == N, "skinny_partials_ln_: row / parameter sizes");
+  TORCH_CHECK(hist.dim() == 3 && hist.size(0) == M && hist.size(2) == N, "skinny_partials_ln_: hist (M, n, N)");
+  TORCH_CHECK(cnt.numel() >= 1 && err.numel() >= 1, "skinny_partials_ln_: counter / error words");
+  const int KS = dalle::skinny_partials_ks(M, N, K);
+  auto part = torch::empty({KS, M, N}, X.options().dtype(torch::kFloat32));
+  dalle::SkinnyArgs a{};
+  a.X = X.data_ptr(); a.W = W.data_ptr(); a.M = M; a.N = N; a.K = K; a.ldx = X.stride(0); a.KS = KS;
+  a.out = part.data_ptr();
+  a.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN((*bias), torch::kBFloat16);
+    TORCH_CHECK(bias->numel() == N, "skinny_partials_ln_: bias size");
+    a.bias = bias->data_ptr();
+  }
+  a.scale = scale.data_ptr<float>();
+  a.resid = x.data_ptr<float>();
+  a.ln_w = ln_w.data_ptr<float>(); a.ln_b = ln_b.data_ptr<float>();
+  a.hist = hist.data_ptr(); a.y = y.data_ptr();
+  a.pos = pos.data_ptr<int>(); a.n = hist.size(1);
+  a.T = T; a.S = S; a.shift = shift ? 1 : 0;
+  a.cnt = cnt.data_ptr<int>();
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  TORCH_CHECK(dalle::skinny_partials_ln(a, cur_stream()), "skinny_partials_ln_: unsupported shape");
+}
+
 Tensor skinny_geglu(Tensor X, Tensor W, c10::optional<Tensor> bias, Tensor cnt) {
   TORCH_CHECK(W.size(0) % 2 == 0, "skinny_geglu: W holds the value and gate halves");
   Tensor ws;
@@ -1378,6 +1420,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attn_", &decode_attn_);
   m.def("skinny_linear", &skinny_linear);
   m.def("skinny_partials", &skinny_partials);
+  m.def("skinny_partials_ln_", &skinny_partials_ln_, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("scale"), py::arg("x"),
+        py::arg("ln_w"), py::arg("ln_b"), py::arg("hist"), py::arg("y"), py::arg("pos"), py::arg("T"), py::arg("S"),
+        py::arg("shift"), py::arg("cnt"), py::arg("err"));
+  m.def("skinny_partials_ln_ok", [](int64_t M, int64_t N, int64_t K) { return dalle::skinny_partials_ln_ok(M, N, K); });
   m.def("skinny_partials_config", &dalle::skinny_partials_config);
   m.def("residual_from_partials_", &residual_from_partials_, py::arg("x"), py::arg("part"), py::arg("pbias"), py::arg("pscale"));
   m.def("decode_attn_part_", &decode_attn_part_);

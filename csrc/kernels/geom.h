@@ -78,6 +78,16 @@ struct SkinnyArgs {
   int H, n;
   float qscale;
   int dbg;  // benchmark-only: bit 0 skips the X loads, bit 1 the W loads
+  // EPI 5 (split-K slabs + LayerNorm tail): the slabs (a.out) are stored write-through, every workgroup
+  // takes a ticket on *cnt, and the last M arrivers each finish one row: resid += scale * (sum + bias),
+  // then the decode LayerNorm + cached token shift of that row (ln_w / ln_b, LN history `hist` (M, n, N)
+  // bf16 at *pos, shifted row to `y` (M, N) bf16); T / S: text length / image side, shift: 0 = plain LN
+  const float* ln_w;
+  const float* ln_b;
+  void* hist;
+  void* y;
+  int T, S, shift;
+  unsigned* err;  // set to 1 if a tail's wait for the other workgroups gave up (bounded spin)
 };
 
 // Fused decode sampler (sample.hip): top-k / top-p / temperature / Gumbel-max + token bookkeeping.

@@ -26,6 +26,122 @@ namespace dalle {
 constexpr int SK_U = 4;            // MFMA steps per wave (K = 128 per wave)
 constexpr int SK_KW = 32 * SK_U;   // K elements per wave
 
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// ---- EPI 5 tail: one row of the pending residual update, then the decode LayerNorm + cached token shift ----
+// (the same arithmetic as decode_ln_shift_kernel in decode.hip, which does it as a launch of its own). The KS
+// split-K slabs of the row were stored write-through (sc1) by the other workgroups of this launch, so every
+// load of them here is an agent-scope (sc1) load; everything else was written by earlier launches.
+// NT threads, CH chunks of 4 columns per thread (N <= 4 * NT * CH; columns past N idle), KS <= KSM slabs.
+template <int NT, int CH, int KSM>
+__device__ __forceinline__ void ln_tail_row(const SkinnyArgs& a, int row, int pos) {
+  constexpr int NW = NT / 64;
+  __shared__ float tred[2][NW], tpiv[NW];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int D = a.N, B = a.M;
+  float* xr = a.resid + (size_t)row * D;
+  __bf16* hb = static_cast<__bf16*>(a.hist) + (size_t)row * a.n * D;
+  const float* part = static_cast<const float*>(a.out);
+  f32x4 v[CH], wv[CH], bv[CH], sc[CH];
+  s16x4 sh[CH], pbr[CH];
+  unsigned long long t[CH][KSM][2];
+  // every load first (one memory round trip): slabs, the row, the LN and pending parameters, the shifted row
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch) {
+    const int c = 4 * (tid + ch * NT);
+    const bool in = c < D;
+    const int cc = in ? c : 0;  // idle columns re-read column 0 and are masked out of everything below
+#pragma unroll
+    for (int k = 0; k < KSM; ++k) {
+      const int kk = k < a.KS ? k : a.KS - 1;  // slabs past KS re-read the last one and are weighted 0
+      gu64* p = (gu64*)(part + ((size_t)kk * B + row) * D + cc);
+      t[ch][k][0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t[ch][k][1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    v[ch] = *reinterpret_cast<const f32x4*>(xr + cc);
+    wv[ch] = *reinterpret_cast<const f32x4*>(a.ln_w + cc);
+    bv[ch] = *reinterpret_cast<const f32x4*>(a.ln_b + cc);
+    sc[ch] = *reinterpret_cast<const f32x4*>(a.scale + cc);
+    pbr[ch] = a.bias ? *reinterpret_cast<const s16x4*>(static_cast<const __bf16*>(a.bias) + cc) : s16x4{};
+    sh[ch] = s16x4{};
+    if (a.shift && cc < D / 2) {
+      int src = -1;
+      if (pos < a.T) {
+        src = pos - 1;
+      } else {
+        const int k = pos - a.T;
+        if (cc < D / 4) src = (k >= a.S) ? pos - a.S : -1;
+        else src = (k % a.S) ? pos - 1 : -1;
+      }
+      if (src >= 0) sh[ch] = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + cc);
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch) {
+    const int c = 4 * (tid + ch * NT);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KSM; ++k) {  // fixed ks order: deterministic
+      const float wk = k < a.KS ? 1.f : 0.f;
+      acc[0] += wk * __uint_as_float((unsigned)t[ch][k][0]);
+      acc[1] += wk * __uint_as_float((unsigned)(t[ch][k][0] >> 32));
+      acc[2] += wk * __uint_as_float((unsigned)t[ch][k][1]);
+      acc[3] += wk * __uint_as_float((unsigned)(t[ch][k][1] >> 32));
+    }
+    float pb[4];
+    unpack4(pbr[ch], pb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[ch][i] += sc[ch][i] * (acc[i] + pb[i]);
+    if (c < D) *reinterpret_cast<f32x4*>(xr + c) = v[ch];
+  }
+  // both moments in one reduction round, shifted about each wave's first element (as decode_ln_shift); a wave's
+  // element count from the columns it holds (every wave holds at least column 4 * 64 * wave < D, or none)
+  const float piv = __shfl(v[0][0], 0, 64);
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = 4 * (tid + ch * NT) < D ? v[ch][i] - piv : 0.f;
+      s += d;
+      q += d * d;
+    }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if (lane == 0) { tred[0][wave] = s; tred[1][wave] = q; tpiv[wave] = piv; }
+  __syncthreads();
+  const float p0 = tpiv[0];
+  float S = 0.f, Q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    int cnt = 0;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) cnt += min(max(D - 4 * (ch * NT + 64 * i), 0), 256);
+    if (cnt == 0) continue;
+    const float dp = tpiv[i] - p0, si = tred[0][i], n = (float)cnt;
+    S += si + n * dp;
+    Q += tred[1][i] + 2.f * dp * si + n * dp * dp;
+  }
+  const float inv_d = 1.0f / (float)D;
+  const float dm = S * inv_d;
+  const float mean = p0 + dm;
+  const float var = fmaxf(Q * inv_d - dm * dm, 0.f);
+  const float rstd = rsqrtf(var + 1e-5f);
+  __bf16* yr = static_cast<__bf16*>(a.y) + (size_t)row * D;
+#pragma unroll
+  for (int ch = 0; ch < CH; ++ch) {
+    const int c = 4 * (tid + ch * NT);
+    if (c >= D) continue;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[ch][i] - mean) * rstd * wv[ch][i] + bv[ch][i];
+    const s16x4 packed = pack4(o);
+    *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
+    *reinterpret_cast<s16x4*>(yr + c) = (a.shift && c < D / 2) ? sh[ch] : packed;
+  }
+}
+
 // MB: 16-row M-blocks; NBV: 16-column output blocks per wave (they share the wave's X fragments, so
 // X bytes per W byte fall as 4 / NBV at M = 64); EPI 1 (GEGLU) adds NBV gate blocks; WK: waves per
 // workgroup, each on its own 128-wide K chunk.
@@ -123,7 +239,7 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
   // Partials are written and read with agent-scope (device-coherent, L2-bypassing `sc1`) accesses and
   // ordered by vmcnt + barrier only: a __threadfence() here would write back and invalidate the L2
   // of the XCD on every workgroup (measured 5x slower).
-  if (a.KS > 1 && EPI != 4) {
+  if (a.KS > 1 && EPI != 4 && EPI != 5) {
 #pragma unroll
     for (int c = 0; c < PPT; ++c) {
       const int idx = tid + c * NT;
@@ -177,6 +293,12 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
       *reinterpret_cast<float2*>(reinterpret_cast<float*>(a.out) + ((size_t)ks * a.M + row) * a.N + col) = make_float2(y0, y1);
       continue;
     }
+    if (EPI == 5) {  // the same slab, stored write-through (sc1): read back in this launch by the tail workgroups
+      gu64* sp = (gu64*)(reinterpret_cast<float*>(a.out) + ((size_t)ks * a.M + row) * a.N + col);
+      __hip_atomic_store(sp, (unsigned long long)__float_as_uint(y0) | ((unsigned long long)__float_as_uint(y1) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
     if (bias != nullptr) { y0 += (float)bias[col]; y1 += (float)bias[col + 1]; }
     if (EPI == 0) {
       if (a.out_f32) {
@@ -213,6 +335,41 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
       }
       *reinterpret_cast<uint32_t*>(dst) = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
     }
+  }
+  if constexpr (EPI == 5) {
+    // hand-off (guide Guideline 16, R1 with a ticket counter): every storing wave drains its sc1 slab stores,
+    // the workgroup meets, ONE lane takes a ticket. Tickets of one launch are [e * total, (e + 1) * total)
+    // for the e-th launch on this counter word (every workgroup takes exactly one), so the epoch comes from
+    // the ticket itself and no per-launch reset or argument is needed under graph replay.
+    __shared__ unsigned s_tk;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_tk = __hip_atomic_fetch_add((gu32*)a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned total = gridDim.x * gridDim.y, tk = s_tk, within = tk % total;
+    if (within < total - (unsigned)a.M) return;  // not one of the last M arrivers
+    const int trow = (int)(within - (total - (unsigned)a.M));
+    if (tid == 0) {
+      // the last M arrivers wait for the rest of the launch: every workgroup with a smaller ticket has
+      // already added, so this waits at most for the other tail workgroups' adds (all resident: they run)
+      const unsigned target = (tk / total + 1) * total;
+      unsigned spins = 0;
+      while (__hip_atomic_load((gu32*)a.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) {  // bounded: never hang the device on a lost arrival
+          __hip_atomic_store((gu32*)a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    const int pos = *a.pos;
+    if (pos < 0 || pos >= a.n) return;  // a replay past the cache end is a no-op, as decode_ln_shift
+    constexpr int NT = 64 * WK;
+    const int ch = (a.N + 4 * NT - 1) / (4 * NT);
+    if (ch == 1) ln_tail_row<NT, 1, 8>(a, trow, pos);
+    else if (ch == 2) ln_tail_row<NT, 2, 8>(a, trow, pos);
+    else if (ch == 4) ln_tail_row<NT, 4, 4>(a, trow, pos);
   }
 }
 
@@ -326,6 +483,33 @@ bool skinny_partials(SkinnyArgs a, hipStream_t st) {
   a.dbg = g_dbg;
   skinny_launch<4>(a, dim3(a.N / 16, KS), 1, WK, st);
   return true;
+}
+
+// The same split-K slabs with the consumer's LayerNorm in the launch's tail (EPI 5): the last M workgroups to
+// finish each take one row (see ln_tail_row). False where the tail's register tiling does not fit (then the
+// caller keeps the separate decode_ln_shift launch).
+bool skinny_partials_ln(SkinnyArgs a, hipStream_t st) {
+  if (a.M < 1 || a.M > 64 || a.N % 16 || a.K % SK_KW) return false;
+  const int chunks = a.K / SK_KW;
+  const int KS = skinny_partials_ks(a.M, a.N, a.K);
+  const int WK = chunks / KS;
+  if (KS != a.KS || !skinny_valid(a.M, a.N, a.K, 1, 1, WK)) return false;
+  const int NT = 64 * WK, ch = (a.N + 4 * NT - 1) / (4 * NT);
+  if (!(((ch == 1 || ch == 2) && KS <= 8) || (ch == 4 && KS <= 4))) return false;
+  if ((a.N / 16) * KS < a.M) return false;  // fewer workgroups than tail rows
+  a.steps = 1;
+  a.dbg = g_dbg;
+  const dim3 grid(a.N / 16, KS);
+  if (a.M <= 16) skinny_launch_wk<1, 1, 5>(a, grid, WK, st);
+  else if (a.M <= 32) skinny_launch_wk<2, 1, 5>(a, grid, WK, st);
+  else skinny_launch_wk<4, 1, 5>(a, grid, WK, st);
+  return true;
+}
+bool skinny_partials_ln_ok(int M, int N, int K) {
+  if (M < 1 || M > 64 || N % 16 || K % SK_KW) return false;
+  const int KS = skinny_partials_ks(M, N, K), WK = (K / SK_KW) / KS, NT = 64 * WK;
+  const int ch = (N + 4 * NT - 1) / (4 * NT);
+  return (((ch == 1 || ch == 2) && KS <= 8) || (ch == 4 && KS <= 4)) && (N / 16) * KS >= M;
 }
 
 // Host entry (the binding validates tensors); false for unsupported shapes.

@@ -48,12 +48,17 @@ def gumbel_sample(logits: torch.Tensor, temperature: float = 1.0, generator=None
 
 class DecodeEngine:
     def __init__(self, model, batch_size: int, device=None, use_hip: Optional[bool] = None, skinny: bool = True,
-                 partials: int = 2, fused_sampler: bool = True):
+                 partials: int = 2, fused_sampler: bool = True, ln_tail: Optional[bool] = None):
         """``skinny``: decode projections on the skinny MFMA GEMM with fused epilogues (when the shapes allow);
         ``partials``: 2 = every projection leaves split-K slabs summed by its consumer (measured fastest,
         profiles/r2_decode_partials_ab.txt), 1 = the residual projections only, 0 = in-GEMM split-K hand-off;
-        ``fused_sampler``: the one-kernel top-k / top-p / Gumbel sampler (K18). The non-default forms are
-        kept for the numerics A/B in tests/test_generation_gpu.py."""
+        ``fused_sampler``: the one-kernel top-k / top-p / Gumbel sampler (K18); ``ln_tail`` (None: env
+        DALLE_AMD_DECODE_LN_TAIL, default off): the out-proj / FF-out slabs and the next LayerNorm + shift in ONE
+        launch (skinny EPI 5: the projection's last workgroups finish the rows) instead of the projection
+        plus a decode_ln_shift launch -- 5 instead of 7 launches per layer, but measured slower
+        (profiles/r6_decode_ln_tail.txt: 14.2 vs 16.8 images/s at batch 64; the in-launch hand-off's
+        write-through, ticket, poll and read-back round trips cost more than the kernel boundary they remove).
+        The non-default forms are kept for the numerics A/B in tests/test_generation_gpu.py."""
         self.model = model
         cfg = self.cfg = model.cfg
         self.B = batch_size
@@ -100,7 +105,22 @@ class DecodeEngine:
         mode = int(partials) if self.skinny else 0
         self.partials = mode in (1, 2)
         self.qkv_partials = mode == 2
-        self._pending = None  # (stream, partial slabs, bias, LayerScale) not yet added to the stream
+        # pending residual update of a stream, not yet applied: ("part", stream, slabs, bias, LayerScale) -- slabs
+        # already computed -- or ("gemm", stream, X, W, bias, LayerScale) -- the projection itself deferred, so
+        # that it runs as one launch with the LayerNorm that reads the stream (skinny_partials_ln_)
+        self._pending = None
+        if ln_tail is None:
+            import os
+            ln_tail = os.environ.get("DALLE_AMD_DECODE_LN_TAIL", "0") == "1"
+        self.ln_tail = False
+        if self.partials and ln_tail:
+            from ..ops.hip_ops import C
+            ok = C().skinny_partials_ln_ok
+            self.ln_tail = ok(B, self.d, self.H * self.Dh) and ok(B, self.d, cfg.ff_mult * self.d)
+        # one ticket word per fused launch site of a step (2 per layer), zeroed per generate call; error word
+        self.ln_cnt = torch.zeros(2 * L + 2, dtype=torch.int32, device=dev) if self.ln_tail else None
+        self.ln_err = torch.zeros(1, dtype=torch.int32, device=dev) if self.ln_tail else None
+        self._site = 0
 
     # -- weights (one bf16 cast per generate call) --------------------------------------------------
     def _wt(self, p):
@@ -121,25 +141,41 @@ class DecodeEngine:
                 w.copy_(p.detach().reshape(w.shape))
         for k in self.kc + self.vc:
             k.zero_()
+        if self.ln_cnt is not None:
+            self.ln_cnt.zero_()
+            self.ln_err.zero_()
 
     # -- branch steps -------------------------------------------------------------------------------
     def _flush_pending(self):
         if self._pending is not None:
             from ..ops.hip_ops import C
-            x, part, bias, scale = self._pending
+            kind, x, *rest = self._pending
             self._pending = None
-            C().residual_from_partials_(x, part, bias, scale)
+            if kind == "gemm":
+                X, W, bias, scale = rest
+                C().residual_from_partials_(x, C().skinny_partials(X, W), bias, scale)
+            else:
+                part, bias, scale = rest
+                C().residual_from_partials_(x, part, bias, scale)
 
     def _ln_shift(self, ls, hist, x):
         pre = ls.fn
         if self.use_hip:
             from ..ops.hip_ops import C
             pend = self._pending
-            if pend is not None and pend[0] is not x:
+            if pend is not None and pend[1] is not x:
                 self._flush_pending()
                 pend = None
             self._pending = None
-            part, pbias, pscale = (pend[1], pend[2], pend[3]) if pend is not None else (None, None, None)
+            if pend is not None and pend[0] == "gemm":
+                _, _, X, W, pbias, pscale = pend
+                site = self._site
+                self._site += 1
+                C().skinny_partials_ln_(X, W, pbias, pscale, x, pre.norm.weight.detach(), pre.norm.bias.detach(), hist,
+                                        self.hbuf, self.pos, self.T, self.S, bool(pre.fn.enabled),
+                                        self.ln_cnt[site:site + 1], self.ln_err)
+                return self.hbuf
+            part, pbias, pscale = (pend[2], pend[3], pend[4]) if pend is not None else (None, None, None)
             C().decode_ln_shift_(x, pre.norm.weight.detach(), pre.norm.bias.detach(), hist, self.hbuf, self.pos,
                                  self.T, self.S, bool(pre.fn.enabled), part, pbias, pscale)
             return self.hbuf
@@ -175,9 +211,13 @@ class DecodeEngine:
                                  self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
             C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
                              self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+        if self.ln_tail:
+            self._pending = ("gemm", x_res, self.obuf, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias),
+                             self._scale(ls))
+            return x_res
         if self.partials:
             po = C().skinny_partials(self.obuf, self._wt(attn.to_out[0].weight))
-            self._pending = (x_res, po, self._wt(attn.to_out[0].bias), self._scale(ls))
+            self._pending = ("part", x_res, po, self._wt(attn.to_out[0].bias), self._scale(ls))
             return x_res
         C().skinny_residual_(x_res, self.obuf, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias),
                              self._scale(ls), self.sk_cnt)
@@ -191,8 +231,12 @@ class DecodeEngine:
         ff = ls.fn.fn.fn
         h = self._ln_shift(ls, self.hist[li][1], x_in)
         a = C().skinny_geglu(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias), self.sk_cnt)
+        if self.ln_tail:
+            self._pending = ("gemm", x_res, a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias), self._scale(ls))
+            return x_res
         if self.partials:
-            self._pending = (x_res, C().skinny_partials(a, self._wt(ff.net[3].weight)), self._wt(ff.net[3].bias), self._scale(ls))
+            self._pending = ("part", x_res, C().skinny_partials(a, self._wt(ff.net[3].weight)), self._wt(ff.net[3].bias),
+                             self._scale(ls))
             return x_res
         C().skinny_residual_(x_res, a, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias), self._scale(ls), self.sk_cnt)
         return x_res
@@ -262,6 +306,7 @@ class DecodeEngine:
         W = self.model.to_logits[1].weight
         x = F.embedding(self.tok, W.detach()).float()
         self._pending = None
+        self._site = 0
         if self.cfg.reversible:
             x1, x2 = x, x.clone()
             for li, (f, g) in enumerate(self.pairs):
