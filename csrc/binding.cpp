@@ -70,7 +70,6 @@ bool skinny_partials(SkinnyArgs, hipStream_t);
 bool skinny_partials_ln(SkinnyArgs, hipStream_t);
 bool skinny_partials_ln_ok(int, int, int);
 int skinny_partials_ks(int, int, int);
-void skinny_partials_config(int, int);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
                  hipStream_t);
 void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
@@ -80,16 +79,11 @@ bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, i
 void column_sum(const float*, int, int, const GradSink&, hipStream_t);
 bool gemm_pt(const void*, const void*, void*, const void*, int, int, int, int, int, int, hipStream_t);
 void gemm_set_cpol(int);
-int gemm_cpol();
-void gemm_set_lines(int);
-void gemm_set_prefetch(int);
 void gemm_set_pt_overlap(int, int);
 void gemm_set_geglu_bwd_2wg(int);
 void gemm_set_2wg_stagger(int, int);
 bool gemm_2wg(const void*, const void*, void*, const void*, int, int, int, hipStream_t);
-int gemm_lines();
 void gemm_set_drain(int);
-int gemm_drain();
 bool gemm_pt_qkv_rope(const void*, const void*, void*, void*, void*, const float*, int, int, int, int, int, int, int, float,
                       hipStream_t, int);
 bool gemm_pt_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
@@ -1363,10 +1357,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("variant") = 0);
   m.def("gemm_set_cpol", [](int64_t c) { dalle::gemm_set_cpol((int)c); }, py::arg("cpol"),
         "cache policy of the hand-written GEMMs' output stores: 0 plain, 1 sc0, 2 nt, 16 sc1, 17 sc0 sc1");
-  m.def("gemm_cpol", []() { return (int64_t)dalle::gemm_cpol(); });
-  m.def("gemm_set_lines", [](int64_t v) { dalle::gemm_set_lines((int)v); }, py::arg("lines"),
-        "1: register-epilogue GEMM stores of whole 128-B lines (default), 0: 16 rows x 64 B per store");
-  m.def("gemm_lines", []() { return (int64_t)dalle::gemm_lines(); });
   m.def("gemm_set_geglu_bwd_2wg", [](int64_t v) { dalle::gemm_set_geglu_bwd_2wg((int)v); }, py::arg("v"),
         "1: FF-out dgrad + GEGLU backward on the two-workgroups-per-CU kernel");
   m.def("gemm_set_2wg_stagger", [](int64_t ticks, int64_t first_wave) { dalle::gemm_set_2wg_stagger((int)ticks, (int)first_wave); },
@@ -1383,11 +1373,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_pt_overlap", [](int64_t v, int64_t stagger) { dalle::gemm_set_pt_overlap((int)v, (int)stagger); },
         py::arg("overlap"), py::arg("stagger_pct") = 0,
         "persistent plain GEMM: epilogue stores beside the next tile's first K-step; start stagger in % of a tile");
-  m.def("gemm_set_prefetch", [](int64_t v) { dalle::gemm_set_prefetch((int)v); }, py::arg("prefetch"),
-        "1: the FF-out dgrad + GEGLU-backward GEMM prefetches its epilogue's pre-activation lines in the main loop");
   m.def("gemm_set_drain", [](int64_t d) { dalle::gemm_set_drain((int)d); }, py::arg("drain"),
         "1: hand-written GEMM workgroups wait for their output stores before ending");
-  m.def("gemm_drain", []() { return (int64_t)dalle::gemm_drain(); });
   m.def("asm_gemm", &asm_gemm, py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out") = py::none());
   m.def("asm_qkv_rope", &asm_qkv_rope, py::arg("h"), py::arg("w"), py::arg("cs3"), py::arg("T"), py::arg("S"), py::arg("H"),
         py::arg("n"), py::arg("col_major"));
@@ -1424,7 +1411,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ln_w"), py::arg("ln_b"), py::arg("hist"), py::arg("y"), py::arg("pos"), py::arg("T"), py::arg("S"),
         py::arg("shift"), py::arg("cnt"), py::arg("err"));
   m.def("skinny_partials_ln_ok", [](int64_t M, int64_t N, int64_t K) { return dalle::skinny_partials_ln_ok(M, N, K); });
-  m.def("skinny_partials_config", &dalle::skinny_partials_config);
   m.def("residual_from_partials_", &residual_from_partials_, py::arg("x"), py::arg("part"), py::arg("pbias"), py::arg("pscale"));
   m.def("decode_attn_part_", &decode_attn_part_);
   m.def("skinny_force_config", &dalle::skinny_force_config);

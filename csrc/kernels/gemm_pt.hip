@@ -855,13 +855,11 @@ void gemm_set_drain(int d) { g_gemm_drain = d; }
 int gemm_drain() { return g_gemm_drain; }
 
 // former switch GEMM_LINES (default 1): epilogue stores of whole 128-B lines (8 rows x 128 B per store
-// instruction, lines16) instead of 16 rows x 64 B; gemm_set_lines overrides it at run time (benchmarks)
-static int g_gemm_lines = 1;
-void gemm_set_lines(int v) { g_gemm_lines = v; }
+// instruction, lines16) instead of 16 rows x 64 B
+static const int g_gemm_lines = 1;
 // former switch GEMM_PREFETCH (default 0 until measured): the FF-out dgrad + GEGLU-backward GEMM prefetches
-// its epilogue's pre-activation lines during the main loop; gemm_set_prefetch overrides it at run time
-static int g_gemm_prefetch = 0;
-void gemm_set_prefetch(int v) { g_gemm_prefetch = v; }
+// its epilogue's pre-activation lines during the main loop (off)
+static const int g_gemm_prefetch = 0;
 // former switch PT_OVERLAP (default 0; measured slower at every B128 shape): persistent plain GEMMs (no bias) issue a tile's stores beside the next
 // tile's first K-step (see gemm_pt_kernel phase 1); former switch PT_STAGGER=<percent of one tile>: start the
 // persistent workgroups at four phases so their epilogues do not all hit HBM at once
@@ -871,7 +869,6 @@ void gemm_set_pt_overlap(int v, int stagger_pct) {
   g_pt_overlap = v;
   g_pt_stagger = stagger_pct;
 }
-int gemm_lines() { return g_gemm_lines; }
 
 template <int EPI, bool LINES>
 static void pt_launch_k(const void* A, const void* B, int M, int N, int K, PtArgs& e, hipStream_t st, int persist, int ntiles) {

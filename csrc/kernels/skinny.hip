@@ -461,15 +461,10 @@ static void skinny_launch(const SkinnyArgs& a, dim3 grid, int NBV, int WK, hipSt
 // Split-K partials for a consumer that sums them (EPI 4): every workgroup covers 16 columns x a
 // 128 * WK slice of K and stores its fp32 slab; no hand-off between workgroups, so K is split as finely
 // as the X bytes per CU want (the kernel is bound by the X rows each CU reads, see skinny_shape).
-static int g_part_wk[2] = {0, 0};  // override for K < 4096 / K >= 4096 (0: measured default)
-void skinny_partials_config(int wk_small, int wk_large) {
-  g_part_wk[0] = wk_small;
-  g_part_wk[1] = wk_large;
-}
 int skinny_partials_ks(int M, int N, int K) {
   const int chunks = K / SK_KW;
   const int big = K >= 4096;
-  int wk = g_part_wk[big] > 0 ? g_part_wk[big] : (big ? 4 : 2);
+  int wk = big ? 4 : 2;  // waves per workgroup (measured: benchmarks/bench_skinny.py)
   while (wk > 1 && (chunks % wk || !skinny_valid(M, N, K, 1, 1, wk))) wk >>= 1;
   return chunks / wk;
 }
