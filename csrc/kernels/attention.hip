@@ -372,17 +372,15 @@ __device__ __forceinline__ void dq_tile(f32x16& dq0, f32x16& dq1, const __bf16* 
 // query tile -- its own row's (column's) -- so that tile's dK / dV are produced right here, by the wave
 // that owns the query tile, from the K / V it already staged and the Q / dO it already holds: the
 // separate image-key dK/dV kernel (a launch that re-read Q, dO, K and V of every local tile) disappears.
-// STAGE: 0 = text tiles register-staged two per barrier step (round 1-3 form); 2 / 3 = LDS-DMA'd (no
-// staging VGPRs, no ds_write) two / three per step (the forward's scheme)
-template <int MINB, bool FUSE_LOCAL, bool PREFETCH_LOCAL = false, int STAGE = 0>
+// Text tiles are register-staged, two per barrier step (LDS-DMA staging two or three tiles per step, one or two
+// steps ahead, measured no different: profiles/r6_attn_staging_depth.txt).
+template <int MINB, bool FUSE_LOCAL, bool PREFETCH_LOCAL = false>
 __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ Kt,
                                                              const __bf16* __restrict__ V, const __bf16* __restrict__ dout,
                                                              const __bf16* __restrict__ out, const float* __restrict__ lse,
                                                              float* __restrict__ delta, __bf16* __restrict__ dQ, AttnGeom g,
                                                              RopeOut ro, int delta_ready) {
-  static_assert(STAGE == 0 || STAGE == 2 || STAGE == 3, "STAGE");
-  constexpr int TPS = STAGE == 3 ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * TPS * TILE];  // 32 / 48 KB
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 2 * TILE];  // 32 KB
   __shared__ float fstats[FUSE_LOCAL ? 4 : 1][2][32];                 // fused dK/dV: per wave {lse, delta}
   __shared__ float dsh[4][32];                                          // prologue: per wave row deltas
   int grp, bh;
@@ -483,35 +481,8 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dq_kernel(const __bf16* __
   };
   if (has_local && PREFETCH_LOCAL) load_loc(lo);
 
-  // ---- phase A: shared text tiles, two (three) per step ----
-  if constexpr (STAGE != 0) {
-    const int nsteps = (n_text + TPS - 1) / TPS;
-    auto dma_step = [&](int si, int buf) {
-      __bf16* S0 = smem + buf * (2 * TPS * TILE);
-#pragma unroll
-      for (int t = 0; t < TPS; ++t) {
-        const int tt = min(TPS * si + t, n_text - 1);
-        dma_tile(Kt + base + (size_t)tt * 32 * 64, S0 + t * TILE, wave, lane);
-        dma_tile(V + base + (size_t)tt * 32 * 64, S0 + (TPS + t) * TILE, wave, lane);
-      }
-    };
-    dma_step(0, 0);
-    __builtin_amdgcn_s_waitcnt(WAIT_VM0);
-    __syncthreads();
-    for (int si = 0; si < nsteps; ++si) {
-      const bool more = si + 1 < nsteps;
-      if (more) dma_step(si + 1, (si + 1) & 1);  // that buffer was released by the previous step's barrier
-      const __bf16* S0 = smem + (si & 1) * (2 * TPS * TILE);
-#pragma unroll
-      for (int t = 0; t < TPS; ++t) {
-        const int tile = TPS * si + t;
-        if (tile < my_text_end)
-          dq_tile(dq0, dq1, S0 + t * TILE, S0 + (TPS + t) * TILE, tile, qf, dof, lq, dl, g, qb, qs, lane);
-      }
-      __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the next step's tiles landed (this wave's pieces) before the barrier
-      __syncthreads();
-    }
-  } else {
+  // ---- phase A: shared text tiles, two per step ----
+  {
   const int st_row = tid >> 3, st_col = (tid & 7) * 8;
   const int st_off = lds_idx(st_row, st_col);
   const int npairs = (n_text + 1) >> 1;
@@ -1004,10 +975,10 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* out, cons
   const bool fuse_local = dqkv != nullptr && (g.pattern == 1 || g.pattern == 2);
   const int ntext = g.Tp / 32, nimg = g.Np / 32 - ntext;
   if (fuse_local)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, false, 0>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
                        (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, 0);
   else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false, false, 0>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false, false>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
                        (const __bf16*)v, (const __bf16*)dout, (const __bf16*)out, lse, delta, (__bf16*)dq, g, ro, 0);
   // text key blocks (long, every image query attends them): one block per workgroup, queries split over waves
   hipLaunchKernelGGL((attn_bwd_dkdv_text_kernel<2, 4>), dim3((ntext + 1) / 2, BH), dim3(256), 0, st, (const __bf16*)q,
