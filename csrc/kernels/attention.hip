@@ -946,7 +946,7 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_text_kernel(const __b
 // (profiles/r1_attn_occupancy.txt): the forward is latency-bound at 2 waves/SIMD (178 VGPRs) and runs
 // 225 -> 183 us at 3 (168 VGPRs); dq fits 148 VGPRs at 3; the dK/dV kernels spill at 3 and slow down
 // 1.9-2.8x, so they stay at 2. Staging per barrier step: forward 2 text tiles (3 measured slower), dQ
-// register-staged text pairs (LDS-DMA measured slower), text dK/dV 4 query tiles (-0.9 ms per bench24
+// register-staged text pairs (LDS-DMA no different, profiles/r6_attn_staging_depth.txt), text dK/dV 4 query tiles (-0.9 ms per bench24
 // B128 step vs 2); local-tile prefetch off (more spills at occupancy 3). Round-4 numbers of every
 // variant: profiles/r4ab_switches_b128.txt, profiles/INDEX.md.
 void attn_fwd(const void* q, const void* k, const void* v, void* out, float* lse, const AttnGeom& g, int BH, hipStream_t st) {
