@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-vae", action="store_true")
+    ap.add_argument("--same-caption", action="store_true",
+                    help="one caption repeated over the batch, as inference/run_inference.py generates (the decode "
+                         "attention then reads the text keys from one cache row); default: a distinct caption per row")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="batched caption prefill + N image-position decode steps (graph replays unless --no-graph), "
                          "then exit (rocprof)")
@@ -38,7 +41,8 @@ def main():
     model = DALLE(cfg).to(dev).eval()
     if not args.no_vae:
         model.vae = VQGanVAE().to(dev).eval()
-    text = torch.randint(2, cfg.num_text_tokens, (args.batch, cfg.text_seq_len), device=dev)
+    text = torch.randint(2, cfg.num_text_tokens, (1 if args.same_caption else args.batch, cfg.text_seq_len), device=dev)
+    text = text.expand(args.batch, -1).contiguous()
     use_graph = not args.no_graph
     from dalle_amd.models.generation import make_decode_engine
     eng = make_decode_engine(model, args.batch, device=dev)
@@ -99,6 +103,7 @@ def main():
                       "sampling_seconds": round(codes_s, 3), "decode_parts": parts,
                       "batch": args.batch, "model": args.model, "depth": cfg.depth, "graph": use_graph,
                       "vae": not args.no_vae, "out_shape": list(out.shape), "dtype": "bf16",
+                      "captions": "one repeated" if args.same_caption else "distinct per row",
                       "data": "random-init weights, synthetic captions"}), flush=True)
 
 

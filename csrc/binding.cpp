@@ -65,14 +65,14 @@ void decode_ln_shift(float*, const float*, const float*, void*, void*, const int
 void residual_from_partials(float*, const float*, const void*, const float*, int, int, int, hipStream_t);
 void prefill_rope(const void*, const float*, const float*, void*, void*, void*, int, int, int, int, float, hipStream_t);
 void decode_attn_part(const float*, int, const float*, const float*, float, void*, void*, void*, const int*, const DecodeGeom&, int,
-                      hipStream_t);
+                      hipStream_t, const int*);
 bool skinny_partials(SkinnyArgs, hipStream_t);
 bool skinny_partials_ln(SkinnyArgs, hipStream_t);
 bool skinny_partials_ln_ok(int, int, int);
 int skinny_partials_ks(int, int, int);
 void decode_rope(const void*, const float*, const float*, void*, void*, void*, const int*, const DecodeGeom&, int, float,
                  hipStream_t);
-void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t);
+void decode_attn(const void*, void*, void*, void*, const int*, const DecodeGeom&, int, hipStream_t, const int*);
 void vq_embed(const int64_t*, const float*, float*, int, int, int, hipStream_t);
 bool sample_step(const SampleArgs&, hipStream_t);
 bool gemm_geglu_bwd(const void*, const void*, const void*, void*, float*, int, int, int, hipStream_t, int);
@@ -1151,8 +1151,16 @@ void residual_from_partials_(Tensor x, Tensor part, c10::optional<Tensor> pbias,
 }
 
 // attention of the new token whose q / k / v are still split-K partials of the QKV projection
+// text_shared: optional int32 device flag, 1 = every batch row has the same caption (text keys read from row 0's cache)
+static const int* shared_flag(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_CUDA((*t)); CHECK_DT((*t), torch::kInt32);
+  TORCH_CHECK(t->numel() == 1, "text_shared: one int32 flag");
+  return t->data_ptr<int>();
+}
+
 void decode_attn_part_(Tensor part, Tensor cosT, Tensor sinT, double qscale, Tensor kc, Tensor vc, Tensor out, Tensor pos,
-                       int64_t T, int64_t S, int64_t H, int64_t K, int64_t pattern) {
+                       int64_t T, int64_t S, int64_t H, int64_t K, int64_t pattern, c10::optional<Tensor> text_shared) {
   CHECK_IN(part, torch::kFloat32); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
   CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(out, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
   const int BH = kc.size(0), B = BH / H;
@@ -1162,7 +1170,8 @@ void decode_attn_part_(Tensor part, Tensor cosT, Tensor sinT, double qscale, Ten
   TORCH_CHECK(cosT.size(0) >= kc.size(1) && cosT.size(1) == 64 && sinT.sizes() == cosT.sizes());
   auto g = make_decode_geom(T, S, kc.size(1), H, K, pattern);
   dalle::decode_attn_part(part.data_ptr<float>(), part.size(0), cosT.data_ptr<float>(), sinT.data_ptr<float>(), (float)qscale,
-                          kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, B, cur_stream());
+                          kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, B, cur_stream(),
+                          shared_flag(text_shared));
 }
 
 // caption prefill: qkv (B, P, 3*H*64) bf16 -> q (B*H, P, 64) rotated + pre-scaled, k / v rotated into cache rows 0..P-1
@@ -1190,14 +1199,15 @@ void decode_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Ten
 }
 
 void decode_attn_(Tensor q, Tensor kc, Tensor vc, Tensor out, Tensor pos, int64_t T, int64_t S, int64_t H, int64_t K,
-                  int64_t pattern) {
+                  int64_t pattern, c10::optional<Tensor> text_shared) {
   CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16);
   CHECK_IN(out, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
   const int BH = kc.size(0);
   TORCH_CHECK(BH % H == 0 && q.numel() == (long)BH * 64 && out.numel() == (long)BH * 64 && vc.sizes() == kc.sizes());
   TORCH_CHECK(kc.size(1) == T + S * S - 1, "decode cache must hold the full sequence");
   auto g = make_decode_geom(T, S, kc.size(1), H, K, pattern);
-  dalle::decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, BH / H, cur_stream());
+  dalle::decode_attn(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), pos.data_ptr<int>(), g, BH / H, cur_stream(),
+                     shared_flag(text_shared));
 }
 
 // Fused sampler. Returns the raw samples (B,); with text/codes/tok given it also does the decode-step
@@ -1404,7 +1414,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pbias") = py::none(), py::arg("pscale") = py::none());
   m.def("decode_rope_", &decode_rope_);
   m.def("prefill_rope_", &prefill_rope_);
-  m.def("decode_attn_", &decode_attn_);
+  m.def("decode_attn_", &decode_attn_, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("out"), py::arg("pos"), py::arg("T"),
+        py::arg("S"), py::arg("H"), py::arg("K"), py::arg("pattern"), py::arg("text_shared") = py::none());
   m.def("skinny_linear", &skinny_linear);
   m.def("skinny_partials", &skinny_partials);
   m.def("skinny_partials_ln_", &skinny_partials_ln_, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("scale"), py::arg("x"),
@@ -1412,7 +1423,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("shift"), py::arg("cnt"), py::arg("err"));
   m.def("skinny_partials_ln_ok", [](int64_t M, int64_t N, int64_t K) { return dalle::skinny_partials_ln_ok(M, N, K); });
   m.def("residual_from_partials_", &residual_from_partials_, py::arg("x"), py::arg("part"), py::arg("pbias"), py::arg("pscale"));
-  m.def("decode_attn_part_", &decode_attn_part_);
+  m.def("decode_attn_part_", &decode_attn_part_, py::arg("part"), py::arg("cosT"), py::arg("sinT"), py::arg("qscale"), py::arg("kc"),
+        py::arg("vc"), py::arg("out"), py::arg("pos"), py::arg("T"), py::arg("S"), py::arg("H"), py::arg("K"), py::arg("pattern"),
+        py::arg("text_shared") = py::none());
   m.def("skinny_force_config", &dalle::skinny_force_config);
   m.def("skinny_shape_info", &dalle::skinny_shape_info);
   m.def("skinny_geglu", &skinny_geglu);

@@ -208,6 +208,10 @@ struct QkvPartials {
   const float* sinT;
   int KS, B;
   float qscale;
+  // device flag (may be null): every batch row carries the same caption, so the text positions' K / V are
+  // identical in every row's cache and all rows read them from row 0's (one L2-resident copy per head instead of
+  // B copies streamed from HBM: the reference's generation workload repeats one query over the batch)
+  const int* text_shared;
 };
 
 __device__ __forceinline__ int decode_num_keys(const DecodeGeom& g, int pos, int& nloc, int& r0, int& c0, int& nr, int& nc) {
@@ -278,6 +282,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
   const bool one_chunk = nkeys <= DA_CHUNK;
   const __bf16* kb = kc + (size_t)bh * g.n * 64 + sub * 8;
   const __bf16* vb = vc + (size_t)bh * g.n * 64 + sub * 8;
+  // shared caption: text keys before this position come from row 0 of the same head (< 2^31 elements back:
+  // B <= 64, H <= 32, n <= 2048); the new key itself (a text query's last key) stays this row's own
+  const int tshift = (qp.text_shared != nullptr && *qp.text_shared) ? -(bh / g.H) * g.H * g.n * 64 : 0;
+  const int tlim = min(g.T, pos);
 
   // FROM_PART: q / k / v of the new token are split-K slabs of the QKV projection (threads 0..95: q | k
   // | v x dim pair). Every load the query needs before its first score -- q, or its slabs and rotary
@@ -348,7 +356,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
     int kidx[DA_U];
     issue_q();
 #pragma unroll
-    for (int u = 0; u < DA_U; ++u) kidx[u] = decode_key_at(g, min(u * 32 + wave * 8 + slot, nkeys - 1), pos, r0, c0, nc) * 64;
+    for (int u = 0; u < DA_U; ++u) {
+      const int i = min(u * 32 + wave * 8 + slot, nkeys - 1);
+      kidx[u] = decode_key_at(g, i, pos, r0, c0, nc) * 64 + (i < tlim ? tshift : 0);
+    }
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) kf[u] = *reinterpret_cast<const s16x8*>(kb + kidx[u]);
     asm volatile("" ::: "memory");  // every K row ahead of every V row: the scores start while V streams
@@ -400,7 +411,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
 #pragma unroll
       for (int u = 0; u < DA_U; ++u) {
         const int i = c + u * 32 + wave * 8 + slot;
-        kf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(kb + (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64) : s16x8{};
+        kf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(kb + ((long)decode_key_at(g, i, pos, r0, c0, nc) * 64 + (i < tlim ? tshift : 0)))
+                          : s16x8{};
       }
 #pragma unroll
       for (int u = 0; u < DA_U; ++u) {
@@ -422,7 +434,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
 #pragma unroll
       for (int u = 0; u < DA_U; ++u) {
         const int i = c + u * 32 + wave * 8 + slot;
-        vf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(vb + (size_t)decode_key_at(g, i, pos, r0, c0, nc) * 64) : s16x8{};
+        vf[u] = i < nkeys ? *reinterpret_cast<const s16x8*>(vb + ((long)decode_key_at(g, i, pos, r0, c0, nc) * 64 + (i < tlim ? tshift : 0)))
+                          : s16x8{};
       }
 #pragma unroll
       for (int u = 0; u < DA_U; ++u) {
@@ -497,15 +510,18 @@ void decode_rope(const void* qkv, const float* cosT, const float* sinT, void* q,
                      (__bf16*)q, (__bf16*)kc, (__bf16*)vc, pos, g, B, qscale);
 }
 
-void decode_attn(const void* q, void* kc, void* vc, void* out, const int* pos, const DecodeGeom& g, int B, hipStream_t st) {
+void decode_attn(const void* q, void* kc, void* vc, void* out, const int* pos, const DecodeGeom& g, int B, hipStream_t st,
+                 const int* text_shared) {
+  QkvPartials qp{};
+  qp.text_shared = text_shared;
   hipLaunchKernelGGL(decode_attn_kernel<false>, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)q, (__bf16*)kc, (__bf16*)vc,
-                     (__bf16*)out, pos, g, QkvPartials{});
+                     (__bf16*)out, pos, g, qp);
 }
 
 void decode_attn_part(const float* part, int KS, const float* cosT, const float* sinT, float qscale, void* kc, void* vc, void* out,
-                      const int* pos, const DecodeGeom& g, int B, hipStream_t st) {
+                      const int* pos, const DecodeGeom& g, int B, hipStream_t st, const int* text_shared) {
   hipLaunchKernelGGL(decode_attn_kernel<true>, dim3(B * g.H), dim3(256), 0, st, (const __bf16*)nullptr, (__bf16*)kc, (__bf16*)vc,
-                     (__bf16*)out, pos, g, QkvPartials{part, cosT, sinT, KS, B, qscale});
+                     (__bf16*)out, pos, g, QkvPartials{part, cosT, sinT, KS, B, qscale, text_shared});
 }
 
 void vq_embed(const int64_t* idx, const float* codebook, float* z, int HW, int C, int B, hipStream_t st) {

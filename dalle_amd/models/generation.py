@@ -81,6 +81,10 @@ class DecodeEngine:
         self.hist = [[torch.zeros(B, self.n, self.d, dtype=self.cdt, device=dev) for _ in range(2)] for _ in range(L)]
         self.cos, self.sin = rotary_tables(self.T, self.S, self.Dh, device=dev)
         self.pos = torch.zeros((), dtype=torch.int32, device=dev)
+        # 1 while every row carries the same caption (set per generate call, on device: a captured graph serves both
+        # cases): the decode attention then reads the text positions' K / V from row 0's cache for all rows
+        self.text_shared = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.share_text = True
         self.tok = torch.zeros(B, dtype=torch.long, device=dev)
         self.hbuf = torch.zeros(B, self.d, dtype=self.cdt, device=dev)
         self.qbuf = torch.zeros(B, self.H, self.Dh, dtype=self.cdt, device=dev)
@@ -205,12 +209,12 @@ class DecodeEngine:
         if self.qkv_partials:
             part = C().skinny_partials(h, self._wt(attn.to_qkv.weight))
             C().decode_attn_part_(part, self.cos, self.sin, self.Dh ** -0.5, self.kc[li], self.vc[li], self.obuf, self.pos,
-                                  self.T, self.S, self.H, self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+                                  self.T, self.S, self.H, self.geom.kernel_size, PATTERN_IDS[attn.attn_type], self.text_shared)
         else:
             C().skinny_qkv_rope_(h, self._wt(attn.to_qkv.weight), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li],
                                  self.pos, self.H, self.Dh ** -0.5, self.sk_cnt)
             C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
-                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type], self.text_shared)
         if self.ln_tail:
             self._pending = ("gemm", x_res, self.obuf, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias),
                              self._scale(ls))
@@ -257,7 +261,7 @@ class DecodeEngine:
             C().decode_rope_(qkv.contiguous(), self.cos, self.sin, self.qbuf, self.kc[li], self.vc[li], self.pos, self.H,
                              self.Dh ** -0.5)
             C().decode_attn_(self.qbuf, self.kc[li], self.vc[li], self.obuf, self.pos, self.T, self.S, self.H,
-                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type])
+                             self.geom.kernel_size, PATTERN_IDS[attn.attn_type], self.text_shared)
             o = self.obuf
         else:
             o = self._attn_torch(li, attn, qkv)
@@ -359,6 +363,10 @@ class DecodeEngine:
             self.text_bos = torch.zeros_like(text_bos)
         self.text_bos.copy_(text_bos)
         self.tok.copy_(text_bos[:, 0])
+        if self.share_text:
+            self.text_shared.copy_((text_bos == text_bos[:1]).all().view(1))
+        else:
+            self.text_shared.zero_()
 
     @torch.no_grad()
     def prefill(self, text_bos: torch.Tensor):

@@ -169,3 +169,28 @@ def test_decode_ln_tail_reference_width(cuda, B):
     rel = ((out[0] - out[1]).norm() / out[0].norm()).item()
     assert rel < 2e-3, rel
     assert (out[0].argmax(-1) == out[1].argmax(-1)).float().mean().item() > 0.98
+
+
+@pytest.mark.parametrize("mode", ["2", "0"])
+def test_shared_caption_text_keys_from_row0_are_exact(cuda, mode):
+    """One caption repeated over the batch (the reference's generation workload): the decode attention reads the
+    text positions' K / V from row 0's cache for every row. Those rows' caches hold bitwise the same values, so the
+    logits are bitwise those of the per-row reads; with distinct captions the flag stays off."""
+    torch.manual_seed(0)
+    cfg = _cfg(False)
+    m = DALLE(cfg).eval().to(cuda)
+    B = 4
+    one = torch.randint(2, cfg.num_text_tokens, (1, cfg.text_seq_len), device=cuda)
+    tb = m.prepare_text(one.expand(B, -1).contiguous())
+    img = torch.randint(0, cfg.num_image_tokens, (B, cfg.image_seq_len), device=cuda)
+    out = []
+    for share in (False, True):
+        eng = DecodeEngine(m, B, device=cuda, partials=int(mode))
+        eng.share_text = share
+        out.append(eng.teacher_forced_logits(tb, img))
+        assert int(eng.text_shared.item()) == int(share)
+    assert torch.equal(out[0], out[1])
+    eng = DecodeEngine(m, B, device=cuda)
+    distinct = m.prepare_text(torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len), device=cuda))
+    eng.prefill(distinct)
+    assert int(eng.text_shared.item()) == 0
