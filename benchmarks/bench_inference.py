@@ -104,6 +104,7 @@ def main():
                       "batch": args.batch, "model": args.model, "depth": cfg.depth, "graph": use_graph,
                       "vae": not args.no_vae, "out_shape": list(out.shape), "dtype": "bf16",
                       "captions": "one repeated" if args.same_caption else "distinct per row",
+                      "text_shared": [int(e.text_shared.item()) for e in getattr(eng, "parts", [eng])],
                       "data": "random-init weights, synthetic captions"}), flush=True)
 
 

@@ -244,7 +244,9 @@ __device__ __forceinline__ int decode_key_at(const DecodeGeom& g, int i, int pos
 // in one chunk of 32 * DA_U) every K AND V load of the lane is issued before the first score is
 // formed -- V does not depend on the softmax -- so the whole (b, h) is one memory round trip. Longer
 // key sets (full attention late in the sequence) take a chunked two-pass path with scores in LDS.
-constexpr int DA_U = 12;                 // rounds per chunk: 384 keys
+// 10 rounds per chunk = 320 keys: the reference geometry's 257 text + <= 32 axial (<= 25 conv) keys in one chunk at
+// 128 VGPRs, so four (b, h) workgroups fit a CU (12 rounds: 146 VGPRs, three)
+constexpr int DA_U = 10;
 constexpr int DA_CHUNK = 32 * DA_U;
 constexpr int DA_MAXN = 2048;
 
@@ -254,6 +256,17 @@ __device__ __forceinline__ float dot8(const float* q, const s16x8& k) {
   float a = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) a += q[e] * f[e];
+  return a;
+}
+
+// q . k over a lane's 8 dims as four packed-bf16 dot products (v_dot2c_f32_bf16: no unpacking; q is bf16-exact)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+__device__ __forceinline__ float dot8_bf(const uint32_t (&q)[4], const s16x8& k) {
+  const uint32_t* kw = reinterpret_cast<const uint32_t*>(&k);
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, q[j]), __builtin_bit_cast(bf16x2, kw[j]), a, false);
   return a;
 }
 
@@ -312,8 +325,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
     }
     asm volatile("" ::: "memory");  // keeps these loads ahead of the cache stream (hipcc sinks them otherwise)
   };
-  float qd[8];
-  // q / k / v of the new token: q to every lane (qd), k / v to LDS and the caches
+  float qd[8];      // q (x log2 e) as floats: the chunked path
+  uint32_t qb2[4];  // q as bf16 pairs: the single-chunk path's packed dot products
+  // q / k / v of the new token: q to every lane (qd, qb2), k / v to LDS and the caches
   auto prologue = [&]() {
     if (FROM_PART) {
       if (tid < 96) {
@@ -338,8 +352,14 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
       __threadfence_block();  // the chunked path reads the new row back from the cache
       __syncthreads();
 #pragma unroll
-      for (int e = 0; e < 8; ++e) qd[e] = qsh[sub * 8 + e] * LOG2E;
+      for (int e = 0; e < 8; ++e) qd[e] = qsh[sub * 8 + e];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qb2[j] = (uint32_t)f2bf(qd[2 * j]) | ((uint32_t)f2bf(qd[2 * j + 1]) << 16);  // exact: bf16 values
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
     } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qb2[j] = reinterpret_cast<const uint32_t*>(&qraw)[j];
       unpack8(qraw, qd);
 #pragma unroll
       for (int e = 0; e < 8; ++e) qd[e] *= LOG2E;
@@ -382,7 +402,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
 #pragma unroll
     for (int u = 0; u < DA_U; ++u) {
       const int i = u * 32 + wave * 8 + slot;
-      sv[u] = i < nkeys ? slot_sum(dot8(qd, kf[u])) : NEG_BIG;
+      sv[u] = i < nkeys ? slot_sum(dot8_bf(qb2, kf[u])) * LOG2E : NEG_BIG;
       mloc = fmaxf(mloc, sv[u]);
     }
     mloc = wave_max(mloc);
@@ -390,14 +410,23 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const __bf16* __restri
     __syncthreads();
     m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
     float ssum = 0.f;
+    // P.V two rounds at a time: this lane's keys of rounds u and u + 1 (same 8 dims) as one packed-bf16 dot per
+    // dim -- P rounded to bf16 (as the training kernels feed it to the MFMAs), summed for the denominator as rounded
+    static_assert(DA_U % 2 == 0, "DA_U");
 #pragma unroll
-    for (int u = 0; u < DA_U; ++u) {
-      const float p = exp2f(sv[u] - m);  // 0 for invalid slots
-      ssum += p;
-      float f[8];
-      unpack8(vf[u], f);
+    for (int u = 0; u < DA_U; u += 2) {
+      const bf16_raw p0 = f2bf(exp2f(sv[u] - m)), p1 = f2bf(exp2f(sv[u + 1] - m));  // 0 for invalid slots
+      ssum += bf2f(p0) + bf2f(p1);
+      const bf16x2 pp = __builtin_bit_cast(bf16x2, (uint32_t)p0 | ((uint32_t)p1 << 16));
+      const uint32_t* va = reinterpret_cast<const uint32_t*>(&vf[u]);
+      const uint32_t* vb2 = reinterpret_cast<const uint32_t*>(&vf[u + 1]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * f[e];
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = __builtin_amdgcn_perm(va[j], vb2[j], 0x01000504u);  // (v_u[2j], v_u+1[2j])
+        const uint32_t hi = __builtin_amdgcn_perm(va[j], vb2[j], 0x03020706u);  // (v_u[2j+1], v_u+1[2j+1])
+        acc[2 * j] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2, lo), acc[2 * j], false);
+        acc[2 * j + 1] = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2, hi), acc[2 * j + 1], false);
+      }
     }
     ssum = wave_sum(ssum) * 0.125f;  // each key counted once per lane of its row
     if (lane == 0) red[1][wave] = ssum;

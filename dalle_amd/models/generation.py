@@ -574,7 +574,8 @@ class SplitDecodeEngine:
             p.prefill_parallel(text_bos[i * b:(i + 1) * b])
 
     def _capture(self):
-        if self.graph is not None and self._graph_cfg == (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p):
+        cfg = (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p)
+        if self.graph is not None and self._graph_cfg == cfg:
             return
         main = torch.cuda.current_stream()
         streams = [torch.cuda.Stream() for _ in self.parts[1:]]
@@ -598,7 +599,7 @@ class SplitDecodeEngine:
                 cap.wait_stream(s)
         self.graph = g
         self._streams = streams
-        self._graph_cfg = (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p)
+        self._graph_cfg = cfg
 
     @torch.no_grad()
     def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
