@@ -95,6 +95,7 @@ class DecodeEngine:
         self.fused_sampler = use_hip and fused_sampler
         self.seed = torch.zeros((), dtype=torch.int64, device=dev)
         self.graph = None
+        self._pf_graphs = {}  # captured caption prefills, by (rows, input buffer)
         self._static_logits = None
         self._w = {}
         # decode-step projections through the skinny MFMA GEMM (csrc/kernels/skinny.hip) with the
@@ -397,15 +398,16 @@ class DecodeEngine:
     def _pf_attn(self, li, ls, x):
         attn = ls.fn.fn.fn
         B, P, H, Dh = x.shape[0], x.shape[1], self.H, self.Dh
-        h = self._pf_ln_shift(ls, self.hist[li][0], x)
+        h = self._pf_ln_shift(ls, self.hist[li][0][:B], x)
+        kc, vc = self.kc[li][: B * H], self.vc[li][: B * H]  # the first B rows' caches (all of them, or row 0)
         if self.use_hip:
             # one kernel rotates q / k / v and writes k / v into the caches (q pre-scaled, bf16 as in the
             # decode steps); scores in fp32, causal over the caption
             from ..ops.hip_ops import C
             qkv = F.linear(h, self._wt(attn.to_qkv.weight)).contiguous()
             q = torch.empty(B * H, P, Dh, dtype=self.cdt, device=x.device)
-            C().prefill_rope_(qkv, self.cos, self.sin, q, self.kc[li], self.vc[li], H, Dh ** -0.5)
-            k, v = self.kc[li][:, :P], self.vc[li][:, :P]
+            C().prefill_rope_(qkv, self.cos, self.sin, q, kc, vc, H, Dh ** -0.5)
+            k, v = kc[:, :P], vc[:, :P]
             sc = torch.bmm(q, k.transpose(1, 2), out_dtype=torch.float32)
             mask = static_mask(self.geom, attn.attn_type, self.n, device=x.device)[:P, :P]
             sc.masked_fill_(~mask, float("-inf"))
@@ -416,8 +418,8 @@ class DecodeEngine:
         qkv = F.linear(h, self._wt(attn.to_qkv.weight)).view(B, P, 3, H, Dh).permute(2, 0, 3, 1, 4).float()
         c, sn = self.cos[:P], self.sin[:P]
         q, k, v = (apply_rotary(t, c, sn) for t in qkv)
-        self.kc[li].view(B, H, self.n, Dh)[:, :, :P] = k.to(self.cdt)
-        self.vc[li].view(B, H, self.n, Dh)[:, :, :P] = v.to(self.cdt)
+        kc.view(B, H, self.n, Dh)[:, :, :P] = k.to(self.cdt)
+        vc.view(B, H, self.n, Dh)[:, :, :P] = v.to(self.cdt)
         # the cached (rounded) keys / values, as the decode steps will read them
         k, v = k.to(self.cdt).float(), v.to(self.cdt).float()
         sc = (q * Dh ** -0.5) @ k.transpose(-1, -2)
@@ -429,7 +431,7 @@ class DecodeEngine:
 
     def _pf_ff(self, li, ls, x):
         ff = ls.fn.fn.fn
-        h = self._pf_ln_shift(ls, self.hist[li][1], x)
+        h = self._pf_ln_shift(ls, self.hist[li][1][: x.shape[0]], x)
         a = F.linear(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias))
         if self.use_hip:
             from ..ops.hip_ops import C
@@ -444,23 +446,49 @@ class DecodeEngine:
         """Positions 0..T-2 (BOS + caption) as one batched pass per layer instead of T-1 decode steps:
         fills the KV caches and LN histories exactly where the steps would, then leaves the engine at
         position T-1 (the first sampling step) -- at batch 64 on the reference model this replaces
-        ~0.9 s of sequential steps with a few ms."""
+        ~0.9 s of sequential steps with a few ms.
+
+        One caption repeated over the batch (the decode attention then reads the text keys / values from row
+        0's cache, ``text_shared``): the pass runs for row 0 alone, and the other rows get only what the decode
+        steps read of their own: the LN history at position T-2 (the shift of the first step, at T-1)."""
         self._start(text_bos)
         P = self.T - 1
+        one = self.use_hip and self.share_text and self.B > 1 and bool(self.text_shared.item())
+        rows = 1 if one else self.B
         if P > 0:
-            W = self.model.to_logits[1].weight.detach()
-            x = F.embedding(text_bos[:, :P], W).float()
-            if self.cfg.reversible:
-                x1, x2 = x, x.clone()
-                for li, (f, g) in enumerate(self.pairs):
-                    x1 = x1 + self._pf_attn(li, f, x2)
-                    x2 = x2 + self._pf_ff(li, g, x1)
+            if self.use_hip:
+                # the pass is ~25 launches per layer: captured once per (rows, input buffer) and replayed
+                key = (rows, self.text_bos.data_ptr())
+                graph = self._pf_graphs.get(key)
+                if graph is None:
+                    self._pf_body(rows, P)  # the result, and the libraries' warm-up for the capture
+                    graph = torch.cuda.CUDAGraph()
+                    with _CAPTURE_LOCK, torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                        self._pf_body(rows, P)
+                    self._pf_graphs[key] = graph
+                else:
+                    graph.replay()
             else:
-                for li, (f, g) in enumerate(self.pairs):
-                    x = x + self._pf_attn(li, f, x)
-                    x = x + self._pf_ff(li, g, x)
+                self._pf_body(rows, P)
             self.pos.fill_(P)
         self.tok.copy_(text_bos[:, P])
+
+    def _pf_body(self, rows: int, P: int):
+        W = self.model.to_logits[1].weight.detach()
+        x = F.embedding(self.text_bos[:rows, :P], W).float()
+        if self.cfg.reversible:
+            x1, x2 = x, x.clone()
+            for li, (f, g) in enumerate(self.pairs):
+                x1 = x1 + self._pf_attn(li, f, x2)
+                x2 = x2 + self._pf_ff(li, g, x1)
+        else:
+            for li, (f, g) in enumerate(self.pairs):
+                x = x + self._pf_attn(li, f, x)
+                x = x + self._pf_ff(li, g, x)
+        if rows < self.B:  # the other rows' own reads: the LN history the first decode step shifts in
+            for hs in self.hist:
+                for hb in hs:
+                    hb[rows:, P - 1].copy_(hb[0, P - 1].expand(self.B - rows, -1))
 
     @torch.no_grad()
     def generate(self, text_bos: torch.Tensor, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,

@@ -86,11 +86,21 @@ def _static_mask_cpu(geom: AttnGeometry, attn_type: str, n: int) -> torch.Tensor
     return allowed(geom, attn_type, i, j)
 
 
+@lru_cache(maxsize=64)
+def _static_mask_dev(geom: AttnGeometry, attn_type: str, n: int, device: str) -> torch.Tensor:
+    return _static_mask_cpu(geom, attn_type, n).to(device)
+
+
 def static_mask(geom: AttnGeometry, attn_type: str, n: int | None = None, device=None) -> torch.Tensor:
-    """Dense (n, n) boolean mask (True = attend) -- the inference / golden-test form (D6)."""
+    """Dense (n, n) boolean mask (True = attend) -- the inference / golden-test form (D6). Cached per device (read-only:
+    the caption prefill asks for it in every layer, and a 1.6 MB pageable host copy each time cost most of its time)."""
     n = geom.seq_len if n is None else n
-    m = _static_mask_cpu(geom, attn_type, n)
-    return m.to(device) if device is not None else m
+    if device is None:
+        return _static_mask_cpu(geom, attn_type, n)
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return _static_mask_dev(geom, attn_type, n, str(dev))
 
 
 def storage_index(geom: AttnGeometry, attn_type: str) -> torch.Tensor:

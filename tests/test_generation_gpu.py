@@ -194,3 +194,25 @@ def test_shared_caption_text_keys_from_row0_are_exact(cuda, mode):
     distinct = m.prepare_text(torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len), device=cuda))
     eng.prefill(distinct)
     assert int(eng.text_shared.item()) == 0
+
+
+@pytest.mark.parametrize("reversible", [False, True])
+def test_repeated_caption_prefill_runs_row0_only(cuda, reversible):
+    """One caption over the batch: the batched caption prefill runs for row 0 alone (the decode attention reads the
+    text K / V from row 0's cache; the other rows receive the LN history the first step shifts in). Greedy
+    generation matches the full-batch prefill with per-row text reads."""
+    torch.manual_seed(2)
+    cfg = _cfg(reversible)
+    m = DALLE(cfg).eval().to(cuda)
+    B = 4
+    one = torch.randint(2, cfg.num_text_tokens, (1, cfg.text_seq_len), device=cuda)
+    tb = m.prepare_text(one.expand(B, -1).contiguous())
+    full = DecodeEngine(m, B, device=cuda)
+    full.share_text = False
+    ref = full.generate(tb, top_k=1, seed=3, parallel_prefill=True)
+    eng = DecodeEngine(m, B, device=cuda)
+    got = eng.generate(tb, top_k=1, seed=3, parallel_prefill=True)
+    assert int(eng.text_shared.item()) == 1
+    assert (got == ref).float().mean().item() > 0.95
+    # rows 1.. never had their own text caches filled: the reads really come from row 0
+    assert eng.kc[0].view(B, cfg.heads, -1, cfg.dim_head)[1:, :, : eng.T - 1].abs().sum().item() == 0.0
