@@ -551,15 +551,33 @@ class DecodeEngine:
         return torch.stack(outs, dim=1)
 
 
-class SplitDecodeEngine:
-    """The batch split into ``parts`` independent :class:`DecodeEngine` s whose steps run on separate
-    HIP streams inside ONE captured graph. At batch 64 a decode step is a chain of short kernels
-    whose time is mostly fixed latency (a skinny GEMM takes 8-10 us whether it streams 2 or 16 MB of
-    weights), so two half-batch chains interleaved on the GPU overlap one chain's latency with the
-    other's work. The parts share the bf16 weight copies; each has its own KV caches, LN histories,
-    device position and sampler seed (``seed + part``), so the parts never touch the same buffer."""
+class _PartGraphs:
+    """One image-position step of every part: each part's own captured graph replayed on the part's stream
+    (the ``graph`` of a :class:`SplitDecodeEngine` in per-part mode)."""
 
-    def __init__(self, model, batch_size: int, device=None, parts: int = 2):
+    def __init__(self, eng):
+        self.eng = eng
+
+    def replay(self):
+        self.eng.replay_steps(1)
+
+
+class SplitDecodeEngine:
+    """The batch split into ``parts`` independent :class:`DecodeEngine` s whose steps run concurrently
+    on separate HIP streams. At batch 64 a decode step is a chain of short kernels whose time is mostly
+    fixed latency (a skinny GEMM takes 8-10 us whether it streams 2 or 16 MB of weights), so two
+    half-batch chains interleaved on the GPU overlap one chain's latency with the other's work. The
+    parts share the bf16 weight copies; each has its own KV caches, LN histories, device position and
+    sampler seed (``seed + part``), so the parts never touch the same buffer.
+
+    ``graphs`` (``DALLE_AMD_DECODE_GRAPHS``): "per-part" (default) captures each part's step as its own
+    LINEAR graph, replayed on the part's stream with no per-step join -- the HIP runtime launches a linear
+    graph from pre-built packets, 0.17 ms of host time per step for both parts. "joint": one graph with the
+    parts as parallel branches joined at the end of every step -- the runtime launches a multi-branch graph
+    node by node, ~2.5 ms of host time per ~3 ms step, so the host barely stays ahead and its jitter reaches
+    the GPU (profiles/r6_decode_replay_host.txt: 3.00-3.02 vs 3.05-3.11 ms per step)."""
+
+    def __init__(self, model, batch_size: int, device=None, parts: int = 2, graphs: Optional[str] = None):
         if batch_size % parts:
             raise ValueError(f"batch {batch_size} is not divisible into {parts} parts")
         self.model, self.B, self.nparts = model, batch_size, parts
@@ -569,8 +587,15 @@ class SplitDecodeEngine:
             p._refresh_weights = False
         self.device = self.parts[0].device
         self.use_hip = self.parts[0].use_hip
+        if graphs is None:
+            import os
+            graphs = os.environ.get("DALLE_AMD_DECODE_GRAPHS", "per-part")
+        if graphs not in ("per-part", "joint"):
+            raise ValueError(f"DALLE_AMD_DECODE_GRAPHS={graphs!r}: expected per-part or joint")
+        self.graph_mode = graphs
         self.graph = None
         self._graph_cfg = None
+        self._part_streams = None
 
     @property
     def codes(self) -> torch.Tensor:
@@ -604,6 +629,14 @@ class SplitDecodeEngine:
     def _capture(self):
         cfg = (self.parts[0].temperature, self.parts[0].top_k, self.parts[0].top_p)
         if self.graph is not None and self._graph_cfg == cfg:
+            return
+        if self.graph_mode == "per-part":
+            for p in self.parts:
+                p._capture()  # a linear graph of the part's own step (its warm-up steps are reset by the prefill)
+            if self._part_streams is None:
+                self._part_streams = [torch.cuda.Stream() for _ in self.parts]
+            self.graph = _PartGraphs(self)
+            self._graph_cfg = cfg
             return
         main = torch.cuda.current_stream()
         streams = [torch.cuda.Stream() for _ in self.parts[1:]]
@@ -653,11 +686,22 @@ class SplitDecodeEngine:
         return self.codes.clone()
 
     def replay_steps(self, k: int):
-        """``k`` decode steps through the captured graph (one graph, the parts as parallel branches joined at
-        the end of every step: one graph per part on its own stream measured 10.8 vs 16.6 images/s,
-        profiles/r3_decode_graph_launch.txt)."""
+        """``k`` decode steps through the captured graph(s). Per-part: the part streams fork from the current
+        stream, each replays its part's graph ``k`` times with no join in between, and the current stream
+        joins them at the end (the codes are read there)."""
+        if self.graph_mode == "joint":
+            for _ in range(k):
+                self.graph.replay()
+            return
+        main = torch.cuda.current_stream()
+        for st in self._part_streams:
+            st.wait_stream(main)
         for _ in range(k):
-            self.graph.replay()
+            for p, st in zip(self.parts, self._part_streams):
+                with torch.cuda.stream(st):
+                    p.graph.replay()
+        for st in self._part_streams:
+            main.wait_stream(st)
 
 
 def decode_parts(batch_size: int, device, parts: Optional[int] = None) -> int:

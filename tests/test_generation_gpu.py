@@ -51,10 +51,11 @@ def test_graph_replay_matches_eager(cuda):
     assert torch.equal(eager, graph)
 
 
-@pytest.mark.parametrize("use_graph", [False, True])
-def test_split_decode_engine_matches_single(cuda, use_graph):
-    """Two half-batch chains on separate streams (one captured graph) == one full-batch engine under
-    greedy sampling (top-k 1: the sampler's noise, which differs per part, cannot change the pick)."""
+@pytest.mark.parametrize("use_graph,graphs", [(False, "per-part"), (True, "per-part"), (True, "joint")])
+def test_split_decode_engine_matches_single(cuda, use_graph, graphs):
+    """Two half-batch chains on separate streams (per-part graphs, or one graph with the chains as branches)
+    == one full-batch engine under greedy sampling (top-k 1: the sampler's noise, which differs per part,
+    cannot change the pick)."""
     from dalle_amd.models.generation import SplitDecodeEngine
 
     torch.manual_seed(0)
@@ -64,7 +65,7 @@ def test_split_decode_engine_matches_single(cuda, use_graph):
     text = torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len), device=cuda)
     tb = m.prepare_text(text)
     single = DecodeEngine(m, B, device=cuda).generate(tb, top_k=1, use_graph=use_graph, seed=5)
-    split = SplitDecodeEngine(m, B, device=cuda, parts=2)
+    split = SplitDecodeEngine(m, B, device=cuda, parts=2, graphs=graphs)
     assert len(split.parts) == 2 and split.parts[1]._w is split.parts[0]._w
     got = split.generate(tb, top_k=1, use_graph=use_graph, seed=5)
     assert got.shape == single.shape
@@ -72,6 +73,30 @@ def test_split_decode_engine_matches_single(cuda, use_graph):
     # a second call reuses the captured graph and the shared weights
     again = split.generate(tb, top_k=1, use_graph=use_graph, seed=7)
     assert torch.equal(again, got)
+
+
+def test_split_decode_per_part_graphs_equal_joint_graph(cuda):
+    """The per-part graphs (each part's step a linear graph on its own stream) run the same kernels on the same
+    buffers as the joint two-branch graph: bitwise the same codes under top-k sampling with a fixed seed, and
+    the same as the eager steps."""
+    from dalle_amd.models.generation import SplitDecodeEngine
+
+    torch.manual_seed(0)
+    cfg = _cfg(True)
+    m = DALLE(cfg).eval().to(cuda)
+    B = 8
+    text = torch.randint(2, cfg.num_text_tokens, (B, cfg.text_seq_len), device=cuda)
+    tb = m.prepare_text(text)
+    out = {}
+    for graphs in ("per-part", "joint"):
+        eng = SplitDecodeEngine(m, B, device=cuda, parts=2, graphs=graphs)
+        assert eng.graph_mode == graphs
+        out[graphs] = eng.generate(tb, top_k=16, use_graph=True, seed=11)
+        out[graphs + "-eager"] = eng.generate(tb, top_k=16, use_graph=False, seed=11)
+    assert torch.equal(out["per-part"], out["joint"])
+    assert torch.equal(out["per-part"], out["per-part-eager"])
+    with pytest.raises(ValueError):
+        SplitDecodeEngine(m, B, device=cuda, parts=2, graphs="bogus")
 
 
 def test_parallel_prefill_generation_matches_sequential(cuda):
