@@ -12,6 +12,7 @@ The CPU path runs the same step with the reference ops (tests compare it against
 from __future__ import annotations
 
 import math
+import os
 import threading
 from typing import List, Optional
 
@@ -115,7 +116,6 @@ class DecodeEngine:
         # that it runs as one launch with the LayerNorm that reads the stream (skinny_partials_ln_)
         self._pending = None
         if ln_tail is None:
-            import os
             ln_tail = os.environ.get("DALLE_AMD_DECODE_LN_TAIL", "0") == "1"
         self.ln_tail = False
         if self.partials and ln_tail:
@@ -588,7 +588,6 @@ class SplitDecodeEngine:
         self.device = self.parts[0].device
         self.use_hip = self.parts[0].use_hip
         if graphs is None:
-            import os
             graphs = os.environ.get("DALLE_AMD_DECODE_GRAPHS", "per-part")
         if graphs not in ("per-part", "joint"):
             raise ValueError(f"DALLE_AMD_DECODE_GRAPHS={graphs!r}: expected per-part or joint")
@@ -705,12 +704,15 @@ class SplitDecodeEngine:
 
 
 def decode_parts(batch_size: int, device, parts: Optional[int] = None) -> int:
-    """How many concurrent batch-slice chains a decode engine uses: ``parts``, default 2 for batches of 32
-    and more (1 below). Reference model, batch 64, same box
+    """How many concurrent batch-slice chains a decode engine uses: ``parts`` (else ``DALLE_AMD_DECODE_PARTS``),
+    default 2 for batches of 32 and more (1 below); 4 chains measured 17.7 vs 20.1 images/s with per-part graphs
+    (profiles/r6_decode_replay_host.txt). Reference model, batch 64, same box
     (profiles/r2_decode_split_parts.txt): 2 parts 3.53 ms per image-position step and 17.0 images/s vs
     3.74 ms / 16.0 for one chain; 4 parts 4.0-6.1 ms. With the decode kernels at a few us each, two
     half-batch chains overlap one chain's latency-bound kernels with the other's (it measured +1 % when
     the skinny GEMMs still carried their split-K hand-off)."""
+    if parts is None and os.environ.get("DALLE_AMD_DECODE_PARTS"):
+        parts = int(os.environ["DALLE_AMD_DECODE_PARTS"])
     n = max(1, int(parts if parts is not None else (2 if batch_size >= 32 else 1)))
     return n if batch_size % n == 0 else 1
 
