@@ -69,6 +69,16 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     res["event_ms_per_step"] = round(ev0.elapsed_time(ev1) / 64, 3)
+    # the step time along the image: 16 chunks of 64 positions after one prefill
+    chunks = []
+    eng.prefill_parallel(tb)
+    torch.cuda.synchronize()
+    for _ in range(cfg.image_seq_len // 64):
+        t0 = time.perf_counter()
+        replay(64)
+        torch.cuda.synchronize()
+        chunks.append(round((time.perf_counter() - t0) / 64 * 1e3, 3))
+    res["ms_per_step_by_64_positions"] = chunks
     env = {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_", "PROBE_", "DALLE_AMD_"))}
     print(json.dumps({"probe": "decode graph replay, host submit vs GPU", "batch": B, "model": cfg.depth, "env": env,
                       "parts": getattr(eng, "nparts", 1),
