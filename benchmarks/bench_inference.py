@@ -84,21 +84,24 @@ def main():
     torch.cuda.synchronize()
     codes_s = time.perf_counter() - t2
     eng = model._decode_engine
-    # decode-only timing: 64 image positions right after the batched caption prefill (every step
-    # reads the 256 text keys of each layer's cache plus its local image keys)
+    # decode-only timing: 256 image positions right after the batched caption prefill (every step
+    # reads the 256 text keys of each layer's cache plus its local image keys). 256, not 64: the two
+    # chains' per-part graphs run free and the window ends on the later one (~19 ms per window,
+    # profiles/r6_decode_replay_host.txt), which a 64-step window would spread as +0.3 ms per step
+    NDEC = 256
     prefill(tb)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if use_graph and hasattr(eng, "replay_steps"):
-        eng.replay_steps(64)
-    for _ in range(0 if (use_graph and hasattr(eng, "replay_steps")) else 64):
+        eng.replay_steps(NDEC)
+    for _ in range(0 if (use_graph and hasattr(eng, "replay_steps")) else NDEC):
         eng.graph.replay() if use_graph else eng._step()
     torch.cuda.synchronize()
-    per_tok = (time.perf_counter() - t1) / 64
+    per_tok = (time.perf_counter() - t1) / NDEC
     print(json.dumps({"metric": "text->image generation throughput (batch 64, top-k, hipGraph decode)",
                       "value": round(args.batch / el, 3), "unit": "images/s", "n_gpus": 1,
                       "seconds_per_batch": round(el, 3), "ms_per_decode_step": round(per_tok * 1e3, 3),
-                      "decode_step_positions": f"image positions {cfg.text_len - 1}..{cfg.text_len + 62}",
+                      "decode_step_positions": f"image positions {cfg.text_len - 1}..{cfg.text_len + NDEC - 2}",
                       "ms_per_image_token": round(codes_s / cfg.image_seq_len * 1e3, 3),
                       "sampling_seconds": round(codes_s, 3), "decode_parts": parts,
                       "batch": args.batch, "model": args.model, "depth": cfg.depth, "graph": use_graph,
