@@ -13,6 +13,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--chains", type=int, default=1,
+                    help="sampler kernels per image-position step (one per batch-slice chain that runs its own graph)")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -20,10 +22,11 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     ends = [i for i, (_, _, n) in enumerate(rows) if "sample_kernel" in n]
-    if len(ends) < a.steps + 1:
+    n_ends = a.steps * a.chains
+    if len(ends) < n_ends + 1:
         print(f"only {len(ends)} sampler kernels")
         return
-    i0, i1 = ends[-a.steps - 1] + 1, ends[-1]
+    i0, i1 = ends[-n_ends - 1] + 1, ends[-1]
     win = rows[i0:i1 + 1]
     t0, t1 = win[0][0], max(e for _, e, _ in win)
     wall = (t1 - t0) / 1e3 / a.steps
