@@ -64,6 +64,9 @@ void decode_ln_shift(float*, const float*, const float*, void*, void*, const int
                      const float*, const void*, const float*, int);
 void residual_from_partials(float*, const float*, const void*, const float*, int, int, int, hipStream_t);
 void prefill_rope(const void*, const float*, const float*, void*, void*, void*, int, int, int, int, float, hipStream_t);
+void prefill_ln_shift(const float*, const float*, const float*, void*, void*, int, int, int, int, float, int, hipStream_t);
+void prefill_softmax(const float*, const bool*, void*, long, int, hipStream_t);
+void prefill_residual(float*, const void*, const float*, long, int, hipStream_t);
 void decode_attn_part(const float*, int, const float*, const float*, float, void*, void*, void*, const int*, const DecodeGeom&, int,
                       hipStream_t, const int*);
 bool skinny_partials(SkinnyArgs, hipStream_t);
@@ -1187,6 +1190,39 @@ void prefill_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Te
                       B, P, H, kc.size(1), (float)qscale, cur_stream());
 }
 
+// caption prefill: LN + text shift of x (B, P, D) fp32 -> hist[:, :P] (B, n, D) bf16 (unshifted) and out (B, P, D) bf16
+void prefill_ln_shift_(Tensor x, Tensor w, Tensor b, Tensor hist, Tensor out, bool shift, double eps) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(w, torch::kFloat32); CHECK_IN(b, torch::kFloat32);
+  CHECK_IN(hist, torch::kBFloat16); CHECK_IN(out, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 3, "prefill_ln_shift: x (B, P, D)");
+  const int B = x.size(0), P = x.size(1), D = x.size(2);
+  TORCH_CHECK(D == 256 || D == 512 || D == 1024 || D == 2048, "prefill_ln_shift: unsupported hidden size");
+  TORCH_CHECK(w.numel() == D && b.numel() == D && out.sizes() == x.sizes() && hist.dim() == 3 && hist.size(0) == B &&
+              hist.size(1) >= P && hist.size(2) == D, "prefill_ln_shift: shapes");
+  dalle::prefill_ln_shift(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), hist.data_ptr(), out.data_ptr(), B, P,
+                          hist.size(1), D, (float)eps, shift ? 1 : 0, cur_stream());
+}
+
+// caption prefill: masked row softmax of fp32 scores (R, P, P) -> bf16, mask (>= P, >= P) bool, row i of a (P, P) block
+// reads mask row i
+void prefill_softmax_(Tensor sc, Tensor mask, Tensor out) {
+  CHECK_IN(sc, torch::kFloat32); CHECK_IN(out, torch::kBFloat16); CHECK_CUDA(mask);
+  TORCH_CHECK(mask.scalar_type() == torch::kBool, "prefill_softmax: mask must be bool");
+  TORCH_CHECK(sc.dim() == 3 && sc.size(1) == sc.size(2) && out.sizes() == sc.sizes(), "prefill_softmax: sc / out (R, P, P)");
+  const int P = sc.size(2);
+  TORCH_CHECK(P <= 512, "prefill_softmax: at most 512 keys");
+  TORCH_CHECK(mask.dim() == 2 && mask.size(0) == P && mask.size(1) == P && mask.is_contiguous(), "prefill_softmax: mask (P, P) contiguous");
+  dalle::prefill_softmax(sc.data_ptr<float>(), mask.data_ptr<bool>(), out.data_ptr(), (long)sc.size(0) * P, P, cur_stream());
+}
+
+// caption prefill: x += scale * y (x fp32, y bf16, same shape (.., D); scale (D,) fp32)
+void prefill_residual_(Tensor x, Tensor y, Tensor scale) {
+  CHECK_IN(x, torch::kFloat32); CHECK_IN(y, torch::kBFloat16); CHECK_IN(scale, torch::kFloat32);
+  const int D = x.size(-1);
+  TORCH_CHECK(y.sizes() == x.sizes() && scale.numel() == D && D % 4 == 0, "prefill_residual: shapes");
+  dalle::prefill_residual(x.data_ptr<float>(), y.data_ptr(), scale.data_ptr<float>(), x.numel(), D, cur_stream());
+}
+
 void decode_rope_(Tensor qkv, Tensor cosT, Tensor sinT, Tensor q, Tensor kc, Tensor vc, Tensor pos, int64_t H, double qscale) {
   CHECK_IN(qkv, torch::kBFloat16); CHECK_IN(cosT, torch::kFloat32); CHECK_IN(sinT, torch::kFloat32);
   CHECK_IN(q, torch::kBFloat16); CHECK_IN(kc, torch::kBFloat16); CHECK_IN(vc, torch::kBFloat16); CHECK_IN(pos, torch::kInt32);
@@ -1414,6 +1450,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pbias") = py::none(), py::arg("pscale") = py::none());
   m.def("decode_rope_", &decode_rope_);
   m.def("prefill_rope_", &prefill_rope_);
+  m.def("prefill_ln_shift_", &prefill_ln_shift_);
+  m.def("prefill_softmax_", &prefill_softmax_);
+  m.def("prefill_residual_", &prefill_residual_);
   m.def("decode_attn_", &decode_attn_, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("out"), py::arg("pos"), py::arg("T"),
         py::arg("S"), py::arg("H"), py::arg("K"), py::arg("pattern"), py::arg("text_shared") = py::none());
   m.def("skinny_linear", &skinny_linear);

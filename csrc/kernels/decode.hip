@@ -187,6 +187,126 @@ void prefill_rope(const void* qkv, const float* cosT, const float* sinT, void* q
                      (__bf16*)q, (__bf16*)kc, (__bf16*)vc, B, P, H, n, qscale);
 }
 
+// ---- batched caption prefill: LayerNorm + text token shift of every (b, p) row, one wave per row ----
+// x (B, P, D) fp32 -> hist[b, p] (the unshifted LN output, bf16: the history the decode steps shift from,
+// hist is (B, n, D)) and out (B, P, D) bf16 with the shift applied by push: channels [0, D/2) of row p land
+// in row p + 1 and row 0 gets zeros there (shift = 0: out = the LN output). Replaces the PyTorch chain
+// layer_norm -> bf16 cast -> history copy -> clone -> two slice copies (six passes over the rows).
+template <int D>
+__global__ __launch_bounds__(256) void prefill_ln_shift_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ bias, __bf16* __restrict__ hist,
+                                                               __bf16* __restrict__ out, int B, int P, int n, float eps, int shift) {
+  constexpr int PER = D / 256;  // float4 per lane
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (row >= B * P) return;
+  const int b = row / P, p = row - b * P;
+  const float* xr = x + (size_t)row * D;
+  f32x4 v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = *reinterpret_cast<const f32x4*>(xr + 4 * (lane + 64 * j));
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const float d = v[j][i] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  __bf16* hr = hist + ((size_t)b * n + p) * D;
+  __bf16* orow = out + (size_t)row * D;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[j][i] - mean) * rstd * wv[i] + bv[i];
+    const s16x4 pk = pack4(o);
+    *reinterpret_cast<s16x4*>(hr + c) = pk;
+    if (shift && c < D / 2) {
+      if (p + 1 < P) *reinterpret_cast<s16x4*>(orow + D + c) = pk;
+      if (p == 0) *reinterpret_cast<s16x4*>(orow + c) = s16x4{};
+    } else {
+      *reinterpret_cast<s16x4*>(orow + c) = pk;
+    }
+  }
+}
+
+void prefill_ln_shift(const float* x, const float* w, const float* b, void* hist, void* out, int B, int P, int n, int D, float eps,
+                      int shift, hipStream_t st) {
+  const dim3 grid(((long)B * P + 3) / 4);
+  switch (D) {
+    case 256: hipLaunchKernelGGL(prefill_ln_shift_kernel<256>, grid, dim3(256), 0, st, x, w, b, (__bf16*)hist, (__bf16*)out, B, P, n, eps, shift); break;
+    case 512: hipLaunchKernelGGL(prefill_ln_shift_kernel<512>, grid, dim3(256), 0, st, x, w, b, (__bf16*)hist, (__bf16*)out, B, P, n, eps, shift); break;
+    case 1024: hipLaunchKernelGGL(prefill_ln_shift_kernel<1024>, grid, dim3(256), 0, st, x, w, b, (__bf16*)hist, (__bf16*)out, B, P, n, eps, shift); break;
+    case 2048: hipLaunchKernelGGL(prefill_ln_shift_kernel<2048>, grid, dim3(256), 0, st, x, w, b, (__bf16*)hist, (__bf16*)out, B, P, n, eps, shift); break;
+  }
+}
+
+// ---- batched caption prefill: masked softmax of the fp32 scores (R, P, P) -> bf16 probabilities, one wave per
+// row (query i = row % P reads mask row i: the layer's static pattern over the caption, true = attend). One pass
+// instead of masked_fill -> softmax -> bf16 cast over the fp32 scores. P <= 512 (8 columns per lane). ----
+__global__ __launch_bounds__(256) void prefill_softmax_kernel(const float* __restrict__ sc, const bool* __restrict__ mask,
+                                                              __bf16* __restrict__ out, long rows, int P) {
+  const long row = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int i = row % P;
+  const float* sr = sc + row * P;
+  const bool* mr = mask + (size_t)i * P;
+  float v[8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    v[t] = (j < P && mr[j]) ? sr[j] : -INFINITY;
+    m = fmaxf(m, v[t]);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    v[t] = v[t] == -INFINITY ? 0.f : __expf(v[t] - m);
+    s += v[t];
+  }
+  s = wave_sum(s);
+  const float inv = s > 0.f ? 1.0f / s : 0.f;
+  __bf16* orow = out + row * P;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int j = lane + 64 * t;
+    if (j < P) orow[j] = (__bf16)(v[t] * inv);
+  }
+}
+
+void prefill_softmax(const float* sc, const bool* mask, void* out, long rows, int P, hipStream_t st) {
+  hipLaunchKernelGGL(prefill_softmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, sc, mask, (__bf16*)out, rows, P);
+}
+
+// ---- batched caption prefill: the residual update x += scale * y of a sublayer (y: the projection's bf16
+// output, bias included; scale: LayerScale (D,)), one pass instead of the bf16->fp32 cast, the scale and the add ----
+__global__ __launch_bounds__(256) void prefill_residual_kernel(float* __restrict__ x, const __bf16* __restrict__ y,
+                                                               const float* __restrict__ scale, long n4, int D) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n4) return;
+  const int c = i % D;
+  float yv[4];
+  unpack4(*reinterpret_cast<const s16x4*>(y + i), yv);
+  f32x4 xv = *reinterpret_cast<const f32x4*>(x + i);
+  const f32x4 sv = *reinterpret_cast<const f32x4*>(scale + c);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) xv[t] += sv[t] * yv[t];
+  *reinterpret_cast<f32x4*>(x + i) = xv;
+}
+
+void prefill_residual(float* x, const void* y, const float* scale, long n, int D, hipStream_t st) {
+  hipLaunchKernelGGL(prefill_residual_kernel, dim3((n / 4 + 255) / 256), dim3(256), 0, st, x, (const __bf16*)y, scale, n, D);
+}
+
 // the last pending update of a step (before the final LayerNorm): x += scale * (sum_ks part + bias)
 __global__ __launch_bounds__(256) void residual_from_partials_kernel(float* __restrict__ x, PendingRes pr, int B, int D) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;

@@ -97,6 +97,7 @@ class DecodeEngine:
         self.seed = torch.zeros((), dtype=torch.int64, device=dev)
         self.graph = None
         self._pf_graphs = {}  # captured caption prefills, by (rows, input buffer)
+        self._pf_masks = {}   # contiguous (P, P) caption blocks of the layer patterns
         self._static_logits = None
         self._w = {}
         # decode-step projections through the skinny MFMA GEMM (csrc/kernels/skinny.hip) with the
@@ -385,6 +386,12 @@ class DecodeEngine:
         shifted rows (the text shift takes channels [0, d/2) from the previous position)."""
         pre = ls.fn
         P = x.shape[1]
+        if self.use_hip:  # one kernel: LN, the history rows and the pushed shift (decode.hip prefill_ln_shift)
+            from ..ops.hip_ops import C
+            out = torch.empty(x.shape, dtype=self.cdt, device=x.device)
+            C().prefill_ln_shift_(x, pre.norm.weight.detach(), pre.norm.bias.detach(), hist, out, bool(pre.fn.enabled),
+                                  float(pre.norm.eps))
+            return out
         y = F.layer_norm(x, (self.d,), pre.norm.weight.detach(), pre.norm.bias.detach(), pre.norm.eps).to(self.cdt)
         hist[:, :P] = y
         if not pre.fn.enabled:
@@ -401,20 +408,20 @@ class DecodeEngine:
         h = self._pf_ln_shift(ls, self.hist[li][0][:B], x)
         kc, vc = self.kc[li][: B * H], self.vc[li][: B * H]  # the first B rows' caches (all of them, or row 0)
         if self.use_hip:
-            # one kernel rotates q / k / v and writes k / v into the caches (q pre-scaled, bf16 as in the
-            # decode steps); scores in fp32, causal over the caption
+            # the projections on the assembly GEMM where the rows tile (_pf_linear); one kernel rotates q / k / v and
+            # writes k / v into the caches (q pre-scaled, bf16 as in the decode steps); scores in fp32, then one
+            # masked-softmax kernel to bf16 probabilities. Returns the bf16 projection output (bias included).
             from ..ops.hip_ops import C
-            qkv = F.linear(h, self._wt(attn.to_qkv.weight)).contiguous()
+            qkv = self._pf_linear(h.view(B * P, self.d), attn.to_qkv.weight).view(B, P, -1)
             q = torch.empty(B * H, P, Dh, dtype=self.cdt, device=x.device)
             C().prefill_rope_(qkv, self.cos, self.sin, q, kc, vc, H, Dh ** -0.5)
             k, v = kc[:, :P], vc[:, :P]
             sc = torch.bmm(q, k.transpose(1, 2), out_dtype=torch.float32)
-            mask = static_mask(self.geom, attn.attn_type, self.n, device=x.device)[:P, :P]
-            sc.masked_fill_(~mask, float("-inf"))
-            o = torch.bmm(torch.softmax(sc, -1).to(self.cdt), v)
-            o = o.view(B, H, P, Dh).transpose(1, 2).reshape(B, P, H * Dh)
-            y = F.linear(o, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias)).float()
-            return y * self._scale(ls)
+            pr = torch.empty(sc.shape, dtype=self.cdt, device=x.device)
+            C().prefill_softmax_(sc, self._pf_mask(attn.attn_type, P, x.device), pr)
+            o = torch.bmm(pr, v)
+            o = o.view(B, H, P, Dh).transpose(1, 2).reshape(B * P, H * Dh)
+            return self._pf_linear(o, attn.to_out[0].weight, attn.to_out[0].bias).view(B, P, -1)
         qkv = F.linear(h, self._wt(attn.to_qkv.weight)).view(B, P, 3, H, Dh).permute(2, 0, 3, 1, 4).float()
         c, sn = self.cos[:P], self.sin[:P]
         q, k, v = (apply_rotary(t, c, sn) for t in qkv)
@@ -426,20 +433,48 @@ class DecodeEngine:
         mask = static_mask(self.geom, attn.attn_type, self.n, device=x.device)[:P, :P]
         o = torch.softmax(sc.masked_fill(~mask, float("-inf")), -1) @ v
         o = o.transpose(1, 2).reshape(B, P, H * Dh).to(self.cdt)
-        y = F.linear(o, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias)).float()
-        return y * self._scale(ls)
+        return F.linear(o, self._wt(attn.to_out[0].weight), self._wt(attn.to_out[0].bias))
+
+    def _pf_linear(self, x2, w, b=None):
+        """x2 (M, K) bf16 . W^T (+ b) for the prefill: the assembly GEMM where the rows tile (its epilogue reads the
+        fp32 bias parameter), else hipBLASLt -- with the engine's own bf16 copies either way, never the per-forward
+        cast cache (a captured prefill must hold only buffers that outlive it)."""
+        from ..ops.hip_ops import ASM_GEMM, C, _asm_ok
+        wb = self._wt(w)
+        if ASM_GEMM and _asm_ok(x2, wb) and (b is None or (b.dtype == torch.float32 and b.is_contiguous())):
+            return C().asm_gemm(x2, wb, None if b is None else b.detach(), None)
+        return F.linear(x2, wb, None if b is None else self._wt(b))
+
+    def _pf_mask(self, attn_type: str, P: int, device):
+        """The layer pattern's (P, P) caption block, contiguous (cached: the first, eager prefill fills it before
+        the pass is captured)."""
+        key = (attn_type, P)
+        m = self._pf_masks.get(key)
+        if m is None:
+            m = static_mask(self.geom, attn_type, self.n, device=device)[:P, :P].contiguous()
+            self._pf_masks[key] = m
+        return m
 
     def _pf_ff(self, li, ls, x):
         ff = ls.fn.fn.fn
-        h = self._pf_ln_shift(ls, self.hist[li][1][: x.shape[0]], x)
-        a = F.linear(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias))
+        B, P = x.shape[0], x.shape[1]
+        h = self._pf_ln_shift(ls, self.hist[li][1][:B], x)
         if self.use_hip:
             from ..ops.hip_ops import C
-            u = C().geglu_fwd(a.reshape(-1, a.shape[-1]).contiguous()).view(*a.shape[:-1], -1)
-        else:
-            val, gate = a.float().chunk(2, -1)
-            u = (val * F.gelu(gate)).to(self.cdt)
-        return F.linear(u, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias)).float() * self._scale(ls)
+            u = C().geglu_fwd(self._pf_linear(h.view(B * P, self.d), ff.net[0].weight, ff.net[0].bias))
+            return self._pf_linear(u, ff.net[3].weight, ff.net[3].bias).view(B, P, -1)
+        a = F.linear(h, self._wt(ff.net[0].weight), self._wt(ff.net[0].bias))
+        val, gate = a.float().chunk(2, -1)
+        u = (val * F.gelu(gate)).to(self.cdt)
+        return F.linear(u, self._wt(ff.net[3].weight), self._wt(ff.net[3].bias))
+
+    def _pf_add(self, x, ls, y):
+        """x + LayerScale * y for a sublayer's projection output y: in place, one kernel, on MI355X."""
+        if self.use_hip:
+            from ..ops.hip_ops import C
+            C().prefill_residual_(x, y, self._scale(ls))
+            return x
+        return x + y.float() * self._scale(ls)
 
     def _pf_rows(self) -> int:
         """Rows the caption prefill runs for (after ``_start``): 1 when every row holds row 0's caption (a
@@ -488,12 +523,12 @@ class DecodeEngine:
         if self.cfg.reversible:
             x1, x2 = x, x.clone()
             for li, (f, g) in enumerate(self.pairs):
-                x1 = x1 + self._pf_attn(li, f, x2)
-                x2 = x2 + self._pf_ff(li, g, x1)
+                x1 = self._pf_add(x1, f, self._pf_attn(li, f, x2))
+                x2 = self._pf_add(x2, g, self._pf_ff(li, g, x1))
         else:
             for li, (f, g) in enumerate(self.pairs):
-                x = x + self._pf_attn(li, f, x)
-                x = x + self._pf_ff(li, g, x)
+                x = self._pf_add(x, f, self._pf_attn(li, f, x))
+                x = self._pf_add(x, g, self._pf_ff(li, g, x))
         if rows < self.B:  # the other rows' own reads: the LN history the first decode step shifts in
             for hs in self.hist:
                 for hb in hs:

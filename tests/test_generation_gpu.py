@@ -241,3 +241,41 @@ def test_repeated_caption_prefill_runs_row0_only(cuda, reversible):
     assert (got == ref).float().mean().item() > 0.95
     # rows 1.. never had their own text caches filled: the reads really come from row 0
     assert eng.kc[0].view(B, cfg.heads, -1, cfg.dim_head)[1:, :, : eng.T - 1].abs().sum().item() == 0.0
+
+
+def test_prefill_kernels_match_torch(cuda):
+    """The caption-prefill kernels (decode.hip) against the PyTorch chains they replace, fp32 references:
+    LN + pushed text shift + history rows, masked row softmax to bf16, the LayerScale residual update."""
+    from dalle_amd.ops.hip_ops import C
+
+    torch.manual_seed(0)
+    B, P, n, D = 3, 256, 300, 1024
+    x = torch.randn(B, P, D, device=cuda) * 2 + 0.5
+    w, b = torch.randn(D, device=cuda), torch.randn(D, device=cuda)
+    for shift in (True, False):
+        hist = torch.zeros(B, n, D, dtype=torch.bfloat16, device=cuda)
+        out = torch.empty(B, P, D, dtype=torch.bfloat16, device=cuda)
+        C().prefill_ln_shift_(x, w, b, hist, out, shift, 1e-5)
+        y = torch.nn.functional.layer_norm(x, (D,), w, b, 1e-5)
+        ref = y.clone()
+        if shift:
+            ref[:, 1:, : D // 2] = y[:, :-1, : D // 2]
+            ref[:, 0, : D // 2] = 0
+        assert (hist[:, :P].float() - y).abs().max().item() < 0.05
+        assert torch.count_nonzero(hist[:, P:]) == 0  # nothing past the caption rows
+        assert (out.float() - ref).abs().max().item() < 0.05
+    R = 2 * 16
+    sc = torch.randn(R, P, P, device=cuda) * 3
+    mask = torch.tril(torch.ones(P, P, dtype=torch.bool, device=cuda))
+    mask[5, :3] = False  # a non-causal hole: the kernel reads the mask, it does not assume causality
+    pr = torch.empty(R, P, P, dtype=torch.bfloat16, device=cuda)
+    C().prefill_softmax_(sc, mask, pr)
+    ref = torch.softmax(sc.masked_fill(~mask, float("-inf")), -1)
+    assert (pr.float() - ref).abs().max().item() < 4e-3
+    assert torch.count_nonzero(pr.float() * (~mask).float()) == 0
+    xr = torch.randn(B, P, D, device=cuda)
+    yb = torch.randn(B, P, D, device=cuda).to(torch.bfloat16)
+    s = torch.rand(D, device=cuda)
+    want = xr + yb.float() * s
+    C().prefill_residual_(xr, yb, s)
+    assert torch.allclose(xr, want, rtol=1e-6, atol=1e-6)
