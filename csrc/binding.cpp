@@ -1078,7 +1078,7 @@ Tensor conv_out(Tensor x, Tensor w, Tensor bias, Tensor mean, Tensor rstd, Tenso
   auto img = torch::empty({N, 3, H, W}, x.options().dtype(torch::kFloat32));
   TORCH_CHECK(dalle::conv_out(x.data_ptr(), w.data_ptr(), opt_f32(bias, 3, "conv_out bias"), opt_f32(mean, (long)N * 32, "mean"),
                               opt_f32(rstd, (long)N * 32, "rstd"), opt_f32(gamma, C, "gamma"), opt_f32(beta, C, "beta"),
-                              img.data_ptr<float>(), N, H, W, C, cur_stream()), "conv_out: C must be <= 128 and a multiple of 8");
+                              img.data_ptr<float>(), N, H, W, C, cur_stream()), "conv_out: C must be <= 128 and a multiple of 32");
   return img;
 }
 

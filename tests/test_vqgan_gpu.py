@@ -45,6 +45,28 @@ def test_conv3x3_kernel_vs_torch(cuda):
         assert _rel(y, ref) < 2e-2, (n, h, w, cin, cout, ups, gn, _rel(y, ref))
 
 
+@pytest.mark.parametrize("n,h,w,cin", [(2, 256, 256, 128), (1, 40, 24, 64), (2, 16, 48, 32)])
+def test_conv_out_kernel_vs_torch(cuda, n, h, w, cin):
+    """The RGB output conv (GroupNorm + SiLU + 3x3 conv to 3 channels + clamp / rescale, NCHW fp32) on 16 x 16
+    LDS tiles over 32-channel chunks, including image sides that are not tile multiples."""
+    C = __import__("dalle_amd.ops.ext", fromlist=["x"]).load_extension(required=True)
+    torch.manual_seed(1)
+    x = torch.randn(n, h, w, cin, device=cuda)
+    conv = torch.nn.Conv2d(cin, 3, 3, 1, 1).to(cuda)
+    norm = torch.nn.GroupNorm(32, cin, eps=1e-6).to(cuda)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.3, 0.3)
+    xb = x.bfloat16().contiguous()
+    ref = conv(torch.nn.functional.silu(norm(xb.float().permute(0, 3, 1, 2))))
+    ref = (ref.clamp(-1, 1) + 1) * 0.5
+    mean, rstd = C.gn_stats(xb, 1e-6)
+    wk = conv.weight.detach().permute(0, 2, 3, 1).reshape(3, -1).bfloat16().contiguous()
+    img = C.conv_out(xb, wk, conv.bias.detach().float(), mean, rstd, norm.weight.detach().float(), norm.bias.detach().float())
+    assert img.shape == ref.shape
+    assert (img - ref).abs().max().item() < 2e-2, (n, h, w, cin, (img - ref).abs().max().item())
+
+
 def test_hip_decoder_matches_torch(cuda, monkeypatch):
     torch.manual_seed(0)
     ddconfig = dict(ch=128, out_ch=3, ch_mult=(1, 2, 4), num_res_blocks=1, attn_resolutions=(16,), resolution=64,
