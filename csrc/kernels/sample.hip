@@ -6,9 +6,9 @@
 //   * top-p on the softmax of the kept logits, sorted descending: keep while the EXCLUSIVE cumulative
 //     probability <= p (the token that crosses p stays);
 //   * sample argmax(l / T - log(-log u)) over the kept set (T <= 1e-10: greedy argmax).
-// One workgroup (256 threads) per batch row, the row's logits (V <= 8192) live in registers:
-//   * k-th largest by a 4-pass 8-bit radix select on order-preserving uint32 keys (LDS histograms
-//     with integer atomics -- exact and order independent), the bin search is one wave's suffix scan;
+// One workgroup (1024 threads) per batch row, the row's logits (V <= 8192) live in registers:
+//   * k-th largest on order-preserving uint32 keys, bit by bit from the top (32 block counts, no atomics:
+//     exact and order independent);
 //   * top-p only: the survivors are compacted (index order) into LDS as 64-bit (key, ~index) words,
 //     bitonic-sorted descending, and a fixed-order block scan of exp(l - max) finds the cut;
 //   * the uniforms come from a counter-based hash of (seed, position, row, token) -- replay-safe inside
@@ -20,8 +20,9 @@
 
 namespace dalle {
 
-constexpr int SMP_THREADS = 256;
-constexpr int SMP_VPT = 32;                           // logits per thread
+constexpr int SMP_THREADS = 1024;                     // 16 waves: the top-k select's per-step work is per lane
+constexpr int SMP_VPT = 8;                            // logits per thread
+constexpr int SMP_NW = SMP_THREADS / 64;
 constexpr int SMP_VMAX = SMP_THREADS * SMP_VPT;       // 8192 = the image vocabulary
 
 __device__ __forceinline__ uint32_t order_key(float f) {
@@ -45,9 +46,9 @@ __device__ __forceinline__ float gumbel(uint64_t seed, int pos, int row, int idx
   return -__logf(-__logf(u));
 }
 
-// Exclusive scan over the 256 threads of the block in a fixed order (wave shuffles + 4 wave totals);
-// returns this thread's exclusive prefix and the block total. `red` holds >= 4 floats of LDS.
-__device__ __forceinline__ float block_excl_scan_256(float v, float* red, float& total) {
+// Exclusive scan over the SMP_THREADS threads of the block in a fixed order (wave shuffles + the wave totals);
+// returns this thread's exclusive prefix and the block total. `red` holds >= SMP_NW floats of LDS.
+__device__ __forceinline__ float block_excl_scan(float v, float* red, float& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float inc = v;
 #pragma unroll
@@ -58,9 +59,12 @@ __device__ __forceinline__ float block_excl_scan_256(float v, float* red, float&
   __syncthreads();
   if (lane == 63) red[wave] = inc;
   __syncthreads();
-  float before = 0.f;
-  for (int w = 0; w < wave; ++w) before += red[w];
-  total = red[0] + red[1] + red[2] + red[3];
+  float before = 0.f, tot = 0.f;
+  for (int w = 0; w < SMP_NW; ++w) {
+    if (w < wave) before += red[w];
+    tot += red[w];
+  }
+  total = tot;
   return before + inc - v;
 }
 
@@ -72,59 +76,43 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 
 __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
   __shared__ uint64_t srt[SMP_VMAX];  // top-p: (key << 32 | ~index), 64 KB
-  __shared__ int hist[256];
-  __shared__ int s_bin, s_rem;
-  __shared__ float redf[SMP_THREADS / 64];
-  __shared__ int redi[SMP_THREADS / 64];
+  __shared__ int cntb[2][SMP_NW];
+  __shared__ float redf[SMP_NW];
+  __shared__ int redi[SMP_NW];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* lr = a.logits + (size_t)row * a.V;
 
   uint32_t key[SMP_VPT];
+  {
+    // unconditional (clamped) loads: all 32 in flight at once (a guarded load per slot compiled to 32 serial
+    // load -> vmcnt(0) round trips, ~7 us per row)
+    float lv[SMP_VPT];
 #pragma unroll
-  for (int i = 0; i < SMP_VPT; ++i) {
-    const int idx = i * SMP_THREADS + tid;  // coalesced
-    key[i] = idx < a.V ? order_key(lr[idx]) : 0u;
+    for (int i = 0; i < SMP_VPT; ++i) lv[i] = lr[min(i * SMP_THREADS + tid, a.V - 1)];  // coalesced
+#pragma unroll
+    for (int i = 0; i < SMP_VPT; ++i) key[i] = i * SMP_THREADS + tid < a.V ? order_key(lv[i]) : 0u;
   }
 
-  // ---- top-k threshold: the k-th largest key (exact radix select) ----
+  // ---- top-k threshold: the k-th largest key, bit by bit from the top ----
+  // t = the largest key with #{key >= t} >= k (exact; ties kept), one block count per bit. No atomics: the former
+  // radix histograms' LDS atomics serialised on the few exponent bins that logits share. (Two bits per step --
+  // three candidate counts per barrier -- measured slower at 256 and at 1024 threads.)
   uint32_t kth = 0u;
   if (a.top_k > 0 && a.top_k < a.V) {
-    uint32_t prefix = 0u, pmask = 0u;
-    int rem = a.top_k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
-      __syncthreads();
+    uint32_t t = 0u;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = t | (1u << bit);
+      int c = 0;  // the wave's count: one compare-to-mask and a scalar popcount per slot, no cross-lane shuffles
 #pragma unroll
-      for (int i = 0; i < SMP_VPT; ++i)
-        if (i * SMP_THREADS + tid < a.V && (key[i] & pmask) == prefix) atomicAdd(&hist[(key[i] >> shift) & 255], 1);
+      for (int i = 0; i < SMP_VPT; ++i) c += __popcll(__ballot(key[i] >= cand));  // padding keys are 0 < cand
+      if (lane == 0) cntb[bit & 1][wave] = c;  // two buffers: one barrier per bit suffices
       __syncthreads();
-      if (wave == 0) {
-        // lane l owns bins 4l..4l+3; suffix scan (from the top bin down) across lanes
-        int c[4], own = 0;
+      int tot = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { c[j] = hist[4 * lane + j]; own += c[j]; }
-        int suf = own;  // inclusive suffix over lanes >= lane
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int v = __shfl_down(suf, o, 64);
-          if (lane + o < 64) suf += v;
-        }
-        const int above = suf - own;  // count in bins owned by higher lanes
-        if (above < rem && suf >= rem) {
-          int acc = above;
-          for (int j = 3; j >= 0; --j) {
-            if (acc + c[j] >= rem) { s_bin = 4 * lane + j; s_rem = rem - acc; break; }
-            acc += c[j];
-          }
-        }
-      }
-      __syncthreads();
-      prefix |= (uint32_t)s_bin << shift;
-      pmask |= 255u << shift;
-      rem = s_rem;
-      __syncthreads();
+      for (int w = 0; w < SMP_NW; ++w) tot += cntb[bit & 1][w];
+      if (tot >= a.top_k) t = cand;
     }
-    kth = prefix;
+    kth = t;
   }
 
   // ---- top-p: compact the survivors, sort descending, cut at the exclusive-cumsum crossing ----
@@ -136,7 +124,7 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
     for (int i = 0; i < SMP_VPT; ++i) mine += (i * SMP_THREADS + tid < a.V && key[i] >= kth) ? 1 : 0;
     // slots by an exclusive scan of the per-thread counts (any fixed order: the sort imposes the final one)
     float ftot;
-    int w = (int)block_excl_scan_256((float)mine, redf, ftot);
+    int w = (int)block_excl_scan((float)mine, redf, ftot);
     const int cnt = (int)ftot;
     int P = 1;
     while (P < cnt) P <<= 1;
@@ -166,7 +154,7 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
     float part = 0.f;
     for (int j = c0; j < c1; ++j) part += __expf(key_float((uint32_t)(srt[j] >> 32)) - mx);
     float psum;
-    float run = block_excl_scan_256(part, redf, psum);
+    float run = block_excl_scan(part, redf, psum);
     const float limit = a.top_p * psum;
     // kept = #{j : exclusive_cum(j) <= limit}; monotone, so each chunk counts its own
     int kept = 0;
@@ -178,7 +166,8 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
     __syncthreads();
     if (lane == 0) redi[wave] = kept;
     __syncthreads();
-    n_keep = redi[0] + redi[1] + redi[2] + redi[3];
+    n_keep = 0;
+    for (int w = 0; w < SMP_NW; ++w) n_keep += redi[w];
     n_keep = max(n_keep, 1);
   }
 
@@ -198,6 +187,26 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
       const uint64_t e = srt[j];
       consider(key_float((uint32_t)(e >> 32)), (int)(~(uint32_t)e));
     }
+  } else if (kth != 0u && !greedy) {
+    // top-k: the kept (key, index) pairs compacted per wave (ballot + prefix popcount) into the wave's region of
+    // the sort buffer, then each lane draws the Gumbel noise of ~1 pair instead of the wave running the hash and
+    // logs for every slot in which any lane kept a logit (divergent: ~11 us per row)
+    uint64_t* wbuf = srt + wave * (SMP_VMAX / SMP_NW);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < SMP_VPT; ++i) {
+      const int idx = i * SMP_THREADS + tid;
+      const bool kept = idx < a.V && key[i] >= kth;
+      const uint64_t m = __ballot(kept);
+      if (kept) wbuf[cnt + __popcll(m & lt)] = ((uint64_t)key[i] << 32) | (uint32_t)idx;
+      cnt += __popcll(m);
+    }
+    __syncthreads();  // the wave's pairs are in LDS before its lanes read each other's
+    for (int j = lane; j < cnt; j += 64) {
+      const uint64_t e = wbuf[j];
+      consider(key_float((uint32_t)(e >> 32)), (int)(uint32_t)e);
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < SMP_VPT; ++i) {
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(SMP_THREADS) void sample_kernel(SampleArgs a) {
   if (lane == 0) { redf[wave] = best; redi[wave] = besti; }
   __syncthreads();
   if (tid == 0) {
-    for (int w = 1; w < SMP_THREADS / 64; ++w)
+    for (int w = 1; w < SMP_NW; ++w)
       if (redf[w] > best || (redf[w] == best && redi[w] < besti)) { best = redf[w]; besti = redi[w]; }
     const int64_t nxt = besti;
     if (a.sampled) a.sampled[row] = nxt;
