@@ -37,39 +37,43 @@ __global__ __launch_bounds__(D / 4) void decode_ln_shift_kernel(float* __restric
   // and the shifted history row (an earlier position, written by an earlier step) -- so all of them
   // are issued before the first reduction: one memory round trip per step
   const int B = gridDim.x;
-  f32x4 t[16];
-  if (pr.part != nullptr) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      t[k] = k < pr.KS ? *reinterpret_cast<const f32x4*>(pr.part + ((size_t)k * B + b) * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  // all loads unconditional and in one basic block (slab index clamped to KS - 1, shift row clamped to row 0 and
+  // masked after): the guarded forms compiled to a vmcnt(0) round trip after the first slab load and after the
+  // shift-row load, two extra memory latencies per call
+  const bool pend = pr.part != nullptr;  // uniform
+  // the row, the LN parameters first; then the slabs through a pointer that is valid either way (the row itself
+  // when nothing is pending, slab index 0) and the bias through one that is (the scale vector: >= D bf16)
   f32x4 v = *reinterpret_cast<const f32x4*>(xr + c);
   const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
   const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + c);
-  s16x4 sh = s16x4{};
-  if (shift && c < D / 2) {
-    int src = -1;
-    if (pos < g.T) {
-      src = pos - 1;
-    } else {
-      const int k = pos - g.T;
-      if (c < D / 4) src = (k >= g.S) ? pos - g.S : -1;
-      else src = (k % g.S) ? pos - 1 : -1;
-    }
-    if (src >= 0) sh = *reinterpret_cast<const s16x4*>(hb + (size_t)src * D + c);
-  }
-  if (pr.part != nullptr) {
-    const f32x4 sc = *reinterpret_cast<const f32x4*>(pr.scale + c);
-    float pb[4] = {0.f, 0.f, 0.f, 0.f};
-    if (pr.bias != nullptr) {
-      float f[4];
-      unpack4(*reinterpret_cast<const s16x4*>(pr.bias + c), f);
+  const float* pp = pend ? pr.part : x;
+  const int klast = pend ? pr.KS - 1 : 0;
+  f32x4 t[16];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pb[i] = f[i];
-    }
+  for (int k = 0; k < 16; ++k) t[k] = *reinterpret_cast<const f32x4*>(pp + ((size_t)min(k, klast) * B + b) * D + c);
+  const float* scp = pend ? pr.scale : w;
+  const f32x4 sc = *reinterpret_cast<const f32x4*>(scp + c);
+  const __bf16* bpp = (pend && pr.bias != nullptr) ? pr.bias : reinterpret_cast<const __bf16*>(w);
+  const s16x4 pbr = *reinterpret_cast<const s16x4*>(bpp + c);
+  const bool has_pb = pend && pr.bias != nullptr;
+  const bool shifted = shift && c < D / 2;
+  int src;
+  if (pos < g.T) {
+    src = pos - 1;
+  } else {
+    const int k = pos - g.T;
+    src = (c < D / 4) ? ((k >= g.S) ? pos - g.S : -1) : ((k % g.S) ? pos - 1 : -1);
+  }
+  const s16x4 shl = *reinterpret_cast<const s16x4*>(hb + (size_t)max(src, 0) * D + c);
+  const s16x4 sh = (shifted && src >= 0) ? shl : s16x4{};
+  if (pend) {
+    float pb[4];
+    unpack4(pbr, pb);
+    if (!has_pb) pb[0] = pb[1] = pb[2] = pb[3] = 0.f;
     f32x4 acc = t[0];  // fixed ks order: deterministic
 #pragma unroll
-    for (int k = 1; k < 16; ++k) acc += t[k];
+    for (int k = 1; k < 16; ++k)
+      if (k < pr.KS) acc += t[k];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] += sc[i] * (acc[i] + pb[i]);
     *reinterpret_cast<f32x4*>(xr + c) = v;
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(D / 4) void decode_ln_shift_kernel(float* __restric
   for (int i = 0; i < 4; ++i) o[i] = (v[i] - mean) * rstd * wv[i] + bv[i];
   const s16x4 packed = pack4(o);
   *reinterpret_cast<s16x4*>(hb + (size_t)pos * D + c) = packed;
-  *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = (shift && c < D / 2) ? sh : packed;
+  *reinterpret_cast<s16x4*>(y + (size_t)b * D + c) = shifted ? sh : packed;
 }
 
 // ---- rotary on q/k/v of the new token; k, v appended to the cache at `pos` ----

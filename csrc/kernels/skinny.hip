@@ -25,6 +25,7 @@ namespace dalle {
 
 constexpr int SK_U = 4;            // MFMA steps per wave (K = 128 per wave)
 constexpr int SK_KW = 32 * SK_U;   // K elements per wave
+constexpr int SK_KSU = 8;          // in-launch split-K: slabs the last arriver reads in one batch (more: a loop)
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -239,6 +240,22 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
   // Partials are written and read with agent-scope (device-coherent, L2-bypassing `sc1`) accesses and
   // ordered by vmcnt + barrier only: a __threadfence() here would write back and invalidate the L2
   // of the XCD on every workgroup (measured 5x slower).
+  // bias values of this thread's outputs, loaded ahead of the hand-off they do not depend on (in the epilogue each
+  // bias read compiled to its own load -> vmcnt(0) round trip after the slab sum)
+  const __bf16* bias = static_cast<const __bf16*>(a.bias);
+  const __bf16* bsrc = bias != nullptr ? bias : static_cast<const __bf16*>(a.W);  // branch-free: a valid address either way
+  float bvv[PPT][G][2];
+#pragma unroll
+  for (int c = 0; c < PPT; ++c) {
+    const int idx = min(tid + c * NT, P - 1);
+    const int col = n0 + 2 * (idx % PR);
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const uint32_t w2 = *reinterpret_cast<const uint32_t*>(bsrc + gi * a.N + col);  // the column pair (col even)
+      bvv[c][gi][0] = bias != nullptr ? __uint_as_float(w2 << 16) : 0.f;
+      bvv[c][gi][1] = bias != nullptr ? __uint_as_float(w2 & 0xffff0000u) : 0.f;
+    }
+  }
   if (a.KS > 1 && EPI != 4 && EPI != 5) {
 #pragma unroll
     for (int c = 0; c < PPT; ++c) {
@@ -264,12 +281,33 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
       if (idx >= P) break;
 #pragma unroll
       for (int gi = 0; gi < G; ++gi) { v[c][gi][0] = 0.f; v[c][gi][1] = 0.f; }
-      for (int s = 0; s < a.KS; ++s) {
-        float* wp = a.ws + (((size_t)s * ntiles + tile) * P + idx) * (2 * G);
+      if (a.KS <= SK_KSU) {
+        // every slab's value loaded at once (slab index clamped, the extra slots not summed): one round trip
+        // instead of one per slab
+        float lv[SK_KSU][G][2];
 #pragma unroll
-        for (int gi = 0; gi < G; ++gi)
+        for (int s = 0; s < SK_KSU; ++s) {
+          float* wp = a.ws + (((size_t)min(s, a.KS - 1) * ntiles + tile) * P + idx) * (2 * G);
 #pragma unroll
-          for (int e = 0; e < 2; ++e) v[c][gi][e] += __hip_atomic_load(wp + 2 * gi + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) lv[s][gi][e] = __hip_atomic_load(wp + 2 * gi + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int s = 0; s < SK_KSU; ++s)
+          if (s < a.KS)
+#pragma unroll
+            for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+              for (int e = 0; e < 2; ++e) v[c][gi][e] += lv[s][gi][e];  // fixed ks order
+      } else {
+        for (int s = 0; s < a.KS; ++s) {
+          float* wp = a.ws + (((size_t)s * ntiles + tile) * P + idx) * (2 * G);
+#pragma unroll
+          for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) v[c][gi][e] += __hip_atomic_load(wp + 2 * gi + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
     if (tid == 0) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -281,7 +319,6 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
     pos = *a.pos;
     if (pos < 0 || pos >= a.n) return;  // a replay past the cache end is a no-op, never an OOB write
   }
-  const __bf16* bias = static_cast<const __bf16*>(a.bias);
 #pragma unroll
   for (int c = 0; c < PPT; ++c) {
     const int idx = tid + c * NT;
@@ -299,7 +336,7 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
-    if (bias != nullptr) { y0 += (float)bias[col]; y1 += (float)bias[col + 1]; }
+    if (bias != nullptr) { y0 += bvv[c][0][0]; y1 += bvv[c][0][1]; }
     if (EPI == 0) {
       if (a.out_f32) {
         *reinterpret_cast<float2*>(reinterpret_cast<float*>(a.out) + (size_t)row * a.N + col) = make_float2(y0, y1);
@@ -309,7 +346,7 @@ __global__ __launch_bounds__(64 * WK) void skinny_gemm_kernel(SkinnyArgs a) {
       }
     } else if (EPI == 1) {
       float g0 = v[c][G - 1][0], g1 = v[c][G - 1][1];
-      if (bias != nullptr) { g0 += (float)bias[a.N + col]; g1 += (float)bias[a.N + col + 1]; }
+      if (bias != nullptr) { g0 += bvv[c][G - 1][0]; g1 += bvv[c][G - 1][1]; }
       uint32_t pk = (uint32_t)f2bf(y0 * gelu_erf(g0)) | ((uint32_t)f2bf(y1 * gelu_erf(g1)) << 16);
       *reinterpret_cast<uint32_t*>(reinterpret_cast<__bf16*>(a.out) + (size_t)row * a.N + col) = pk;
     } else if (EPI == 2) {
