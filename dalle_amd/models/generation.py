@@ -417,8 +417,12 @@ class DecodeEngine:
             C().prefill_rope_(qkv, self.cos, self.sin, q, kc, vc, H, Dh ** -0.5)
             k, v = kc[:, :P], vc[:, :P]
             sc = torch.bmm(q, k.transpose(1, 2), out_dtype=torch.float32)
-            pr = torch.empty(sc.shape, dtype=self.cdt, device=x.device)
-            C().prefill_softmax_(sc, self._pf_mask(attn.attn_type, P, x.device), pr)
+            mask = self._pf_mask(attn.attn_type, P, x.device)
+            if P <= 512:  # the kernel keeps a row's scores in registers (8 per lane)
+                pr = torch.empty(sc.shape, dtype=self.cdt, device=x.device)
+                C().prefill_softmax_(sc, mask, pr)
+            else:
+                pr = torch.softmax(sc.masked_fill_(~mask, float("-inf")), -1).to(self.cdt)
             o = torch.bmm(pr, v)
             o = o.view(B, H, P, Dh).transpose(1, 2).reshape(B * P, H * Dh)
             return self._pf_linear(o, attn.to_out[0].weight, attn.to_out[0].bias).view(B, P, -1)
