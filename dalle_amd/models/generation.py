@@ -386,7 +386,7 @@ class DecodeEngine:
         shifted rows (the text shift takes channels [0, d/2) from the previous position)."""
         pre = ls.fn
         P = x.shape[1]
-        if self.use_hip:  # one kernel: LN, the history rows and the pushed shift (decode.hip prefill_ln_shift)
+        if self.use_hip and self.d in (256, 512, 1024, 2048):  # one kernel: LN, history rows, pushed shift
             from ..ops.hip_ops import C
             out = torch.empty(x.shape, dtype=self.cdt, device=x.device)
             C().prefill_ln_shift_(x, pre.norm.weight.detach(), pre.norm.bias.detach(), hist, out, bool(pre.fn.enabled),
@@ -474,7 +474,7 @@ class DecodeEngine:
 
     def _pf_add(self, x, ls, y):
         """x + LayerScale * y for a sublayer's projection output y: in place, one kernel, on MI355X."""
-        if self.use_hip:
+        if self.use_hip and self.d % 4 == 0:
             from ..ops.hip_ops import C
             C().prefill_residual_(x, y, self._scale(ls))
             return x
