@@ -54,7 +54,7 @@ void transpose_bf16(const void* x, void* xt, int R, int C, hipStream_t st);
 bool conv3x3(const ConvArgs&, hipStream_t);
 bool gn_stats(const void*, float*, float*, float*, int, int, int, float, hipStream_t);
 size_t gn_part_floats(int);
-void gn_apply(const void*, const float*, const float*, const float*, const float*, void*, int, int, int, hipStream_t);
+void gn_apply(const void*, const float*, const float*, const float*, const float*, void*, int, int, int, hipStream_t, int);
 bool conv_out(const void*, const void*, const float*, const float*, const float*, const float*, const float*, float*, int, int,
               int, int, hipStream_t);
 void softmax_rows(const float*, void*, long, int, float, hipStream_t);
@@ -1057,7 +1057,7 @@ std::vector<Tensor> gn_stats(Tensor x, double eps) {
   return {mean, rstd};
 }
 
-Tensor gn_apply(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta) {
+Tensor gn_apply(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, bool silu) {
   CHECK_IN(x, torch::kBFloat16);
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 32 == 0 && x.size(3) % 8 == 0, "gn_apply: x (N, H, W, C)");
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -1066,7 +1066,7 @@ Tensor gn_apply(Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta) {
   const float* g = opt_f32(gamma, C, "gn_apply gamma");
   const float* b = opt_f32(beta, C, "gn_apply beta");
   auto y = torch::empty_like(x);
-  dalle::gn_apply(x.data_ptr(), m, r, g, b, y.data_ptr(), N, HW, C, cur_stream());
+  dalle::gn_apply(x.data_ptr(), m, r, g, b, y.data_ptr(), N, HW, C, cur_stream(), silu ? 1 : 0);
   return y;
 }
 
@@ -1441,7 +1441,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("rstd") = py::none(), py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
         py::arg("ups") = false);
   m.def("gn_stats", &gn_stats);
-  m.def("gn_apply", &gn_apply);
+  m.def("gn_apply", &gn_apply, py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("beta"),
+        py::arg("silu") = false);
   m.def("conv_out", &conv_out);
   m.def("softmax_rows", &softmax_rows);
   m.def("embed_bwd_", &embed_bwd_);

@@ -236,7 +236,7 @@ __global__ void gn_finalize_kernel(const float* __restrict__ part, float* __rest
 __global__ __launch_bounds__(256) void gn_apply_kernel(const __bf16* __restrict__ x, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, __bf16* __restrict__ y, long total8, int HW,
-                                                       int C) {
+                                                       int C, int act) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total8) return;
   const int cpr = C / 8;
@@ -249,6 +249,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const __bf16* __restrict_
   for (int j = 0; j < 8; ++j) {
     const int c = c0 + j, g = c / (C / GN_GROUPS);
     f[j] = (f[j] - mean[n * GN_GROUPS + g]) * rstd[n * GN_GROUPS + g] * gamma[c] + beta[c];
+    if (act) f[j] = silu(f[j]);
   }
   *reinterpret_cast<s16x8*>(y + i * 8) = pack8(f);
 }
@@ -378,10 +379,10 @@ bool gn_stats(const void* x, float* part, float* mean, float* rstd, int N, int H
 size_t gn_part_floats(int N) { return (size_t)N * GN_CHUNKS * GN_GROUPS * 2; }
 
 void gn_apply(const void* x, const float* mean, const float* rstd, const float* gamma, const float* beta, void* y, int N, int HW,
-              int C, hipStream_t st) {
+              int C, hipStream_t st, int act) {
   const long total8 = (long)N * HW * C / 8;
   hipLaunchKernelGGL(gn_apply_kernel, dim3((total8 + 255) / 256), dim3(256), 0, st, (const __bf16*)x, mean, rstd, gamma, beta,
-                     (__bf16*)y, total8, HW, C);
+                     (__bf16*)y, total8, HW, C, act);
 }
 
 bool conv_out(const void* x, const void* w, const float* bias, const float* mean, const float* rstd, const float* gamma,

@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -36,6 +38,13 @@ def _lin_w(conv: torch.nn.Conv2d) -> torch.Tensor:
 
 def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None else t.detach().float().contiguous()
+
+
+# GroupNorm + SiLU as a separate bf16 pass ahead of the 3x3 conv for images of at least this many pixels (default 0:
+# every GN conv; batch 64 decoder 45.0 -> 42.1 ms, the gain at the low-resolution / high-channel levels, neutral at
+# 256 x 256: profiles/r6_vqgan_conv_out.txt). DALLE_AMD_VQGAN_GN_PREPASS=<pixels> keeps smaller images on the
+# fused-gather form.
+_GN_PREPASS_MIN_HW = int(os.environ.get("DALLE_AMD_VQGAN_GN_PREPASS", "0"))
 
 
 class HipDecoder:
@@ -65,6 +74,10 @@ class HipDecoder:
             return self.C.conv3x3(x, w, b, res, ups=ups)
         gamma, beta, eps = self._cached(id(gn), lambda: self._gn(gn))
         mean, rstd = self.C.gn_stats(x, eps)
+        if x.shape[1] * x.shape[2] >= _GN_PREPASS_MIN_HW:
+            # SiLU(GN(x)) once per element into bf16, then the plain conv: the fused form applies it in the gather,
+            # i.e. 9 times per element (once per tap)
+            return self.C.conv3x3(self.C.gn_apply(x, mean, rstd, gamma, beta, silu=True), w, b, res, ups=ups)
         return self.C.conv3x3(x, w, b, res, mean, rstd, gamma, beta, ups=ups)
 
     def linear(self, x, conv):
@@ -131,4 +144,4 @@ def supported(decoder: Decoder) -> bool:
             continue
         if m.in_channels % 64 or m.out_channels % 128:
             return False
-    return decoder.conv_out.in_channels <= 128 and decoder.conv_out.in_channels % 8 == 0
+    return decoder.conv_out.in_channels <= 128 and decoder.conv_out.in_channels % 32 == 0
