@@ -107,6 +107,15 @@ class BatchingGenerator:
             # this thread's current device = the generator's: streams, hipGraph captures and the native
             # ops' stream lookups must bind to that GPU, not to GPU 0
             torch.cuda.set_device(self.device)
+            # and a (non-blocking) stream of the worker's own: work on the legacy default stream would have to
+            # synchronise with every blocking stream -- including a hipGraph capture running in another
+            # generator's thread on the same GPU, which then fails ("legacy stream depend on a capturing stream")
+            with torch.cuda.stream(torch.cuda.Stream(device=self.device)):
+                self._serve()
+        else:
+            self._serve()
+
+    def _serve(self):
         while True:
             first = self._next(None)
             if first is None:
